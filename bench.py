@@ -1,0 +1,228 @@
+"""Benchmark: mm_s2ut_transformer fp16 training throughput (audio frames / s / node).
+
+One step = one full training update on one max-tokens-40000 batch per rank: GPU fbank front end
+(waveforms already resident in HBM) -> Conv1d subsampler -> 12-layer encoder -> gated image fusion
+-> 6-layer unit decoder -> label-smoothed CE -> hand-written backward with bucketed RCCL all-reduce
+-> FP16Optimizer/Adam.  Synthetic Speech-Multi30K-shaped data, random-init weights.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints ONE JSON line (value = frames processed by all ranks / max-over-ranks wall time).
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+mm = importlib.import_module("multimodal-s2ut_amd")
+from importlib import import_module  # noqa: E402
+
+data = import_module("multimodal-s2ut_amd.data")
+frontend_mod = import_module("multimodal-s2ut_amd.frontend")
+runtime = import_module("multimodal-s2ut_amd.runtime")
+kernels = import_module("multimodal-s2ut_amd.kernels")
+parallel = import_module("multimodal-s2ut_amd.parallel")
+trainer_mod = import_module("multimodal-s2ut_amd.trainer")
+
+MFMA_PEAK_F16 = 2500.0   # TFLOP/s dense fp16 (MI355X_MICROARCH.md chip parameters)
+HBM_PEAK = 8000.0        # GB/s spec
+
+
+def fwd_flops_per_utt(Ts, Tt, cfg, Ti=577, Di=768, fusion=True):
+    """SURVEY.md §8(d) closed form (true lengths), forward FLOPs of one utterance."""
+    d, F, C, V = cfg["encoder_embed_dim"], cfg["encoder_ffn_embed_dim"], cfg["conv_channels"], cfg["vocab_size"]
+    T1 = (Ts - 1) // 2 + 1
+    Te = (T1 - 1) // 2 + 1
+    f = 2 * T1 * (80 * 5 * C) + 2 * Te * (C // 2 * 5 * 2 * d)
+    f += cfg["encoder_layers"] * (Te * (8 * d * d + 4 * d * F) + 4 * Te * Te * d)
+    if fusion:
+        k = 1 if cfg["multimodal_attention_type"] == "multimodal_attention" else 0
+        f += Te * 8 * d * d + 4 * Ti * Di * d + 4 * Te * (Ti + k) * d
+    f += cfg["decoder_layers"] * (Tt * (12 * d * d + 4 * d * F) + 4 * Tt * Tt * d + 4 * Te * d * d + 4 * Tt * Te * d)
+    f += 2 * Tt * d * V
+    return f
+
+
+def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000):
+    """nb length-bucketed batches (fairseq batch_by_size), spread evenly over the length
+    distribution of a synthetic corpus; everything moved to HBM before timing."""
+    corpus = data.SyntheticSpeechMulti30K(n_utts=n_utts, seed=1 + rank, img_tokens=577,
+                                          img_dim=cfg["image_feat_dim"], with_images=cfg["fusion"])
+    all_b = corpus.batches(max_tokens)
+    pick = [all_b[int(i)] for i in np.linspace(0, len(all_b) - 1, nb).round()]
+    out = []
+    for bi, idx in enumerate(pick):
+        items = [corpus.item(i, features=False) for i in idx]
+        rng = np.random.default_rng((rank, bi))
+        waves = []
+        for it in items:
+            n = 160 * it["n_frames"] + 240
+            t = np.arange(n) / 16000.0
+            w = (0.1 * rng.standard_normal(n) + 0.3 * np.sin(2 * np.pi * 440.0 * t)) * 2 ** 15
+            waves.append(w.astype(np.float32))
+            it["source"] = torch.zeros(it["n_frames"], 80)  # placeholder: features come from the GPU fbank
+        wb = frontend.upload(waves)
+        sample = data.collater(items)
+        assert sample["net_input"]["src_lengths"].tolist() == wb["n_frames"].tolist()
+        sample["net_input"]["src_tokens"] = None
+        src_dummy = torch.empty(wb["B"], wb["Tmax"], 80, dtype=torch.float16, device=device)
+        batch = runtime.prepare_batch(sample, cfg, device, src_override=src_dummy)
+        tl = sample["target_lengths"].numpy()
+        sl = sample["net_input"]["src_lengths"].numpy()
+        flops = sum(fwd_flops_per_utt(int(s), int(t), cfg, fusion=cfg["fusion"]) for s, t in zip(sl, tl))
+        out.append((wb, batch, sample, 3 * flops))
+    return out
+
+
+def cpu_baseline(cfg, model, sample, budget_s=20.0):
+    """The oracle (fp32 PyTorch-CPU restatement) timed on the host cores on a bounded sample of the
+    same workload: a few utterances of one batch, full training step (fwd + bwd + Adam)."""
+    from oracle import ref_model as R
+    ocfg = R.no_dropout(dict(cfg))
+    sd = {k: v.detach().float().cpu() for k, v in model.params.p.items()}
+    P = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ni = sample["net_input"]
+    n = 2
+    sub = {"net_input": {"src_tokens": torch.randn(n, int(ni["src_lengths"][0]), 80),
+                         "src_lengths": ni["src_lengths"][:n].clone(),
+                         "prev_output_tokens": ni["prev_output_tokens"][:n],
+                         "imgs_list": [ni["imgs_list"][0][:n].float()] if ni["imgs_list"] else [],
+                         "img_masks_list": [None] if ni["imgs_list"] else []},
+           "target": sample["target"][:n]}
+    frames = int(sub["net_input"]["src_lengths"].sum())
+    states = {k: (torch.zeros_like(v), torch.zeros_like(v)) for k, v in P.items()}
+    masters = {k: v.detach().clone() for k, v in P.items()}
+
+    def step(i):
+        for v in P.values():
+            v.grad = None
+        loss, _, _ = R.model_forward(P, sub, ocfg)
+        loss.backward()
+        names = list(P)
+        R.fp16_optimizer_step([masters[k] for k in names], [P[k].grad.half() for k in names],
+                              [states[k] for k in names], i + 1, 1e-4, 1.0 / frames)
+
+    step(0)
+    t0 = time.time()
+    k = 0
+    while True:
+        step(k + 1)
+        k += 1
+        if time.time() - t0 > budget_s or k >= 20:
+            break
+    dt = time.time() - t0
+    return {"value": frames * k / dt, "unit": "audio-frames/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle fp32 training step (fwd+bwd+FP16Optimizer/Adam), {n} utterances / "
+                      f"{frames} frames of the base config, {k} steps in {dt:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--max-tokens", type=int, default=40000)
+    ap.add_argument("--nbatches", type=int, default=8)
+    ap.add_argument("--audio-only", action="store_true")
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gemm-timing", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    rank, world, local = parallel.init_from_env()
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    cfg = mm.default_cfg(fusion=not args.audio_only)
+    model = mm.MMS2UTModel(cfg, device=device).init_params(seed=1)
+    tr = trainer_mod.Trainer(model, lr=5e-4, world_size=world, bucket_mb=args.bucket_mb)
+    fe = frontend_mod.FbankFrontend(device)
+    batches = make_batches(cfg, rank, args.nbatches, args.max_tokens, device, fe)
+
+    def step(i):
+        wb, batch, _, _ = batches[i % len(batches)]
+        batch.src = fe(wb)
+        tr.train_step(batch)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not args.no_gemm_timing:
+        kernels.GEMM_EVENTS = []
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ev = kernels.GEMM_EVENTS
+    kernels.GEMM_EVENTS = None
+    elapsed = t1 - t0
+    frames = sum(int(batches[(args.warmup + i) % len(batches)][1].n_src_frames) for i in range(args.steps))
+    alg_flops = sum(batches[(args.warmup + i) % len(batches)][3] for i in range(args.steps))
+    gemm_ms = sum(a.elapsed_time(b) for a, b, _ in ev) if ev else 0.0
+    n_launch = len(ev) if ev else 0
+    stats = torch.tensor([elapsed, frames, alg_flops, gemm_ms, n_launch], dtype=torch.float64, device=device)
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0])
+        frames_all = float(sm[1])
+        flops_all, gemm_all, nl_all = float(sm[2]), float(sm[3]), float(sm[4])
+    else:
+        frames_all, flops_all, gemm_all, nl_all = float(frames), float(alg_flops), gemm_ms, float(n_launch)
+    ost = tr.opt.stats()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, model, batches[0][2], args.cpu_budget)
+    if rank == 0:
+        achieved = (flops_all / (gemm_all / 1e3) / 1e12) if gemm_all > 0 else None
+        line = {
+            "metric": "audio-frames/sec/node, mm_s2ut_transformer fp16, max-tokens 40000, 1/2/4/8 GPUs",
+            "value": frames_all / elapsed,
+            "unit": "audio-frames/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp16", "data": "synthetic (Speech-Multi30K-shaped; random-init weights)",
+            "config": {"workload": ("mm_s2ut_transformer base audio-only" if args.audio_only else
+                                    "mm_s2ut_transformer base (ViT-768 image feats, multimodal_attention+gate)"),
+                       "model": "mm_s2ut_transformer", "max_tokens": args.max_tokens,
+                       "global_batch_frames_per_step": frames_all / args.steps,
+                       "parallelism": f"dp{world}", "front_end": "GPU fbank+CMVN in step",
+                       "alg_flops_per_frame": flops_all / max(frames_all, 1)},
+            "roofline": {"bound": "mfma", "kernel": "mms2ut gemm_kernel (all GEMM launches)",
+                         "achieved": achieved, "peak": MFMA_PEAK_F16, "unit": "TFLOP/s",
+                         "frac": (achieved / MFMA_PEAK_F16) if achieved else None, "traffic": None,
+                         "gemm_ms_per_step": gemm_all / world / args.steps,
+                         "gemm_launches_per_step": nl_all / world / args.steps},
+            "cpu_baseline": cpu,
+            "optimizer": ost,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,218 @@
+/*
+ * libmms2ut_hip — C-ABI of the MI355X-native mm_s2ut_transformer training path.
+ *
+ * Every entry point takes raw device pointers, int64 sizes/strides, scalars and the HIP stream to
+ * enqueue on (PyTorch's current stream).  The library never allocates or frees: all buffers,
+ * including workspaces, belong to the caller (PyTorch's caching allocator).  Functions return 0 on
+ * success and non-zero on error; mms2ut_last_error() returns the message (thread-local).  The
+ * library is stateless and re-entrant; kernels are only ever enqueued on the passed stream.
+ *
+ * Each entry cites the reference interface (or the fairseq/PyTorch op it executes for the
+ * reference) that it replaces — see SURVEY.md §8(a)/(b) and INTEGRATION.md.
+ */
+#ifndef MMS2UT_H
+#define MMS2UT_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef _Float16 mms2ut_half;
+
+/* ---------------------------------------------------------------- errors / introspection */
+const char* mms2ut_last_error(void);
+int mms2ut_version(void);
+
+/* ---------------------------------------------------------------- GEMM (MFMA fp16, fp32 acc)
+ * Replaces every nn.Linear / bmm / conv-as-GEMM the reference executes through cuBLAS:
+ * fairseq MultiheadAttention q/k/v/out_proj, TransformerEncoderLayer/DecoderLayer fc1/fc2,
+ * Conv1dSubsampler convs (im2col), fusion projections (fuse.py:76-78,116; nn.MultiheadAttention
+ * in_proj/out_proj for fuse.py:161), the gate dense (mm_s2s_transformer.py:613-614) and the tied
+ * output projection — forward, dgrad and wgrad.
+ *   C[m][n] = epi(alpha * sum_k A(m,k) B(n,k))
+ *   A(m,k) = a_kcontig ? A[m*lda+k] : A[k*lda+m];  B(n,k) = b_kcontig ? B[n*ldb+k] : B[k*ldb+n]
+ *   batch z in [0,batch): z1 = z / bdiv, z2 = z % bdiv; X += z1*sX1 + z2*sX2 (elements)
+ *   split-K (epi = MMS_EPI_F32 only): slab s written at C + s*sCsplit (fp32)            */
+enum {
+  MMS_EPI_F16 = 0,          /* C = alpha*acc (+bias)                                      */
+  MMS_EPI_RELU_DROP = 1,    /* C = dropout(relu(alpha*acc + bias))        (fc1)           */
+  MMS_EPI_DROP_RESID = 2,   /* C = aux + dropout(alpha*acc + bias)        (out_proj, fc2) */
+  MMS_EPI_F32 = 3,          /* C(fp32) = alpha*acc                        (split-K slabs) */
+  MMS_EPI_GATE = 4,         /* g = sigmoid(acc+bias); C = t + g*(o-t); out2 = g; o = aux[:, :N], t = aux[:, N:2N] */
+  MMS_EPI_RELU_DROP_BWD = 5,/* C = aux>0 ? alpha*acc/(1-p) : 0            (fc2 dgrad -> fc1 pre-act) */
+  MMS_EPI_F16_ACC = 6       /* C += alpha*acc                                               */
+};
+
+typedef struct mms2ut_gemm_args {
+  const mms2ut_half* A;
+  const mms2ut_half* B;
+  void* C;
+  int M, N, K;
+  int a_kcontig, b_kcontig;
+  int64_t lda, ldb, ldc;
+  int batch, bdiv;
+  int64_t sA1, sA2, sB1, sB2, sC1, sC2;
+  int splitk;
+  int64_t sCsplit;
+  int epi;
+  float alpha;
+  const mms2ut_half* bias;
+  const mms2ut_half* aux;
+  int64_t ldaux, sX1, sX2;
+  mms2ut_half* out2;
+  int64_t ldo2;
+  float dropout_p;
+  uint64_t seed, offset;
+  int64_t ld_rng;
+} mms2ut_gemm_args;
+
+int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
+
+/* sum `nsplit` fp32 slabs [rows, cols] (slab stride `slab`) * alpha -> out, row stride ldo.
+ * mode bit0: fp16 output (else fp32); bit1: accumulate into out (else overwrite)            */
+int mms2ut_splitk_reduce(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                         void* out, int64_t ldo, int mode, float alpha, hipStream_t stream);
+
+/* ---------------------------------------------------------------- LayerNorm (eps, affine)
+ * Replaces fairseq LayerNorm (self_attn_layer_norm / final_layer_norm / encoder_attn_layer_norm /
+ * encoder.layer_norm / decoder.layer_norm) and nn.LayerNorm image_pre_norm_module
+ * (mm_s2s_transformer.py:188-190,595).  Rows of D fp16, statistics fp32.                  */
+int mms2ut_layernorm_fwd(const mms2ut_half* x, const mms2ut_half* gamma, const mms2ut_half* beta,
+                         mms2ut_half* y, float* mean, float* rstd, int64_t rows, int D, float eps,
+                         hipStream_t stream);
+/* dx = LN'(dy) (+ dres if non-null); partial dgamma/dbeta sums -> part[nblk][2][D] (fp32)  */
+int mms2ut_layernorm_bwd(const mms2ut_half* dy, const mms2ut_half* x, const mms2ut_half* gamma,
+                         const float* mean, const float* rstd, const mms2ut_half* dres,
+                         mms2ut_half* dx, float* part, int64_t rows, int D, hipStream_t stream);
+int mms2ut_layernorm_bwd_parts(int64_t rows);
+/* column sums of fp32 partials [nparts][ncol] -> out (fp16), out += if accumulate */
+int mms2ut_colsum_parts(const float* part, int nparts, int ncol, mms2ut_half* out, int accumulate,
+                        hipStream_t stream);
+/* column sums of an fp16 matrix [rows][cols] (row stride ld) -> part[nparts][cols] fp32 (bias grads) */
+int mms2ut_colsum_f16(const mms2ut_half* x, int64_t rows, int cols, int64_t ld, float* part,
+                      int nparts, hipStream_t stream);
+int mms2ut_colsum_nparts(int64_t rows);
+
+/* ---------------------------------------------------------------- attention softmax
+ * Masked softmax over attention scores S[z][Tq][ldS] (fp16) with per-batch key lengths
+ * (key padding mask, fairseq/torch MHA key_padding_mask), optional causal mask
+ * (buffered_future_mask), optional "always-valid" trailing key (add_bias_kv column of
+ * nn.MultiheadAttention, fuse.py:161), and attention-prob dropout (p, counter RNG).
+ * Keys may instead be masked by key_mask[b*ld_mask + j] != 0 (bool key_padding_mask).
+ * Writes P (undropped) and Pd (dropped, may alias P when p == 0).  z = b*H + h.            */
+int mms2ut_attn_softmax_fwd(const mms2ut_half* S, mms2ut_half* P, mms2ut_half* Pd, int Z, int H,
+                            int Tq, int Tk, int64_t ldS, const int32_t* key_len,
+                            const uint8_t* key_mask, int64_t ld_mask, int causal,
+                            int extra_key, float p, uint64_t seed, uint64_t offset,
+                            hipStream_t stream);
+/* dS = P * (dPd*mask/(1-p) - sum_j Pd_j dPd_j) ; dP may alias dS                            */
+int mms2ut_attn_softmax_bwd(const mms2ut_half* P, const mms2ut_half* dPd, mms2ut_half* dS, int Z,
+                            int H, int Tq, int Tk, int64_t ldS, const int32_t* key_len, int causal,
+                            int extra_key, float p, uint64_t seed, uint64_t offset,
+                            hipStream_t stream);
+
+/* ---------------------------------------------------------------- elementwise / embedding */
+/* y = dropout(x) elementwise (n elements, counter offset) ; y may alias x                   */
+int mms2ut_dropout_fwd(const mms2ut_half* x, mms2ut_half* y, int64_t n, float p, uint64_t seed,
+                       uint64_t offset, hipStream_t stream);
+/* materialise the keep-mask (uint8) the kernels use — for parity tests / debugging          */
+int mms2ut_dropout_mask(uint8_t* keep, int64_t n, float p, uint64_t seed, uint64_t offset,
+                        hipStream_t stream);
+/* encoder input: x[b,t,:] = dropout(scale*h[b,t,:] + pos[t+2 if t<len[b] else 1, :])
+ * (fairseq S2TTransformerEncoder._forward: embed_scale, SinusoidalPositionalEmbedding(pad mask)) */
+int mms2ut_encoder_embed_fwd(const mms2ut_half* h, const mms2ut_half* pos_table, const int32_t* len,
+                             mms2ut_half* x, int B, int T, int D, float scale, float p,
+                             uint64_t seed, uint64_t offset, hipStream_t stream);
+/* backward of the above w.r.t. h: dh = scale * dropout_mask * dx                             */
+int mms2ut_scale_dropout_bwd(const mms2ut_half* dx, mms2ut_half* dh, int64_t n, float scale,
+                             float p, uint64_t seed, uint64_t offset, hipStream_t stream);
+/* decoder input (fairseq TransformerDecoder.extract_features, StackedEmbedding n=1):
+ * x = dropout(scale*E[tok] + pos[make_positions(tok)])                                      */
+int mms2ut_token_embed_fwd(const int64_t* tok, const mms2ut_half* E, const mms2ut_half* pos_table,
+                           mms2ut_half* x, int B, int T, int D, int pad_idx, float scale, float p,
+                           uint64_t seed, uint64_t offset, hipStream_t stream);
+/* dE[tok] += scale*mask*dx (fp32 accumulation buffer dE32 [V][D]; pad rows skipped)          */
+int mms2ut_token_embed_bwd(const int64_t* tok, const mms2ut_half* dx, float* dE32, int B, int T,
+                           int D, int pad_idx, float scale, float p, uint64_t seed,
+                           uint64_t offset, hipStream_t stream);
+/* out(fp16) = a(fp16) + b32(fp32) elementwise                                                */
+int mms2ut_add_f32_to_f16(const mms2ut_half* a, const float* b, mms2ut_half* out, int64_t n,
+                          hipStream_t stream);
+/* GLU over the channel (last) dim: y[r, c] = x[r, c] * sigmoid(x[r, c + C]), x row stride 2C */
+int mms2ut_glu_fwd(const mms2ut_half* x, mms2ut_half* y, int64_t rows, int C, hipStream_t stream);
+int mms2ut_glu_bwd(const mms2ut_half* x, const mms2ut_half* dy, mms2ut_half* dx, int64_t rows,
+                   int C, hipStream_t stream);
+/* Conv1d (stride 2, pad k/2) as implicit GEMM: im2col of x[B][Tin][C] -> col[B*Tout][C*k]
+ * ordered (c, k) to match the PyTorch weight [out][C][k] (fairseq Conv1dSubsampler)          */
+int mms2ut_im2col(const mms2ut_half* x, mms2ut_half* col, int B, int Tin, int Tout, int C, int k,
+                  int stride, int pad, hipStream_t stream);
+int mms2ut_col2im(const mms2ut_half* dcol, mms2ut_half* dx, int B, int Tin, int Tout, int C, int k,
+                  int stride, int pad, hipStream_t stream);
+/* fusion gate backward (mm_s2s_transformer.py:613-618):
+ * dpre = dres*(o-t)*g*(1-g); dmerge_direct = [dres*g, dres*(1-g)]                            */
+int mms2ut_gate_bwd(const mms2ut_half* dres, const mms2ut_half* merge, const mms2ut_half* g,
+                    mms2ut_half* dpre, mms2ut_half* dmerge, int64_t rows, int D,
+                    hipStream_t stream);
+/* copy rows with strides (cols fp16 elements)                                               */
+int mms2ut_copy2d(const mms2ut_half* src, int64_t lds, mms2ut_half* dst, int64_t ldd, int64_t rows,
+                  int cols, hipStream_t stream);
+/* out = a + b (fp16) */
+int mms2ut_add_f16(const mms2ut_half* a, const mms2ut_half* b, mms2ut_half* out, int64_t n,
+                   hipStream_t stream);
+
+/* ---------------------------------------------------------------- label-smoothed CE
+ * fairseq speech_to_unit -> LabelSmoothedCrossEntropyCriterion.compute_loss (reference copy
+ * criterions/speech_to_speech_criterion.py:58-102): fp32 log_softmax over V, eps-smoothing,
+ * pad targets ignored, reduce=sum.  loss_out[2] = {loss, nll} (fp32, accumulated atomically;
+ * zero it first).  lse[rows] saved for the backward.                                        */
+int mms2ut_ls_xent_fwd(const mms2ut_half* logits, int64_t ld, const int64_t* target, int64_t rows,
+                       int V, float eps, int pad_idx, float* lse, float* loss_out,
+                       hipStream_t stream);
+/* dlogits = grad * ((1-eps-eps_i)(p - onehot) + eps_i(V p - 1)), 0 on pad rows; in place OK */
+int mms2ut_ls_xent_bwd(const mms2ut_half* logits, int64_t ld, const int64_t* target, int64_t rows,
+                       int V, float eps, int pad_idx, const float* lse, const float* grad,
+                       mms2ut_half* dlogits, hipStream_t stream);
+
+/* ---------------------------------------------------------------- FP16Optimizer + Adam
+ * fairseq FP16Optimizer (fp32 master, dynamic loss scale) + clip_grad_norm_ + Adam (fairseq
+ * optim/adam.py) + DynamicLossScaler, entirely device-side (no host sync per step).
+ * `ost` is a device fp32 state vector (indices MMS_OST_*), initialised by the host once
+ * (loss_scale = --fp16-init-scale, iter = 0, last_overflow = -1, step = 0).
+ *   grad_sqnorm -> grad_norm_finalize (mult = 1/(loss_scale*sample_size), norm, overflow)
+ *   -> optim_prepare (Adam step/step size, clip coef, scaler update) -> adam (skips on overflow) */
+enum {
+  MMS_OST_MULT = 0, MMS_OST_GNORM = 1, MMS_OST_OVERFLOW = 2, MMS_OST_STEP = 3,
+  MMS_OST_STEP_SIZE = 4, MMS_OST_LOSS_SCALE = 5, MMS_OST_ITER = 6, MMS_OST_LAST_OVERFLOW = 7,
+  MMS_OST_LAST_RESCALE = 8, MMS_OST_CLIP_COEF = 9, MMS_OST_FATAL = 10, MMS_OST_SIZE = 16
+};
+int mms2ut_grad_sqnorm(const mms2ut_half* grad, int64_t n, float* part, int nparts,
+                       hipStream_t stream);
+int mms2ut_grad_norm_finalize(const float* part, int nparts, float* ost, const float* sample_size,
+                              hipStream_t stream);
+int mms2ut_optim_prepare(float* ost, float lr, float beta1, float beta2, float clip_norm,
+                         float scale_window, float min_loss_scale, hipStream_t stream);
+int mms2ut_adam_fp16_master(mms2ut_half* param, const mms2ut_half* grad, float* master,
+                            float* exp_avg, float* exp_avg_sq, int64_t n, const float* ost,
+                            float lr, float beta1, float beta2, float eps, float weight_decay,
+                            hipStream_t stream);
+
+/* ---------------------------------------------------------------- fbank front end
+ * fairseq get_fbank -> torchaudio.compliance.kaldi.fbank (audio_utils.py:326-349), 80 bins,
+ * 25 ms / 10 ms, snip_edges, DC removal, pre-emphasis 0.97, povey window, 512-pt FFT, power,
+ * mel (mel_banks: [nbins][257] fp32 dense table), log(max(x, FLT_EPS)); then utterance CMVN
+ * (data-config feature transform) and zero-padded fp16 collation [B][Tmax][nbins]
+ * (_collate_frames).  wave: concatenated fp32 samples (x 2^15), wave_off[B+1].              */
+int mms2ut_fbank_frames(const int64_t* wave_off, int B, int32_t* n_frames_out, hipStream_t stream);
+int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, const int32_t* frame_off, int B,
+                     int total_frames, const float* mel_banks, int nbins, float* feats,
+                     hipStream_t stream);
+int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
+                              int nbins, int cmvn, mms2ut_half* out, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMS2UT_H */

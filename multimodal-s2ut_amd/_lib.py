@@ -1,0 +1,107 @@
+"""ctypes binding of libmms2ut_hip.so (the C-ABI declared in include/mms2ut.h).
+
+The product path has no CPU fallback: if the library is missing or a call fails, this raises.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmms2ut_hip.so")
+
+vp, i32, i64, u64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_float
+
+EPI_F16, EPI_RELU_DROP, EPI_DROP_RESID, EPI_F32, EPI_GATE, EPI_RELU_DROP_BWD, EPI_F16_ACC = range(7)
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [
+        ("A", vp), ("B", vp), ("C", vp),
+        ("M", i32), ("N", i32), ("K", i32),
+        ("a_kcontig", i32), ("b_kcontig", i32),
+        ("lda", i64), ("ldb", i64), ("ldc", i64),
+        ("batch", i32), ("bdiv", i32),
+        ("sA1", i64), ("sA2", i64), ("sB1", i64), ("sB2", i64), ("sC1", i64), ("sC2", i64),
+        ("splitk", i32),
+        ("sCsplit", i64),
+        ("epi", i32),
+        ("alpha", f32),
+        ("bias", vp), ("aux", vp),
+        ("ldaux", i64), ("sX1", i64), ("sX2", i64),
+        ("out2", vp),
+        ("ldo2", i64),
+        ("dropout_p", f32),
+        ("seed", u64), ("offset", u64),
+        ("ld_rng", i64),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/mms2ut.h declares
+SIGNATURES = {
+    "mms2ut_last_error": (C.c_char_p, []),
+    "mms2ut_version": (i32, []),
+    "mms2ut_gemm_f16": (i32, [C.POINTER(GemmArgs), vp]),
+    "mms2ut_splitk_reduce": (i32, [vp, i32, i64, i32, i32, vp, i64, i32, f32, vp]),
+    "mms2ut_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
+    "mms2ut_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),
+    "mms2ut_layernorm_bwd_parts": (i32, [i64]),
+    "mms2ut_colsum_parts": (i32, [vp, i32, i32, vp, i32, vp]),
+    "mms2ut_colsum_f16": (i32, [vp, i64, i32, i64, vp, i32, vp]),
+    "mms2ut_colsum_nparts": (i32, [i64]),
+    "mms2ut_attn_softmax_fwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i64, vp, vp, i64, i32, i32,
+                                      f32, u64, u64, vp]),
+    "mms2ut_attn_softmax_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i64, vp, i32, i32, f32, u64,
+                                      u64, vp]),
+    "mms2ut_dropout_fwd": (i32, [vp, vp, i64, f32, u64, u64, vp]),
+    "mms2ut_dropout_mask": (i32, [vp, i64, f32, u64, u64, vp]),
+    "mms2ut_encoder_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, u64, vp]),
+    "mms2ut_scale_dropout_bwd": (i32, [vp, vp, i64, f32, f32, u64, u64, vp]),
+    "mms2ut_token_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, u64, u64, vp]),
+    "mms2ut_token_embed_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, f32, u64, u64, vp]),
+    "mms2ut_add_f32_to_f16": (i32, [vp, vp, vp, i64, vp]),
+    "mms2ut_add_f16": (i32, [vp, vp, vp, i64, vp]),
+    "mms2ut_glu_fwd": (i32, [vp, vp, i64, i32, vp]),
+    "mms2ut_glu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
+    "mms2ut_im2col": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "mms2ut_col2im": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "mms2ut_gate_bwd": (i32, [vp, vp, vp, vp, vp, i64, i32, vp]),
+    "mms2ut_copy2d": (i32, [vp, i64, vp, i64, i64, i32, vp]),
+    "mms2ut_ls_xent_fwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp]),
+    "mms2ut_ls_xent_bwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp]),
+    "mms2ut_grad_sqnorm": (i32, [vp, i64, vp, i32, vp]),
+    "mms2ut_grad_norm_finalize": (i32, [vp, i32, vp, vp, vp]),
+    "mms2ut_optim_prepare": (i32, [vp, f32, f32, f32, f32, f32, f32, vp]),
+    "mms2ut_adam_fp16_master": (i32, [vp, vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, f32, vp]),
+    "mms2ut_fbank_frames": (i32, [vp, i32, vp, vp]),
+    "mms2ut_fbank_f32": (i32, [vp, vp, vp, i32, i32, vp, i32, vp, vp]),
+    "mms2ut_fbank_cmvn_collate": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+}
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (raises if it was not built — there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipError(f"libmms2ut_hip.so not found at {LIB_PATH}; run "
+                       f"`python multimodal-s2ut_amd/build.py` (hipcc, gfx950)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise HipError(f"{name} failed ({rc}): {_lib.mms2ut_last_error().decode()}")
+    return rc

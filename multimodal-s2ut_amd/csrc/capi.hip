@@ -1,0 +1,67 @@
+// Error plumbing + split-K reduction.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+#include "../../include/mms2ut.h"
+
+namespace mms {
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}
+}  // namespace mms
+
+extern "C" const char* mms2ut_last_error(void) { return mms::g_err; }
+extern "C" int mms2ut_version(void) { return 1; }
+
+namespace {
+__global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int nsplit, long slab,
+                                     int rows, int cols, void* out, long ldo, int out_f16,
+                                     float alpha) {
+  const long n4 = (long)rows * (cols / 4);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / (cols / 4), c = (i % (cols / 4)) * 4;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nsplit; ++k)
+      s += *reinterpret_cast<const f32x4*>(slabs + k * slab + r * cols + c);
+    s *= alpha;
+    // mode bit0: fp16 output (else fp32); bit1: accumulate into the output
+    if (out_f16 & 1) {
+      h16x4* o = reinterpret_cast<h16x4*>(reinterpret_cast<h16*>(out) + r * ldo + c);
+      if (out_f16 & 2) { h16x4 p = *o; s += f32x4{(float)p[0], (float)p[1], (float)p[2], (float)p[3]}; }
+      *o = h16x4{(h16)s[0], (h16)s[1], (h16)s[2], (h16)s[3]};
+    } else {
+      f32x4* o = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + r * ldo + c);
+      if (out_f16 & 2) s += *o;
+      *o = s;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int mms2ut_splitk_reduce(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                                    void* out, int64_t ldo, int out_f16, float alpha,
+                                    hipStream_t stream) {
+  MMS_REQUIRE(cols % 4 == 0 && ldo % 4 == 0, "splitk_reduce: cols/ldo must be multiples of 4");
+  const long n4 = (long)rows * (cols / 4);
+  if (n4 == 0) return 0;
+  int grid = (int)((n4 + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, stream, slabs, nsplit, slab,
+                     rows, cols, out, ldo, out_f16, alpha);
+  return mms::check_launch("splitk_reduce");
+}

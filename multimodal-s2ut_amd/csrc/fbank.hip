@@ -1,0 +1,188 @@
+// Kaldi-compatible 80-bin log-mel filterbank (torchaudio.compliance.kaldi.fbank defaults, the
+// path the reference's get_fbank takes: mm_s2ut/data/audio_utils.py:326-349) + utterance CMVN +
+// zero-padded fp16 collation.  One wave per 25 ms frame: DC removal and pre-emphasis through
+// LDS, povey window, 512-point radix-2 complex FFT in LDS (twiddles from a table), power
+// spectrum, sparse triangular mel filters, log(max(x, FLT_EPSILON)).  HBM-bound: 640 B of wave
+// read (400 samples, hop 160 -> 4 B/sample amortised) + 320 B of features written per frame.
+#include "common.h"
+#include "../../include/mms2ut.h"
+
+namespace {
+
+constexpr int WIN = 400, SHIFT = 160, NFFT = 512, NBIN = 257;
+
+struct FbankConst {
+  float window[WIN];
+  float tw_re[NFFT / 2], tw_im[NFFT / 2];
+};
+
+__constant__ FbankConst c_fb;
+static bool g_fb_init = false;
+
+MMS_DEV int bitrev9(int x) { return (int)(__builtin_bitreverse32((unsigned)x) >> 23); }
+
+__global__ void __launch_bounds__(256) fbank_kernel(const float* __restrict__ wave, const int64_t* __restrict__ wave_off,
+                                                    const int* __restrict__ frame_off, int B, int total,
+                                                    const float* __restrict__ banks, int nbins,
+                                                    float* __restrict__ feats) {
+  __shared__ float s_re[4][NFFT], s_im[4][NFFT], s_x[4][WIN + 4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int f = blockIdx.x * 4 + w;
+  if (f >= total) return;
+  // utterance of this frame (binary search over frame_off)
+  int lo = 0, hi = B;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (frame_off[mid] <= f) lo = mid; else hi = mid;
+  }
+  const int b = lo;
+  const int t = f - frame_off[b];
+  const float* src = wave + wave_off[b] + (long)t * SHIFT;
+  float* X = s_x[w];
+  float* re = s_re[w];
+  float* im = s_im[w];
+  float sum = 0.f;
+  for (int j = lane; j < WIN; j += 64) { const float v = src[j]; X[j] = v; sum += v; }
+  const float mean = wave_sum(sum) / WIN;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // pre-emphasis (replicate-pad at j=0), window, scatter into bit-reversed order
+  for (int j = lane; j < NFFT; j += 64) {
+    float v = 0.f;
+    if (j < WIN) {
+      const float xj = X[j] - mean;
+      const float xp = (j > 0 ? X[j - 1] : X[0]) - mean;
+      v = (xj - 0.97f * xp) * c_fb.window[j];
+    }
+    const int r = bitrev9(j);
+    re[r] = v;
+    im[r] = 0.f;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // iterative radix-2 DIT, 9 stages, 256 butterflies per stage (4 per lane)
+  for (int s = 1; s <= 9; ++s) {
+    const int half = 1 << (s - 1);
+    const int tstride = NFFT >> s;  // twiddle index stride
+    float ar[4], ai[4], br[4], bi[4];
+    int i0s[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int bfly = lane + q * 64;
+      const int grp = bfly >> (s - 1), k = bfly & (half - 1);
+      const int i0 = grp * (half << 1) + k;
+      i0s[q] = i0;
+      const float wr = c_fb.tw_re[k * tstride], wi = c_fb.tw_im[k * tstride];
+      const float xr = re[i0 + half], xi = im[i0 + half];
+      const float tr = wr * xr - wi * xi, ti = wr * xi + wi * xr;
+      const float ur = re[i0], ui = im[i0];
+      ar[q] = ur + tr; ai[q] = ui + ti; br[q] = ur - tr; bi[q] = ui - ti;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      re[i0s[q]] = ar[q]; im[i0s[q]] = ai[q];
+      re[i0s[q] + half] = br[q]; im[i0s[q] + half] = bi[q];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  // power spectrum into X (reuse), bins 0..256
+  for (int k = lane; k < NBIN; k += 64) X[k] = re[k] * re[k] + im[k] * im[k];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const float flt_eps = 1.1920928955078125e-07f;
+  for (int m = lane; m < nbins; m += 64) {
+    const float* bk = banks + (long)m * NBIN;
+    float acc = 0.f;
+    for (int k = 0; k < NBIN; ++k) {
+      const float wgt = bk[k];
+      if (wgt != 0.f) acc += wgt * X[k];
+    }
+    feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
+  }
+}
+
+__global__ void fbank_frames_kernel(const int64_t* wave_off, int B, int* n_frames) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long n = wave_off[b + 1] - wave_off[b];
+  n_frames[b] = n < WIN ? 0 : (int)(1 + (n - WIN) / SHIFT);
+}
+
+__global__ void cmvn_collate_kernel(const float* __restrict__ feats, const int* __restrict__ frame_off,
+                                    int B, int Tmax, int nbins, int cmvn, h16* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int f0 = frame_off[b], T = frame_off[b + 1] - f0;
+  __shared__ float s_mean[256], s_inv[256];
+  for (int c = threadIdx.x; c < nbins; c += blockDim.x) {
+    double sm = 0.0, sq = 0.0;
+    for (int t = 0; t < T; ++t) {
+      const double v = feats[(long)(f0 + t) * nbins + c];
+      sm += v; sq += v * v;
+    }
+    const double mean = T > 0 ? sm / T : 0.0;
+    const double var = T > 0 ? sq / T - mean * mean : 1.0;
+    s_mean[c] = cmvn ? (float)mean : 0.f;
+    s_inv[c] = cmvn ? (float)(1.0 / sqrt(var > 1e-10 ? var : 1e-10)) : 1.f;
+  }
+  __syncthreads();
+  const long n = (long)Tmax * nbins;
+  for (long i = threadIdx.x; i < n; i += blockDim.x) {
+    const int t = (int)(i / nbins), c = (int)(i % nbins);
+    float v = 0.f;
+    if (t < T) v = (feats[(long)(f0 + t) * nbins + c] - s_mean[c]) * s_inv[c];
+    out[(long)b * n + i] = (h16)v;
+  }
+}
+
+int init_consts(hipStream_t s) {
+  if (g_fb_init) return 0;
+  FbankConst h;
+  for (int i = 0; i < WIN; ++i) {
+    const double hann = 0.5 - 0.5 * cos(2.0 * M_PI * i / (WIN - 1));
+    h.window[i] = (float)pow(hann, 0.85);
+  }
+  for (int k = 0; k < NFFT / 2; ++k) {
+    h.tw_re[k] = (float)cos(-2.0 * M_PI * k / NFFT);
+    h.tw_im[k] = (float)sin(-2.0 * M_PI * k / NFFT);
+  }
+  if (hipMemcpyToSymbolAsync(HIP_SYMBOL(c_fb), &h, sizeof(h), 0, hipMemcpyHostToDevice, s) != hipSuccess) {
+    mms::set_error("fbank: constant upload failed");
+    return 1;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) {
+    mms::set_error("fbank: constant upload sync failed");
+    return 1;
+  }
+  g_fb_init = true;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int mms2ut_fbank_frames(const int64_t* wave_off, int B, int32_t* n_frames_out, hipStream_t s) {
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(fbank_frames_kernel, dim3((B + 255) / 256), dim3(256), 0, s, wave_off, B, n_frames_out);
+  return mms::check_launch("fbank_frames");
+}
+
+extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, const int32_t* frame_off, int B,
+                                int total_frames, const float* mel_banks, int nbins, float* feats,
+                                hipStream_t s) {
+  MMS_REQUIRE(nbins > 0 && nbins <= 256, "fbank: nbins must be in (0, 256]");
+  if (init_consts(s)) return 1;
+  if (total_frames == 0) return 0;
+  hipLaunchKernelGGL(fbank_kernel, dim3((total_frames + 3) / 4), dim3(256), 0, s, wave, wave_off, frame_off, B,
+                     total_frames, mel_banks, nbins, feats);
+  return mms::check_launch("fbank");
+}
+
+extern "C" int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
+                                         int nbins, int cmvn, h16* out, hipStream_t s) {
+  MMS_REQUIRE(nbins <= 256, "cmvn: nbins must be <= 256");
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(cmvn_collate_kernel, dim3(B), dim3(256), 0, s, feats, frame_off, B, Tmax, nbins, cmvn, out);
+  return mms::check_launch("fbank_cmvn_collate");
+}

@@ -1,0 +1,326 @@
+// MFMA fp16 GEMM for gfx950 with fused epilogues.
+//
+//   C[m][n] = epilogue( alpha * sum_k A(m,k) * B(n,k) )
+//   A(m,k) = A_KC ? A[m*lda + k] : A[k*lda + m]      (K-contiguous or M-contiguous)
+//   B(n,k) = B_KC ? B[n*ldb + k] : B[k*ldb + n]      (K-contiguous or N-contiguous)
+//
+// One kernel covers every GEMM of the training step: forward projections (NT), dgrad (NN) and
+// wgrad (TN), batched attention products (two-level batch strides), split-K for the skinny
+// wgrad shapes.  Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 tiles of
+// v_mfma_f32_16x16x32_f16.  Operands are register-staged into a double-buffered LDS image:
+//   * K-contiguous tile  -> [128 rows][64 k], 16-B chunks XOR-swizzled by (row & 7), read with
+//     ds_read_b128 (conflict-free per 16-lane group);
+//   * MN-contiguous tile -> [64 k][128 rows], 16-B chunks XOR-swizzled by h(k)<<1, read with the
+//     gfx950 transpose read ds_read_b64_tr_b16 (two per fragment), conflict-free per half-wave.
+// The MFMA is issued with (B,A) swapped so each lane owns 4 consecutive output columns -> 8-B
+// vector stores and 4-wide epilogue math.
+#include "common.h"
+#include "../../include/mms2ut.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;  // 16 KiB per operand per stage
+
+struct GemmP {
+  const h16* A; const h16* B; void* C;
+  int M, N, K;
+  long lda, ldb, ldc;
+  int bdiv;  // batch index z -> (z / bdiv, z % bdiv)
+  long sA1, sA2, sB1, sB2, sC1, sC2;
+  int splitk; int kchunk; long sCsplit;
+  // epilogue
+  float alpha;
+  const h16* bias;
+  const h16* aux; long ldaux; long sX1, sX2;
+  h16* out2; long ldo2;
+  float p; uint32_t thresh; uint64_t seed, offset; long ld_rng;
+};
+
+MMS_DEV int swz_mn(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+
+template <bool KC>
+MMS_DEV void load_tile(const h16* __restrict__ X, long ld, int rows_total, int kdim,
+                       int row0, int k0, int kend, s16x8 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = t + i * NT;
+    s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (KC) {
+      const int row = id >> 3, c = id & 7;
+      const int gr = row0 + row, gk = k0 + c * 8;
+      if (gr < rows_total) {
+        const h16* src = X + (long)gr * ld + gk;
+        if (gk + 8 <= kend) {
+          v = *reinterpret_cast<const s16x8*>(src);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (gk + e < kend) v[e] = reinterpret_cast<const short*>(src)[e];
+        }
+      }
+    } else {
+      const int kr = id >> 4, c = id & 15;
+      const int gk = k0 + kr, gr = row0 + c * 8;
+      if (gk < kend) {
+        const h16* src = X + (long)gk * ld + gr;
+        if (gr + 8 <= rows_total) {
+          v = *reinterpret_cast<const s16x8*>(src);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (gr + e < rows_total) v[e] = reinterpret_cast<const short*>(src)[e];
+        }
+      }
+    }
+    r[i] = v;
+  }
+  (void)kdim;
+}
+
+template <bool KC>
+MMS_DEV void store_tile(char* lds, const s16x8 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = t + i * NT;
+    int off;
+    if (KC) {
+      const int row = id >> 3, c = id & 7;
+      off = row * 128 + ((c ^ (row & 7)) << 4);
+    } else {
+      const int kr = id >> 4, c = id & 15;
+      off = kr * 256 + ((c ^ swz_mn(kr)) << 4);
+    }
+    *reinterpret_cast<s16x8*>(lds + off) = r[i];
+  }
+}
+
+// fragment for rows [sub, sub+16) and k in [kk*32, kk*32+32): lane l holds X(sub + (l&15), kk*32 + 8(l>>4) + j)
+template <bool KC>
+MMS_DEV h16x8 read_frag(const char* lds, int sub, int kk, int lane) {
+  if (KC) {
+    const int r = sub + (lane & 15);
+    const int c = kk * 4 + (lane >> 4);
+    s16x8 v = *reinterpret_cast<const s16x8*>(lds + r * 128 + ((c ^ (r & 7)) << 4));
+    return __builtin_bit_cast(h16x8, v);
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int col = sub + 4 * p;                // element column (row of the logical operand)
+    const int chunk = col >> 3, inb = (col & 7) * 2;
+    const int k1 = kk * 32 + 8 * g + q, k2 = k1 + 4;
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const char* a1 = lds + k1 * 256 + ((chunk ^ swz_mn(k1)) << 4) + inb;
+    const char* a2 = lds + k2 * 256 + ((chunk ^ swz_mn(k2)) << 4) + inb;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a2));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(h16x8, v);
+  }
+}
+
+MMS_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <int EPI>
+MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, int n, f32x4 v) {
+  if (m >= P.M) return;
+  const int N = P.N;
+  float x[4] = {v[0] * P.alpha, v[1] * P.alpha, v[2] * P.alpha, v[3] * P.alpha};
+  if (EPI == MMS_EPI_F32) {
+    float* C = reinterpret_cast<float*>(Cz) + (long)m * P.ldc;
+    if (n + 3 < N) {
+      *reinterpret_cast<f32x4*>(C + n) = f32x4{x[0], x[1], x[2], x[3]};
+    } else {
+      for (int r = 0; r < 4; ++r) if (n + r < N) C[n + r] = x[r];
+    }
+    return;
+  }
+  if (P.bias && EPI != MMS_EPI_RELU_DROP_BWD) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) if (n + r < N) x[r] += (float)P.bias[n + r];
+  }
+  h16* C = reinterpret_cast<h16*>(Cz) + (long)m * P.ldc;
+  float o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float y = x[r];
+    const int nn = n + r;
+    if (EPI == MMS_EPI_RELU_DROP) {
+      y = fmaxf(y, 0.f);
+      if (P.thresh) {
+        const bool keep = mms_keep(P.seed, P.offset + (uint64_t)m * P.ld_rng + nn, P.thresh);
+        y = keep ? y * (1.f / (1.f - P.p)) : 0.f;
+      }
+    } else if (EPI == MMS_EPI_DROP_RESID) {
+      if (P.thresh) {
+        const bool keep = mms_keep(P.seed, P.offset + (uint64_t)m * P.ld_rng + nn, P.thresh);
+        y = keep ? y * (1.f / (1.f - P.p)) : 0.f;
+      }
+      if (nn < N) y += (float)auxz[(long)m * P.ldaux + nn];
+    } else if (EPI == MMS_EPI_GATE) {
+      if (nn < N) {
+        const float g = sigmoidf_(y);
+        const float ov = (float)auxz[(long)m * P.ldaux + nn];
+        const float tv = (float)auxz[(long)m * P.ldaux + nn + N];
+        P.out2[(long)m * P.ldo2 + nn] = (h16)g;
+        y = tv + g * (ov - tv);
+      }
+    } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
+      if (nn < N) {
+        const float h = (float)auxz[(long)m * P.ldaux + nn];
+        y = h > 0.f ? y * (P.thresh ? 1.f / (1.f - P.p) : 1.f) : 0.f;
+      }
+    } else if (EPI == MMS_EPI_F16_ACC) {
+      if (nn < N) y += (float)C[nn];
+    }
+    o[r] = y;
+  }
+  if (n + 3 < N) {
+    *reinterpret_cast<h16x4*>(C + n) = h16x4{(h16)o[0], (h16)o[1], (h16)o[2], (h16)o[3]};
+  } else {
+    for (int r = 0; r < 4; ++r) if (n + r < N) C[n + r] = (h16)o[r];
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  const int ntiles = tiles_m * tiles_n;
+  // XCD-aware bijective remap of the linear block id (8 XCDs, round-robin dispatch)
+  int bid = blockIdx.x;
+  {
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int z = blockIdx.y;
+  const int zb = z / P.splitk, zs = z % P.splitk;
+  const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
+  const h16* A = P.A + z1 * P.sA1 + z2 * P.sA2;
+  const h16* B = P.B + z1 * P.sB1 + z2 * P.sB2;
+  const int kbeg = zs * P.kchunk;
+  const int kend = min(P.K, kbeg + P.kchunk);
+  const int bm = tm * BM, bn = tn * BN;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // stage s: A image at smem + 2s*TILE_BYTES, B image at smem + (2s+1)*TILE_BYTES
+#define SA(s) (smem + (2 * (s)) * TILE_BYTES)
+#define SB(s) (smem + (2 * (s) + 1) * TILE_BYTES)
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  s16x8 ra[4], rb[4];
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    load_tile<A_KC>(A, P.lda, P.M, P.K, bm, kbeg, kend, ra);
+    load_tile<B_KC>(B, P.ldb, P.N, P.K, bn, kbeg, kend, rb);
+    store_tile<A_KC>(SA(0), ra);
+    store_tile<B_KC>(SB(0), rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * BK;
+      load_tile<A_KC>(A, P.lda, P.M, P.K, bm, k0, kend, ra);
+      load_tile<B_KC>(B, P.ldb, P.N, P.K, bn, k0, kend, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      h16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      store_tile<A_KC>(SA(cur ^ 1), ra);
+      store_tile<B_KC>(SB(cur ^ 1), rb);
+    }
+    __syncthreads();
+  }
+#undef SA
+#undef SB
+
+  char* Cz;
+  if (EPI == MMS_EPI_F32)
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
+  else
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
+  const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = bm + wm * 64 + i * 16 + (lane & 15);
+      const int n = bn + wn * 64 + j * 16 + 4 * (lane >> 4);
+      epilogue_store<EPI>(P, Cz, auxz, m, n, acc[i][j]);
+    }
+}
+
+template <bool A_KC, bool B_KC>
+int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
+  dim3 grid(tm * tn, nz), block(NT);
+  const size_t lds = 0;
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, E>), grid, block, lds, s, P, tm, tn); break;
+    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+#undef CASE
+    default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
+  }
+  return mms::check_launch("gemm");
+}
+
+}  // namespace
+
+extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
+  MMS_REQUIRE(a != nullptr, "gemm: null args");
+  MMS_REQUIRE(a->M >= 0 && a->N >= 0 && a->K >= 0, "gemm: negative dims");
+  if (a->M == 0 || a->N == 0 || a->batch == 0) return 0;
+  MMS_REQUIRE(a->lda % 8 == 0 && a->ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8 (lda=%ld ldb=%ld)", a->lda, a->ldb);
+  MMS_REQUIRE(((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0, "gemm: A/B must be 16-byte aligned");
+  MMS_REQUIRE(a->epi == MMS_EPI_F32 ? (a->ldc % 4 == 0) : (a->ldc % 4 == 0), "gemm: ldc must be a multiple of 4");
+  const bool a_kc = a->a_kcontig != 0, b_kc = a->b_kcontig != 0;
+  // strides must keep 16-B alignment for every batch
+  MMS_REQUIRE(a->sA1 % 8 == 0 && a->sA2 % 8 == 0 && a->sB1 % 8 == 0 && a->sB2 % 8 == 0, "gemm: batch strides must be multiples of 8");
+  GemmP P{};
+  P.A = a->A; P.B = a->B; P.C = a->C;
+  P.M = a->M; P.N = a->N; P.K = a->K;
+  P.lda = a->lda; P.ldb = a->ldb; P.ldc = a->ldc;
+  P.bdiv = a->bdiv > 0 ? a->bdiv : 1;
+  P.sA1 = a->sA1; P.sA2 = a->sA2; P.sB1 = a->sB1; P.sB2 = a->sB2; P.sC1 = a->sC1; P.sC2 = a->sC2;
+  int splitk = a->splitk > 0 ? a->splitk : 1;
+  MMS_REQUIRE(splitk == 1 || a->epi == MMS_EPI_F32, "gemm: split-K needs the fp32 slab epilogue");
+  int kchunk = (a->K + splitk - 1) / splitk;
+  kchunk = ((kchunk + BK - 1) / BK) * BK;
+  if (kchunk == 0) kchunk = BK;
+  P.splitk = splitk; P.kchunk = kchunk; P.sCsplit = a->sCsplit;
+  P.alpha = a->alpha; P.bias = a->bias;
+  P.aux = a->aux; P.ldaux = a->ldaux; P.sX1 = a->sX1; P.sX2 = a->sX2;
+  P.out2 = a->out2; P.ldo2 = a->ldo2;
+  P.p = a->dropout_p; P.thresh = mms_drop_thresh(a->dropout_p); P.seed = a->seed; P.offset = a->offset;
+  P.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
+  MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
+  MMS_REQUIRE(a->epi != MMS_EPI_GATE || a->out2, "gemm: gate epilogue needs out2");
+  const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
+  const int nz = a->batch * splitk;
+  MMS_REQUIRE(nz <= 65535, "gemm: batch*splitk too large (%d)", nz);
+  hipStream_t s = stream;
+  if (a_kc && b_kc) return launch_epi<true, true>(a->epi, P, tm, tn, nz, s);
+  if (a_kc && !b_kc) return launch_epi<true, false>(a->epi, P, tm, tn, nz, s);
+  if (!a_kc && b_kc) return launch_epi<false, true>(a->epi, P, tm, tn, nz, s);
+  return launch_epi<false, false>(a->epi, P, tm, tn, nz, s);
+}

@@ -1,0 +1,248 @@
+// Label-smoothed cross entropy (fused fp32 log-softmax) and the FP16Optimizer/Adam update.
+#include "common.h"
+#include "../../include/mms2ut.h"
+
+namespace {
+
+// one wave per row of logits; V <= 64*4*CPL
+template <int CPL>
+__global__ void __launch_bounds__(256) ls_xent_fwd_kernel(const h16* __restrict__ z, long ld,
+                                                          const int64_t* __restrict__ target, long rows,
+                                                          int V, float eps, int pad, float* __restrict__ lse_out,
+                                                          float* __restrict__ loss_out) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long row = (long)blockIdx.x * 4 + w;
+  float loss = 0.f, nll = 0.f;
+  if (row < rows) {
+    const h16* zr = z + row * ld;
+    float v[CPL][4];
+    float mx = -INFINITY, sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int j0 = (lane + c * 64) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[c][e] = -INFINITY;
+      if (j0 < V) {
+        h16x4 t = *reinterpret_cast<const h16x4*>(zr + j0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (j0 + e < V) { v[c][e] = (float)t[e]; mx = fmaxf(mx, v[c][e]); sum += v[c][e]; }
+      }
+    }
+    mx = wave_max(mx);
+    sum = wave_sum(sum);
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) se += (v[c][e] == -INFINITY) ? 0.f : __expf(v[c][e] - mx);
+    se = wave_sum(se);
+    const float lse = mx + __logf(se);
+    if (lane == 0) lse_out[row] = lse;
+    const int64_t t = target[row];
+    if (t != pad) {
+      const float zt = (float)zr[t];
+      const float eps_i = eps / (V - 1);
+      nll = lse - zt;
+      const float smooth = V * lse - sum;
+      loss = (1.f - eps - eps_i) * nll + eps_i * smooth;
+    }
+  }
+  if (lane == 0) { red[0][w] = loss; red[1][w] = nll; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float l = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const float n = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    atomicAdd(loss_out, l);
+    atomicAdd(loss_out + 1, n);
+  }
+}
+
+template <int CPL>
+__global__ void __launch_bounds__(256) ls_xent_bwd_kernel(const h16* __restrict__ z, long ld,
+                                                          const int64_t* __restrict__ target, long rows,
+                                                          int V, float eps, int pad, const float* __restrict__ lse,
+                                                          const float* __restrict__ grad, h16* __restrict__ dz) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int64_t t = target[row];
+  const float g = grad[0];
+  const float eps_i = eps / (V - 1);
+  const float a = (t == pad) ? 0.f : g * (1.f - eps - eps_i);
+  const float bsm = (t == pad) ? 0.f : g * eps_i;
+  const float L = lse[row];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j0 = (lane + c * 64) * 4;
+    if (j0 < V) {
+      h16x4 zv = *reinterpret_cast<const h16x4*>(z + row * ld + j0);
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = j0 + e;
+        const float p = __expf((float)zv[e] - L);
+        o[e] = (j < V) ? a * (p - (j == t ? 1.f : 0.f)) + bsm * (V * p - 1.f) : 0.f;
+      }
+      *reinterpret_cast<h16x4*>(dz + row * ld + j0) = h16x4{(h16)o[0], (h16)o[1], (h16)o[2], (h16)o[3]};
+    }
+  }
+}
+
+__global__ void grad_sqnorm_kernel(const h16* __restrict__ g, long n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    h16x8 v = *reinterpret_cast<const h16x8*>(g + i * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float x = (float)v[e]; s += x * x; }
+  }
+  for (long i = n8 * 8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float x = (float)g[i];
+    s += x * x;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// ost layout (device fp32 optimizer state, see include/mms2ut.h MMS_OST_*)
+__global__ void grad_norm_finalize_kernel(const float* __restrict__ part, int nparts, float* ost,
+                                          const float* __restrict__ sample_size) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
+  s = wave_sum_d(s);
+  if (threadIdx.x == 0) {
+    // FP16Optimizer: multiply factor = 1/loss_scale * 1/sample_size (grads all-reduced as a SUM)
+    const float ss = sample_size ? fmaxf(sample_size[0], 1.f) : 1.f;
+    const float mult = 1.f / (ost[MMS_OST_LOSS_SCALE] * ss);
+    const float norm = (float)sqrt(s) * mult;
+    ost[MMS_OST_MULT] = mult;
+    ost[MMS_OST_GNORM] = norm;
+    ost[MMS_OST_OVERFLOW] = (isfinite(norm) && isfinite((float)s)) ? 0.f : 1.f;
+  }
+}
+
+// one thread: Adam step count / step size / clip coefficient and fairseq DynamicLossScaler
+__global__ void optim_prepare_kernel(float* ost, float lr, float b1, float b2, float clip, float scale_window,
+                                     float min_scale) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const bool overflow = ost[MMS_OST_OVERFLOW] != 0.f;
+  float it = ost[MMS_OST_ITER];
+  if (overflow) {
+    // check_overflow (tolerance 0): decrease, remember, skip the update
+    const float prev = ost[MMS_OST_LOSS_SCALE];
+    ost[MMS_OST_LAST_OVERFLOW] = it;
+    float ns = prev / 2.f;
+    ost[MMS_OST_LAST_RESCALE] = it;
+    if (ns <= min_scale) { ns = prev; ost[MMS_OST_FATAL] = 1.f; }
+    ost[MMS_OST_LOSS_SCALE] = ns;
+    ost[MMS_OST_ITER] = it + 1.f;
+    return;
+  }
+  const float step = ost[MMS_OST_STEP] + 1.f;
+  ost[MMS_OST_STEP] = step;
+  const double bc1 = 1.0 - pow((double)b1, (double)step), bc2 = 1.0 - pow((double)b2, (double)step);
+  ost[MMS_OST_STEP_SIZE] = (float)(lr * sqrt(bc2) / bc1);
+  ost[MMS_OST_CLIP_COEF] = clip > 0.f ? fminf(1.f, clip / (ost[MMS_OST_GNORM] + 1e-6f)) : 1.f;
+  // scaler.update(): grow every scale_window clean iterations
+  const float since = it - ost[MMS_OST_LAST_OVERFLOW];
+  if (fmodf(since, scale_window) == 0.f) {
+    ost[MMS_OST_LOSS_SCALE] *= 2.f;
+    ost[MMS_OST_LAST_RESCALE] = it;
+  }
+  ost[MMS_OST_ITER] = it + 1.f;
+}
+
+__global__ void adam_kernel(h16* __restrict__ param, const h16* __restrict__ grad, float* __restrict__ master,
+                            float* __restrict__ m, float* __restrict__ v, long n, const float* __restrict__ ost,
+                            float lr, float b1, float b2, float eps, float wd) {
+  if (ost[MMS_OST_OVERFLOW] != 0.f) return;  // overflow: skip (FP16Optimizer OverflowError path)
+  const float mult = ost[MMS_OST_MULT] * ost[MMS_OST_CLIP_COEF];
+  const float step_size = ost[MMS_OST_STEP_SIZE];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float g = (float)grad[i] * mult;
+    float p = master[i];
+    if (wd != 0.f) p -= wd * lr * p;
+    const float mi = b1 * m[i] + (1.f - b1) * g;
+    const float vi = b2 * v[i] + (1.f - b2) * g * g;
+    m[i] = mi;
+    v[i] = vi;
+    p -= step_size * mi / (sqrtf(vi) + eps);
+    master[i] = p;
+    param[i] = (h16)p;
+  }
+}
+
+template <typename F>
+int pick_cpl_v(int V, F&& f) {
+  const int cpl = (V + 255) / 256;
+  if (cpl <= 1) return f(std::integral_constant<int, 1>{});
+  if (cpl <= 2) return f(std::integral_constant<int, 2>{});
+  if (cpl <= 4) return f(std::integral_constant<int, 4>{});
+  if (cpl <= 8) return f(std::integral_constant<int, 8>{});
+  if (cpl <= 16) return f(std::integral_constant<int, 16>{});
+  mms::set_error("ls_xent: vocabulary too large (%d)", V);
+  return 1;
+}
+
+}  // namespace
+
+extern "C" int mms2ut_ls_xent_fwd(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
+                                  float eps, int pad_idx, float* lse, float* loss_out, hipStream_t s) {
+  MMS_REQUIRE(ld % 4 == 0 && ld >= V, "ls_xent: ld must be a multiple of 4 and >= V");
+  if (rows == 0) return 0;
+  return pick_cpl_v(V, [&](auto C) {
+    hipLaunchKernelGGL((ls_xent_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       logits, (long)ld, target, (long)rows, V, eps, pad_idx, lse, loss_out);
+    return mms::check_launch("ls_xent_fwd");
+  });
+}
+
+extern "C" int mms2ut_ls_xent_bwd(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
+                                  float eps, int pad_idx, const float* lse, const float* grad, h16* dlogits,
+                                  hipStream_t s) {
+  MMS_REQUIRE(ld % 4 == 0 && ld >= V, "ls_xent_bwd: ld must be a multiple of 4 and >= V");
+  if (rows == 0) return 0;
+  return pick_cpl_v(V, [&](auto C) {
+    hipLaunchKernelGGL((ls_xent_bwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       logits, (long)ld, target, (long)rows, V, eps, pad_idx, lse, grad, dlogits);
+    return mms::check_launch("ls_xent_bwd");
+  });
+}
+
+extern "C" int mms2ut_grad_sqnorm(const h16* grad, int64_t n, float* part, int nparts, hipStream_t s) {
+  MMS_REQUIRE(((uintptr_t)grad & 15) == 0, "grad_sqnorm: grad must be 16-byte aligned");
+  MMS_REQUIRE(nparts > 0 && nparts <= 65535, "grad_sqnorm: bad nparts");
+  hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(nparts), dim3(256), 0, s, grad, (long)n, part);
+  return mms::check_launch("grad_sqnorm");
+}
+
+extern "C" int mms2ut_grad_norm_finalize(const float* part, int nparts, float* ost, const float* sample_size,
+                                         hipStream_t s) {
+  hipLaunchKernelGGL(grad_norm_finalize_kernel, dim3(1), dim3(64), 0, s, part, nparts, ost, sample_size);
+  return mms::check_launch("grad_norm_finalize");
+}
+
+extern "C" int mms2ut_optim_prepare(float* ost, float lr, float beta1, float beta2, float clip_norm,
+                                    float scale_window, float min_loss_scale, hipStream_t s) {
+  MMS_REQUIRE(scale_window >= 1.f, "optim_prepare: scale_window must be >= 1");
+  hipLaunchKernelGGL(optim_prepare_kernel, dim3(1), dim3(64), 0, s, ost, lr, beta1, beta2, clip_norm,
+                     scale_window, min_loss_scale);
+  return mms::check_launch("optim_prepare");
+}
+
+extern "C" int mms2ut_adam_fp16_master(h16* param, const h16* grad, float* master, float* exp_avg,
+                                       float* exp_avg_sq, int64_t n, const float* ost, float lr,
+                                       float beta1, float beta2, float eps, float weight_decay,
+                                       hipStream_t s) {
+  if (n == 0) return 0;
+  long g = (n + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(adam_kernel, dim3((int)g), dim3(256), 0, s, param, grad, master, exp_avg, exp_avg_sq,
+                     (long)n, ost, lr, beta1, beta2, eps, weight_decay);
+  return mms::check_launch("adam");
+}

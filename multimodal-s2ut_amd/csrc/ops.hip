@@ -1,0 +1,741 @@
+// Memory-bound kernels of the training step: LayerNorm fwd/bwd, column reductions (bias /
+// LayerNorm parameter grads), masked attention softmax fwd/bwd with counter-RNG dropout,
+// embeddings, GLU, im2col/col2im, the fusion-gate backward and small elementwise helpers.
+// All HBM-bound: one wave per row for row ops, 8-byte (4 x fp16) vector accesses, fp32 math.
+#include "common.h"
+#include "../../include/mms2ut.h"
+
+namespace {
+
+inline int grid_for(long n, int block, int cap = 8192) {
+  long g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+MMS_DEV h16x4 ld4(const h16* p) { return *reinterpret_cast<const h16x4*>(p); }
+MMS_DEV void st4(h16* p, float a, float b, float c, float d) {
+  *reinterpret_cast<h16x4*>(p) = h16x4{(h16)a, (h16)b, (h16)c, (h16)d};
+}
+
+// ============================================================================ LayerNorm
+template <int CPL>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, const h16* __restrict__ g,
+                                                     const h16* __restrict__ b, h16* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     long rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = D >> 2;
+  const h16* xr = x + row * D;
+  float v[CPL][4];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      h16x4 t = ld4(xr + ch * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[c][e] = (float)t[e]; s += v[c][e]; }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[c][e] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[c][e] - mean; ss += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / D + eps);
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  h16* yr = y + row * D;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      h16x4 gg = ld4(g + ch * 4), bb = ld4(b + ch * 4);
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * (float)gg[e] + (float)bb[e];
+      st4(yr + ch * 4, o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+constexpr int LN_BWD_ROWS = 32;  // rows per block (8 per wave)
+
+template <int CPL>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy, const h16* __restrict__ x,
+                                                     const h16* __restrict__ g, const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, const h16* __restrict__ dres,
+                                                     h16* __restrict__ dx, float* __restrict__ part,
+                                                     long rows, int D) {
+  __shared__ float red[4][2][CPL * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = D >> 2;
+  float dg[CPL][4], db[CPL][4], gam[CPL][4];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { dg[c][e] = 0.f; db[c][e] = 0.f; gam[c][e] = 0.f; }
+    if (ch < nch) {
+      h16x4 gg = ld4(g + ch * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gam[c][e] = (float)gg[e];
+    }
+  }
+  const long r0 = (long)blockIdx.x * LN_BWD_ROWS;
+  for (int rr = w; rr < LN_BWD_ROWS; rr += 4) {
+    const long row = r0 + rr;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[CPL][4], gd[CPL][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        h16x4 xv = ld4(x + row * D + ch * 4), dv = ld4(dy + row * D + ch * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[c][e] = ((float)xv[e] - mu) * rs;
+          const float d = (float)dv[e];
+          gd[c][e] = d * gam[c][e];
+          s1 += gd[c][e] * xh[c][e];
+          s2 += gd[c][e];
+          dg[c][e] += d * xh[c][e];
+          db[c][e] += d;
+        }
+      }
+    }
+    if (!dx) continue;  // parameter grads only (image_pre_norm: image features are leaves)
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nch) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs * (gd[c][e] - xh[c][e] * s1 - s2);
+        if (dres) {
+          h16x4 rv = ld4(dres + row * D + ch * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += (float)rv[e];
+        }
+        st4(dx + row * D + ch * 4, o[0], o[1], o[2], o[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[w][0][(c * 64 + lane) * 4 + e] = dg[c][e];
+      red[w][1][(c * 64 + lane) * 4 + e] = db[c][e];
+    }
+  __syncthreads();
+  float* out = part + (long)blockIdx.x * 2 * D;
+  for (int i = threadIdx.x; i < 2 * D; i += 256) {
+    const int which = i / D, j = i % D;
+    const int ch = j >> 2, e = j & 3;
+    const int c = ch / 64, ln = ch % 64;
+    const int idx = (c * 64 + ln) * 4 + e;
+    out[i] = red[0][which][idx] + red[1][which][idx] + red[2][which][idx] + red[3][which][idx];
+  }
+}
+
+__global__ void colsum_parts_kernel(const float* __restrict__ part, int nparts, int ncol,
+                                    h16* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(long)p * ncol + c];
+  if (accumulate) s += (float)out[c];
+  out[c] = (h16)s;
+}
+
+constexpr int COLSUM_ROWS = 64;
+__global__ void colsum_f16_kernel(const h16* __restrict__ x, long rows, int cols, long ld,
+                                  float* __restrict__ part) {
+  const long r0 = (long)blockIdx.x * COLSUM_ROWS;
+  const long r1 = min(rows, r0 + COLSUM_ROWS);
+  for (int c4 = threadIdx.x; c4 * 4 < cols; c4 += blockDim.x) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (long r = r0; r < r1; ++r) {
+      h16x4 v = ld4(x + r * ld + c4 * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += (float)v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[(long)blockIdx.x * cols + c4 * 4 + e] = s[e];
+  }
+}
+
+// ============================================================================ attention softmax
+// One wave per score row; lane owns contiguous 4-key chunks (chunk = lane + 64*c).
+MMS_DEV bool key_valid(int j, int i, int Tk, int klen, const uint8_t* km, int causal, int extra_key) {
+  if (j >= Tk) return false;
+  if (extra_key && j == Tk - 1) return true;
+  if (j >= klen) return false;
+  if (km && km[j]) return false;
+  if (causal && j > i) return false;
+  return true;
+}
+
+template <int CPL>
+__global__ void __launch_bounds__(256) softmax_fwd_kernel(const h16* __restrict__ S, h16* __restrict__ P,
+                                                          h16* __restrict__ Pd, int Z, int H, int Tq, int Tk,
+                                                          long ldS, const int* __restrict__ key_len,
+                                                          const uint8_t* __restrict__ key_mask, long ld_mask,
+                                                          int causal, int extra_key, float p, uint32_t thresh,
+                                                          uint64_t seed, uint64_t offset) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)Z * Tq) return;
+  const int z = (int)(row / Tq), i = (int)(row % Tq);
+  const int b = z / H;
+  const int klen = key_len ? key_len[b] : Tk;
+  const uint8_t* km = key_mask ? key_mask + (long)b * ld_mask : nullptr;
+  const h16* sr = S + row * ldS;
+  float v[CPL][4];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j0 = (lane + c * 64) * 4;
+    if (j0 < Tk) {
+      h16x4 t = ld4(sr + j0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = j0 + e;
+        v[c][e] = key_valid(j, i, Tk, klen, km, causal, extra_key) ? (float)t[e] : -INFINITY;
+        mx = fmaxf(mx, v[c][e]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[c][e] = -INFINITY;
+    }
+  }
+  mx = wave_max(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float ex = (v[c][e] == -INFINITY) ? 0.f : __expf(v[c][e] - mx);
+      v[c][e] = ex;
+      s += ex;
+    }
+  s = wave_sum(s);
+  const float inv = s > 0.f ? 1.f / s : 0.f;
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  h16* pr = P + row * ldS;
+  h16* pdr = Pd + row * ldS;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j0 = (lane + c * 64) * 4;
+    if (j0 < Tk) {
+      float o[4], od[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (j0 + e < Tk) ? v[c][e] * inv : 0.f;
+        od[e] = o[e];
+        if (thresh) {
+          const bool keep = mms_keep(seed, offset + (uint64_t)row * Tk + (j0 + e), thresh);
+          od[e] = keep ? o[e] * ds : 0.f;
+        }
+      }
+      st4(pr + j0, o[0], o[1], o[2], o[3]);
+      if (thresh) st4(pdr + j0, od[0], od[1], od[2], od[3]);
+    }
+  }
+}
+
+template <int CPL>
+__global__ void __launch_bounds__(256) softmax_bwd_kernel(const h16* __restrict__ P, const h16* __restrict__ dPd,
+                                                          h16* __restrict__ dS, int Z, int H, int Tq, int Tk,
+                                                          long ldS, float p, uint32_t thresh, uint64_t seed,
+                                                          uint64_t offset) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)Z * Tq) return;
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  float pv[CPL][4], gv[CPL][4];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j0 = (lane + c * 64) * 4;
+    if (j0 < Tk) {
+      h16x4 a = ld4(P + row * ldS + j0), g = ld4(dPd + row * ldS + j0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = j0 + e;
+        float m = ds;
+        if (thresh && j < Tk) m = mms_keep(seed, offset + (uint64_t)row * Tk + j, thresh) ? ds : 0.f;
+        pv[c][e] = (j < Tk) ? (float)a[e] : 0.f;
+        gv[c][e] = (j < Tk) ? (float)g[e] * m : 0.f;  // dP (undropped grad)
+        s += pv[c][e] * gv[c][e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { pv[c][e] = 0.f; gv[c][e] = 0.f; }
+    }
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int j0 = (lane + c * 64) * 4;
+    if (j0 < Tk) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = pv[c][e] * (gv[c][e] - s);
+      st4(dS + row * ldS + j0, o[0], o[1], o[2], o[3]);
+    }
+  }
+  (void)Z; (void)H;
+}
+
+// ============================================================================ elementwise
+__global__ void dropout_kernel(const h16* __restrict__ x, h16* __restrict__ y, long n, float p,
+                               uint32_t thresh, uint64_t seed, uint64_t offset) {
+  const float ds = 1.f / (1.f - p);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = (float)x[i];
+    y[i] = (h16)(mms_keep(seed, offset + i, thresh) ? v * ds : 0.f);
+  }
+}
+
+__global__ void dropout_mask_kernel(uint8_t* keep, long n, uint32_t thresh, uint64_t seed, uint64_t offset) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    keep[i] = thresh ? (uint8_t)mms_keep(seed, offset + i, thresh) : 1;
+}
+
+__global__ void encoder_embed_kernel(const h16* __restrict__ h, const h16* __restrict__ pos,
+                                     const int* __restrict__ len, h16* __restrict__ x, int B, int T,
+                                     int D, float scale, float p, uint32_t thresh, uint64_t seed,
+                                     uint64_t offset) {
+  const long n4 = (long)B * T * (D / 4);
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long e0 = i * 4;
+    const long bt = e0 / D;
+    const int d0 = (int)(e0 % D);
+    const int b = (int)(bt / T), t = (int)(bt % T);
+    const int pidx = (t < len[b]) ? t + 2 : 1;
+    h16x4 hv = ld4(h + e0), pv = ld4(pos + (long)pidx * D + d0);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = scale * (float)hv[e] + (float)pv[e];
+      if (thresh) v = mms_keep(seed, offset + e0 + e, thresh) ? v * ds : 0.f;
+      o[e] = v;
+    }
+    st4(x + e0, o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ void scale_dropout_bwd_kernel(const h16* __restrict__ dx, h16* __restrict__ dh, long n,
+                                         float scale, float p, uint32_t thresh, uint64_t seed,
+                                         uint64_t offset) {
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = (float)dx[i] * scale;
+    if (thresh) v = mms_keep(seed, offset + i, thresh) ? v * ds : 0.f;
+    dh[i] = (h16)v;
+  }
+}
+
+// one wave per token: position = make_positions (cumsum of non-pad tokens up to t)
+__global__ void token_embed_fwd_kernel(const int64_t* __restrict__ tok, const h16* __restrict__ E,
+                                       const h16* __restrict__ pos, h16* __restrict__ x, int B, int T,
+                                       int D, int pad, float scale, float p, uint32_t thresh,
+                                       uint64_t seed, uint64_t offset) {
+  const int lane = threadIdx.x & 63;
+  const long bt = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bt >= (long)B * T) return;
+  const int b = (int)(bt / T), t = (int)(bt % T);
+  const int64_t tk = tok[bt];
+  int cnt = 0;
+  for (int j = lane; j <= t; j += 64) cnt += (tok[(long)b * T + j] != pad);
+  cnt = (int)wave_sum((float)cnt);
+  const int pidx = (tk != pad) ? cnt + pad : pad;
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  for (int d0 = lane * 4; d0 < D; d0 += 256) {
+    h16x4 ev = ld4(E + tk * D + d0), pv = ld4(pos + (long)pidx * D + d0);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = scale * (float)ev[e] + (float)pv[e];
+      if (thresh) v = mms_keep(seed, offset + bt * D + d0 + e, thresh) ? v * ds : 0.f;
+      o[e] = v;
+    }
+    st4(x + bt * D + d0, o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ void token_embed_bwd_kernel(const int64_t* __restrict__ tok, const h16* __restrict__ dx,
+                                       float* __restrict__ dE, int B, int T, int D, int pad, float scale,
+                                       float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
+  const int lane = threadIdx.x & 63;
+  const long bt = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bt >= (long)B * T) return;
+  const int64_t tk = tok[bt];
+  if (tk == pad) return;  // nn.Embedding(padding_idx): no grad to the pad row
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  for (int d = lane; d < D; d += 64) {
+    float v = (float)dx[bt * D + d] * scale;
+    if (thresh) v = mms_keep(seed, offset + bt * D + d, thresh) ? v * ds : 0.f;
+    atomicAdd(dE + tk * D + d, v);
+  }
+  (void)B;
+}
+
+__global__ void add_f32_to_f16_kernel(const h16* __restrict__ a, const float* __restrict__ b,
+                                      h16* __restrict__ out, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = (h16)((float)a[i] + b[i]);
+}
+
+__global__ void add_f16_kernel(const h16* __restrict__ a, const h16* __restrict__ b,
+                               h16* __restrict__ out, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = (h16)((float)a[i] + (float)b[i]);
+}
+
+MMS_DEV float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__global__ void glu_fwd_kernel(const h16* __restrict__ x, h16* __restrict__ y, long rows, int C) {
+  const long n4 = rows * (C / 4);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / (C / 4);
+    const int c = (int)(i % (C / 4)) * 4;
+    h16x4 a = ld4(x + r * 2 * C + c), g = ld4(x + r * 2 * C + C + c);
+    st4(y + r * C + c, (float)a[0] * sigm((float)g[0]), (float)a[1] * sigm((float)g[1]),
+        (float)a[2] * sigm((float)g[2]), (float)a[3] * sigm((float)g[3]));
+  }
+}
+
+__global__ void glu_bwd_kernel(const h16* __restrict__ x, const h16* __restrict__ dy,
+                               h16* __restrict__ dx, long rows, int C) {
+  const long n4 = rows * (C / 4);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / (C / 4);
+    const int c = (int)(i % (C / 4)) * 4;
+    h16x4 a = ld4(x + r * 2 * C + c), g = ld4(x + r * 2 * C + C + c), d = ld4(dy + r * C + c);
+    float da[4], dg[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float s = sigm((float)g[e]);
+      da[e] = (float)d[e] * s;
+      dg[e] = (float)d[e] * (float)a[e] * s * (1.f - s);
+    }
+    st4(dx + r * 2 * C + c, da[0], da[1], da[2], da[3]);
+    st4(dx + r * 2 * C + C + c, dg[0], dg[1], dg[2], dg[3]);
+  }
+}
+
+// col[(b,t)][c*k + kk] = x[b][t*stride - pad + kk][c]
+__global__ void im2col_kernel(const h16* __restrict__ x, h16* __restrict__ col, int B, int Tin,
+                              int Tout, int C, int k, int stride, int pad) {
+  const long W = (long)C * k;
+  const long n = (long)B * Tout * W;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long bt = i / W;
+    const int rem = (int)(i % W);
+    const int c = rem / k, kk = rem % k;
+    const int b = (int)(bt / Tout), t = (int)(bt % Tout);
+    const int ti = t * stride - pad + kk;
+    col[i] = (ti >= 0 && ti < Tin) ? x[((long)b * Tin + ti) * C + c] : (h16)0.f;
+  }
+}
+
+__global__ void col2im_kernel(const h16* __restrict__ dcol, h16* __restrict__ dx, int B, int Tin,
+                              int Tout, int C, int k, int stride, int pad) {
+  const long n = (long)B * Tin * C;
+  const long W = (long)C * k;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long bt = i / C;
+    const int b = (int)(bt / Tin), ti = (int)(bt % Tin);
+    float s = 0.f;
+    for (int kk = 0; kk < k; ++kk) {
+      const int num = ti + pad - kk;
+      if (num < 0 || num % stride) continue;
+      const int t = num / stride;
+      if (t >= Tout) continue;
+      s += (float)dcol[((long)b * Tout + t) * W + (long)c * k + kk];
+    }
+    dx[i] = (h16)s;
+  }
+}
+
+__global__ void gate_bwd_kernel(const h16* __restrict__ dres, const h16* __restrict__ merge,
+                                const h16* __restrict__ g, h16* __restrict__ dpre,
+                                h16* __restrict__ dmerge, long rows, int D) {
+  const long n4 = rows * (D / 4);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / (D / 4);
+    const int c = (int)(i % (D / 4)) * 4;
+    h16x4 dr = ld4(dres + r * D + c), o = ld4(merge + r * 2 * D + c), t = ld4(merge + r * 2 * D + D + c),
+          gv = ld4(g + r * D + c);
+    float dp[4], dmo[4], dmt[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gg = (float)gv[e], d = (float)dr[e];
+      dp[e] = d * ((float)o[e] - (float)t[e]) * gg * (1.f - gg);
+      dmo[e] = d * gg;
+      dmt[e] = d * (1.f - gg);
+    }
+    st4(dpre + r * D + c, dp[0], dp[1], dp[2], dp[3]);
+    st4(dmerge + r * 2 * D + c, dmo[0], dmo[1], dmo[2], dmo[3]);
+    st4(dmerge + r * 2 * D + D + c, dmt[0], dmt[1], dmt[2], dmt[3]);
+  }
+}
+
+__global__ void copy2d_kernel(const h16* __restrict__ src, long lds, h16* __restrict__ dst, long ldd,
+                              long rows, int cols) {
+  const long n = rows * cols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols;
+    const int c = (int)(i % cols);
+    dst[r * ldd + c] = src[r * lds + c];
+  }
+}
+
+template <typename F>
+int pick_cpl(int chunks_per_row, F&& f) {
+  const int cpl = (chunks_per_row + 63) / 64;
+  if (cpl <= 1) return f(std::integral_constant<int, 1>{});
+  if (cpl <= 2) return f(std::integral_constant<int, 2>{});
+  if (cpl <= 3) return f(std::integral_constant<int, 3>{});
+  if (cpl <= 4) return f(std::integral_constant<int, 4>{});
+  if (cpl <= 8) return f(std::integral_constant<int, 8>{});
+  if (cpl <= 16) return f(std::integral_constant<int, 16>{});
+  mms::set_error("row too long (%d chunks)", chunks_per_row);
+  return 1;
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+extern "C" int mms2ut_layernorm_fwd(const h16* x, const h16* gamma, const h16* beta, h16* y,
+                                    float* mean, float* rstd, int64_t rows, int D, float eps,
+                                    hipStream_t s) {
+  MMS_REQUIRE(D % 4 == 0, "layernorm: D must be a multiple of 4");
+  if (rows == 0) return 0;
+  return pick_cpl(D / 4, [&](auto C) {
+    hipLaunchKernelGGL((ln_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       x, gamma, beta, y, mean, rstd, (long)rows, D, eps);
+    return mms::check_launch("layernorm_fwd");
+  });
+}
+
+extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
+  return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
+}
+
+extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamma, const float* mean,
+                                    const float* rstd, const h16* dres, h16* dx, float* part,
+                                    int64_t rows, int D, hipStream_t s) {
+  MMS_REQUIRE(D % 4 == 0 && D <= 1024, "layernorm_bwd: D must be a multiple of 4 and <= 1024");
+  if (rows == 0) return 0;
+  const int nb = mms2ut_layernorm_bwd_parts(rows);
+  return pick_cpl(D / 4, [&](auto C) {
+    constexpr int CPL = decltype(C)::value;
+    if constexpr (CPL <= 4) {
+      hipLaunchKernelGGL((ln_bwd_kernel<CPL>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, rstd,
+                         dres, dx, part, (long)rows, D);
+      return mms::check_launch("layernorm_bwd");
+    } else {
+      mms::set_error("layernorm_bwd: D too large");
+      return 1;
+    }
+  });
+}
+
+extern "C" int mms2ut_colsum_parts(const float* part, int nparts, int ncol, h16* out, int accumulate,
+                                   hipStream_t s) {
+  if (ncol == 0) return 0;
+  hipLaunchKernelGGL(colsum_parts_kernel, dim3((ncol + 255) / 256), dim3(256), 0, s, part, nparts,
+                     ncol, out, accumulate);
+  return mms::check_launch("colsum_parts");
+}
+
+extern "C" int mms2ut_colsum_nparts(int64_t rows) { return (int)((rows + COLSUM_ROWS - 1) / COLSUM_ROWS); }
+
+extern "C" int mms2ut_colsum_f16(const h16* x, int64_t rows, int cols, int64_t ld, float* part,
+                                 int nparts, hipStream_t s) {
+  MMS_REQUIRE(cols % 4 == 0 && ld % 4 == 0, "colsum_f16: cols/ld must be multiples of 4");
+  MMS_REQUIRE(nparts == mms2ut_colsum_nparts(rows), "colsum_f16: nparts mismatch");
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(colsum_f16_kernel, dim3(nparts), dim3(256), 0, s, x, (long)rows, cols, (long)ld, part);
+  return mms::check_launch("colsum_f16");
+}
+
+extern "C" int mms2ut_attn_softmax_fwd(const h16* S, h16* P, h16* Pd, int Z, int H, int Tq, int Tk,
+                                       int64_t ldS, const int32_t* key_len, const uint8_t* key_mask,
+                                       int64_t ld_mask, int causal, int extra_key,
+                                       float p, uint64_t seed, uint64_t offset, hipStream_t s) {
+  MMS_REQUIRE(ldS % 4 == 0 && ldS >= Tk, "softmax: ldS must be a multiple of 4 and >= Tk");
+  MMS_REQUIRE(p < 1.f, "softmax: p must be < 1");
+  const long rows = (long)Z * Tq;
+  if (rows == 0) return 0;
+  const uint32_t th = mms_drop_thresh(p);
+  return pick_cpl((Tk + 3) / 4, [&](auto C) {
+    hipLaunchKernelGGL((softmax_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       S, P, Pd, Z, H, Tq, Tk, (long)ldS, key_len, key_mask, (long)ld_mask, causal,
+                       extra_key, p, th, seed, offset);
+    return mms::check_launch("attn_softmax_fwd");
+  });
+}
+
+extern "C" int mms2ut_attn_softmax_bwd(const h16* P, const h16* dPd, h16* dS, int Z, int H, int Tq,
+                                       int Tk, int64_t ldS, const int32_t* key_len, int causal,
+                                       int extra_key, float p, uint64_t seed, uint64_t offset,
+                                       hipStream_t s) {
+  MMS_REQUIRE(ldS % 4 == 0 && ldS >= Tk, "softmax_bwd: ldS must be a multiple of 4 and >= Tk");
+  const long rows = (long)Z * Tq;
+  if (rows == 0) return 0;
+  const uint32_t th = mms_drop_thresh(p);
+  (void)key_len; (void)causal; (void)extra_key;  // masked entries have P == 0 -> dS == 0
+  return pick_cpl((Tk + 3) / 4, [&](auto C) {
+    hipLaunchKernelGGL((softmax_bwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       P, dPd, dS, Z, H, Tq, Tk, (long)ldS, p, th, seed, offset);
+    return mms::check_launch("attn_softmax_bwd");
+  });
+}
+
+extern "C" int mms2ut_dropout_fwd(const h16* x, h16* y, int64_t n, float p, uint64_t seed,
+                                  uint64_t offset, hipStream_t s) {
+  MMS_REQUIRE(p < 1.f, "dropout: p must be < 1");
+  if (n == 0) return 0;
+  const uint32_t th = mms_drop_thresh(p);
+  if (!th) {
+    if (x != y) return hipMemcpyAsync(y, x, n * 2, hipMemcpyDeviceToDevice, s) == hipSuccess ? 0 : 1;
+    return 0;
+  }
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, y, (long)n, p, th, seed, offset);
+  return mms::check_launch("dropout_fwd");
+}
+
+extern "C" int mms2ut_dropout_mask(uint8_t* keep, int64_t n, float p, uint64_t seed, uint64_t offset,
+                                   hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(dropout_mask_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, keep, (long)n,
+                     mms_drop_thresh(p), seed, offset);
+  return mms::check_launch("dropout_mask");
+}
+
+extern "C" int mms2ut_encoder_embed_fwd(const h16* h, const h16* pos, const int32_t* len, h16* x, int B,
+                                        int T, int D, float scale, float p, uint64_t seed,
+                                        uint64_t offset, hipStream_t s) {
+  MMS_REQUIRE(D % 4 == 0, "encoder_embed: D must be a multiple of 4");
+  const long n4 = (long)B * T * (D / 4);
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL(encoder_embed_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, h, pos, len, x, B,
+                     T, D, scale, p, mms_drop_thresh(p), seed, offset);
+  return mms::check_launch("encoder_embed_fwd");
+}
+
+extern "C" int mms2ut_scale_dropout_bwd(const h16* dx, h16* dh, int64_t n, float scale, float p,
+                                        uint64_t seed, uint64_t offset, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scale_dropout_bwd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, dx, dh, (long)n,
+                     scale, p, mms_drop_thresh(p), seed, offset);
+  return mms::check_launch("scale_dropout_bwd");
+}
+
+extern "C" int mms2ut_token_embed_fwd(const int64_t* tok, const h16* E, const h16* pos, h16* x, int B,
+                                      int T, int D, int pad_idx, float scale, float p, uint64_t seed,
+                                      uint64_t offset, hipStream_t s) {
+  MMS_REQUIRE(D % 4 == 0, "token_embed: D must be a multiple of 4");
+  const long n = (long)B * T;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(token_embed_fwd_kernel, dim3((n + 3) / 4), dim3(256), 0, s, tok, E, pos, x, B, T,
+                     D, pad_idx, scale, p, mms_drop_thresh(p), seed, offset);
+  return mms::check_launch("token_embed_fwd");
+}
+
+extern "C" int mms2ut_token_embed_bwd(const int64_t* tok, const h16* dx, float* dE32, int B, int T,
+                                      int D, int pad_idx, float scale, float p, uint64_t seed,
+                                      uint64_t offset, hipStream_t s) {
+  const long n = (long)B * T;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(token_embed_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, s, tok, dx, dE32, B, T, D,
+                     pad_idx, scale, p, mms_drop_thresh(p), seed, offset);
+  return mms::check_launch("token_embed_bwd");
+}
+
+extern "C" int mms2ut_add_f32_to_f16(const h16* a, const float* b, h16* out, int64_t n, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(add_f32_to_f16_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, a, b, out, (long)n);
+  return mms::check_launch("add_f32_to_f16");
+}
+
+extern "C" int mms2ut_add_f16(const h16* a, const h16* b, h16* out, int64_t n, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(add_f16_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, a, b, out, (long)n);
+  return mms::check_launch("add_f16");
+}
+
+extern "C" int mms2ut_glu_fwd(const h16* x, h16* y, int64_t rows, int C, hipStream_t s) {
+  MMS_REQUIRE(C % 4 == 0, "glu: C must be a multiple of 4");
+  const long n4 = (long)rows * (C / 4);
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL(glu_fwd_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, x, y, (long)rows, C);
+  return mms::check_launch("glu_fwd");
+}
+
+extern "C" int mms2ut_glu_bwd(const h16* x, const h16* dy, h16* dx, int64_t rows, int C, hipStream_t s) {
+  MMS_REQUIRE(C % 4 == 0, "glu_bwd: C must be a multiple of 4");
+  const long n4 = (long)rows * (C / 4);
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL(glu_bwd_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, x, dy, dx, (long)rows, C);
+  return mms::check_launch("glu_bwd");
+}
+
+extern "C" int mms2ut_im2col(const h16* x, h16* col, int B, int Tin, int Tout, int C, int k, int stride,
+                             int pad, hipStream_t s) {
+  const long n = (long)B * Tout * C * k;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, col, B, Tin, Tout, C, k,
+                     stride, pad);
+  return mms::check_launch("im2col");
+}
+
+extern "C" int mms2ut_col2im(const h16* dcol, h16* dx, int B, int Tin, int Tout, int C, int k, int stride,
+                             int pad, hipStream_t s) {
+  const long n = (long)B * Tin * C;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, dcol, dx, B, Tin, Tout, C, k,
+                     stride, pad);
+  return mms::check_launch("col2im");
+}
+
+extern "C" int mms2ut_gate_bwd(const h16* dres, const h16* merge, const h16* g, h16* dpre, h16* dmerge,
+                               int64_t rows, int D, hipStream_t s) {
+  MMS_REQUIRE(D % 4 == 0, "gate_bwd: D must be a multiple of 4");
+  const long n4 = (long)rows * (D / 4);
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL(gate_bwd_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, dres, merge, g, dpre,
+                     dmerge, (long)rows, D);
+  return mms::check_launch("gate_bwd");
+}
+
+extern "C" int mms2ut_copy2d(const h16* src, int64_t lds, h16* dst, int64_t ldd, int64_t rows, int cols,
+                             hipStream_t s) {
+  const long n = (long)rows * cols;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(copy2d_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, src, (long)lds, dst,
+                     (long)ldd, (long)rows, cols);
+  return mms::check_launch("copy2d");
+}

@@ -1,0 +1,359 @@
+"""Torch-tensor front of the C-ABI: validation + pointer plumbing, no arithmetic.
+
+Every function enqueues HIP kernels on PyTorch's current stream through libmms2ut_hip.so.
+Tensors are fp16 (``torch.float16``) unless stated; shapes are checked before the call.
+"""
+import math
+
+import torch
+
+from . import _lib
+from ._lib import GemmArgs, call
+
+EPI_F16, EPI_RELU_DROP, EPI_DROP_RESID, EPI_F32, EPI_GATE, EPI_RELU_DROP_BWD, EPI_F16_ACC = range(7)
+F16 = torch.float16
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _chk(t, dtype=F16):
+    assert t.is_cuda, "HIP kernels need device tensors"
+    assert t.dtype == dtype, f"expected {dtype}, got {t.dtype}"
+
+
+class Dropout:
+    """Counter-based dropout stream: each call site draws a disjoint counter range from one
+    per-step seed, so a backward pass regenerates exactly the forward mask."""
+
+    def __init__(self, seed=1):
+        self.seed = seed
+        self.offset = 0
+
+    def reset(self, seed):
+        self.seed = int(seed) & ((1 << 63) - 1)
+        self.offset = 0
+
+    def take(self, n):
+        off = self.offset
+        self.offset += (int(n) + 255) // 256 * 256
+        return self.seed, off
+
+# ============================================================================ GEMM
+
+
+def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv=1,
+         sA=(0, 0), sB=(0, 0), sC=(0, 0), epi=EPI_F16, alpha=1.0, bias=None, aux=None, ldaux=0,
+         sX=(0, 0), out2=None, ldo2=0, p=0.0, seed=0, offset=0, ld_rng=0, splitk=1, sCsplit=0):
+    a = GemmArgs()
+    a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
+    a.M, a.N, a.K = int(M), int(N), int(K)
+    a.a_kcontig, a.b_kcontig = int(a_kc), int(b_kc)
+    a.lda, a.ldb, a.ldc = int(lda), int(ldb), int(ldc)
+    a.batch, a.bdiv = int(batch), int(bdiv)
+    a.sA1, a.sA2 = sA
+    a.sB1, a.sB2 = sB
+    a.sC1, a.sC2 = sC
+    a.splitk, a.sCsplit = int(splitk), int(sCsplit)
+    a.epi, a.alpha = int(epi), float(alpha)
+    a.bias = _p(bias)
+    a.aux = _p(aux)
+    a.ldaux = int(ldaux)
+    a.sX1, a.sX2 = sX
+    a.out2, a.ldo2 = _p(out2), int(ldo2)
+    a.dropout_p, a.seed, a.offset, a.ld_rng = float(p), int(seed), int(offset), int(ld_rng)
+    if GEMM_EVENTS is None:
+        call("mms2ut_gemm_f16", a, _s())
+    else:  # live per-launch timing with HIP events on the launch stream (bench roofline)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        call("mms2ut_gemm_f16", a, _s())
+        e1.record()
+        GEMM_EVENTS.append((e0, e1, 2.0 * M * N * K * batch))
+
+
+GEMM_EVENTS = None  # set to a list to time every GEMM launch (bench.py)
+
+
+def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
+           ldc=None, alpha=1.0):
+    """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue)."""
+    M, K = x.shape
+    N = W.shape[0]
+    assert W.shape[1] == K, (W.shape, x.shape)
+    if out is None:
+        out = torch.empty(M, N, dtype=F16, device=x.device)
+    seed = off = 0
+    if p > 0.0:
+        seed, off = drop
+    gemm(x, W, out, M, N, K, lda=x.stride(0), ldb=W.stride(0), ldc=ldc or out.stride(0), epi=epi,
+         bias=bias, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), out2=out2,
+         ldo2=(out2.stride(0) if out2 is not None else 0), p=p, seed=seed, offset=off, ld_rng=N,
+         alpha=alpha)
+    return out
+
+
+def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False):
+    """dx[M,K] = dy[M,N] @ W[N,K]  (W row-major, reduction over N)."""
+    M, N = dy.shape
+    K = W.shape[1]
+    if out is None:
+        out = torch.empty(M, K, dtype=F16, device=dy.device)
+    if accumulate:
+        epi = EPI_F16_ACC
+    gemm(dy, W, out, M, K, N, a_kc=True, b_kc=False, lda=dy.stride(0), ldb=W.stride(0),
+         ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p)
+    return out
+
+
+def _splitk_for(tiles, kred):
+    target = 512
+    s = max(1, -(-target // max(1, tiles)))
+    s = min(s, max(1, kred // 256), 32)
+    return s
+
+
+def linear_wgrad(dy, x, dW, *, accumulate_f32=None):
+    """dW[N,K] (fp16 view into the flat grad buffer) = dy[M,N]^T @ x[M,K] (split-K over M).
+    With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead."""
+    M, N = dy.shape
+    K = x.shape[1]
+    assert dW is None or tuple(dW.shape) == (N, K)
+    tiles = -(-N // 128) * -(-K // 128)
+    s = _splitk_for(tiles, M)
+    slabs = torch.empty(s, N, K, dtype=torch.float32, device=dy.device)
+    gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
+         epi=EPI_F32, splitk=s, sCsplit=N * K)
+    if accumulate_f32 is not None:
+        call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, accumulate_f32.data_ptr(),
+             accumulate_f32.stride(0), 2, 1.0, _s())
+        return accumulate_f32
+    call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, dW.data_ptr(), dW.stride(0), 1,
+         1.0, _s())
+    return dW
+
+
+def bias_grad(dy, db, accumulate=False):
+    """db[N] = sum_rows dy[M,N] (fp16 out, fp32 accumulation)."""
+    M, N = dy.shape
+    L = _lib.load()
+    nparts = L.mms2ut_colsum_nparts(M)
+    part = torch.empty(nparts, N, dtype=torch.float32, device=dy.device)
+    call("mms2ut_colsum_f16", dy.data_ptr(), M, N, dy.stride(0), part.data_ptr(), nparts, _s())
+    call("mms2ut_colsum_parts", part.data_ptr(), nparts, N, db.data_ptr(), int(accumulate), _s())
+    return db
+
+# ============================================================================ LayerNorm
+
+
+def layernorm(x, g, b, eps=1e-5):
+    R, D = x.shape
+    y = torch.empty_like(x)
+    mean = torch.empty(R, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+    call("mms2ut_layernorm_fwd", x.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), R, D, eps, _s())
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True):
+    """Returns dx (+dres). dgb: fp16 view of [dgamma | dbeta] (2*D contiguous)."""
+    R, D = x.shape
+    L = _lib.load()
+    nparts = L.mms2ut_layernorm_bwd_parts(R)
+    part = torch.empty(nparts, 2 * D, dtype=torch.float32, device=x.device)
+    dx = torch.empty_like(x) if want_dx else None
+    call("mms2ut_layernorm_bwd", dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr(),
+         rstd.data_ptr(), _p(dres), _p(dx), part.data_ptr(), R, D, _s())
+    call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), 0, _s())
+    return dx
+
+# ============================================================================ attention
+
+
+def attn_softmax(S, Z, H, Tq, Tk, ldS, key_len=None, key_mask=None, causal=False, extra_key=False,
+                 p=0.0, drop=None):
+    P = torch.empty_like(S)
+    Pd = torch.empty_like(S) if p > 0 else P
+    seed, off = drop if p > 0 else (0, 0)
+    call("mms2ut_attn_softmax_fwd", S.data_ptr(), P.data_ptr(), Pd.data_ptr(), Z, H, Tq, Tk, ldS,
+         _p(key_len), _p(key_mask), (key_mask.stride(0) if key_mask is not None else 0),
+         int(causal), int(extra_key), float(p), seed, off, _s())
+    return P, Pd
+
+
+def attn_softmax_bwd(P, dPd, Z, H, Tq, Tk, ldS, p=0.0, drop=None, out=None):
+    seed, off = drop if p > 0 else (0, 0)
+    dS = dPd if out is None else out
+    call("mms2ut_attn_softmax_bwd", P.data_ptr(), dPd.data_ptr(), dS.data_ptr(), Z, H, Tq, Tk, ldS,
+         None, 0, 0, float(p), seed, off, _s())
+    return dS
+
+# ============================================================================ elementwise
+
+
+def dropout(x, p, drop, out=None):
+    out = x if out is None else out
+    if p <= 0:
+        if out.data_ptr() != x.data_ptr():
+            out.copy_(x)
+        return out
+    seed, off = drop
+    call("mms2ut_dropout_fwd", x.data_ptr(), out.data_ptr(), x.numel(), float(p), seed, off, _s())
+    return out
+
+
+def dropout_mask(n, p, seed, offset, device):
+    m = torch.empty(n, dtype=torch.uint8, device=device)
+    call("mms2ut_dropout_mask", m.data_ptr(), n, float(p), int(seed), int(offset), _s())
+    return m
+
+
+def encoder_embed(h, pos_table, lens32, B, T, D, scale, p, drop):
+    x = torch.empty_like(h)
+    seed, off = drop if p > 0 else (0, 0)
+    call("mms2ut_encoder_embed_fwd", h.data_ptr(), pos_table.data_ptr(), lens32.data_ptr(),
+         x.data_ptr(), B, T, D, float(scale), float(p), seed, off, _s())
+    return x
+
+
+def scale_dropout_bwd(dx, scale, p, drop, out=None):
+    out = torch.empty_like(dx) if out is None else out
+    seed, off = drop if p > 0 else (0, 0)
+    call("mms2ut_scale_dropout_bwd", dx.data_ptr(), out.data_ptr(), dx.numel(), float(scale),
+         float(p), seed, off, _s())
+    return out
+
+
+def token_embed(tok, E, pos_table, B, T, D, pad, scale, p, drop):
+    x = torch.empty(B * T, D, dtype=F16, device=E.device)
+    seed, off = drop if p > 0 else (0, 0)
+    call("mms2ut_token_embed_fwd", tok.data_ptr(), E.data_ptr(), pos_table.data_ptr(), x.data_ptr(),
+         B, T, D, pad, float(scale), float(p), seed, off, _s())
+    return x
+
+
+def token_embed_bwd(tok, dx, dE32, B, T, D, pad, scale, p, drop):
+    seed, off = drop if p > 0 else (0, 0)
+    call("mms2ut_token_embed_bwd", tok.data_ptr(), dx.data_ptr(), dE32.data_ptr(), B, T, D, pad,
+         float(scale), float(p), seed, off, _s())
+
+
+def add_f32_to_f16(a, b32, out):
+    call("mms2ut_add_f32_to_f16", a.data_ptr(), b32.data_ptr(), out.data_ptr(), a.numel(), _s())
+    return out
+
+
+def add_f16(a, b, out=None):
+    out = torch.empty_like(a) if out is None else out
+    call("mms2ut_add_f16", a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), _s())
+    return out
+
+
+def glu(x, C):
+    rows = x.shape[0]
+    y = torch.empty(rows, C, dtype=F16, device=x.device)
+    call("mms2ut_glu_fwd", x.data_ptr(), y.data_ptr(), rows, C, _s())
+    return y
+
+
+def glu_bwd(x, dy, C):
+    rows = x.shape[0]
+    dx = torch.empty(rows, 2 * C, dtype=F16, device=x.device)
+    call("mms2ut_glu_bwd", x.data_ptr(), dy.data_ptr(), dx.data_ptr(), rows, C, _s())
+    return dx
+
+
+def im2col(x, B, Tin, Tout, C, k, stride=2, pad=None):
+    pad = k // 2 if pad is None else pad
+    col = torch.empty(B * Tout, C * k, dtype=F16, device=x.device)
+    call("mms2ut_im2col", x.data_ptr(), col.data_ptr(), B, Tin, Tout, C, k, stride, pad, _s())
+    return col
+
+
+def col2im(dcol, B, Tin, Tout, C, k, stride=2, pad=None):
+    pad = k // 2 if pad is None else pad
+    dx = torch.empty(B * Tin, C, dtype=F16, device=dcol.device)
+    call("mms2ut_col2im", dcol.data_ptr(), dx.data_ptr(), B, Tin, Tout, C, k, stride, pad, _s())
+    return dx
+
+
+def gate_bwd(dres, merge, g):
+    R, D = dres.shape
+    dpre = torch.empty_like(dres)
+    dmerge = torch.empty(R, 2 * D, dtype=F16, device=dres.device)
+    call("mms2ut_gate_bwd", dres.data_ptr(), merge.data_ptr(), g.data_ptr(), dpre.data_ptr(),
+         dmerge.data_ptr(), R, D, _s())
+    return dpre, dmerge
+
+
+def copy2d(src, dst, rows, cols):
+    call("mms2ut_copy2d", src.data_ptr(), src.stride(0), dst.data_ptr(), dst.stride(0), rows, cols,
+         _s())
+
+# ============================================================================ loss / optimizer
+
+
+def ls_xent_fwd(logits, ld, target, rows, V, eps, pad, loss_out):
+    lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    call("mms2ut_ls_xent_fwd", logits.data_ptr(), ld, target.data_ptr(), rows, V, float(eps), pad,
+         lse.data_ptr(), loss_out.data_ptr(), _s())
+    return lse
+
+
+def ls_xent_bwd(logits, ld, target, rows, V, eps, pad, lse, grad, out):
+    call("mms2ut_ls_xent_bwd", logits.data_ptr(), ld, target.data_ptr(), rows, V, float(eps), pad,
+         lse.data_ptr(), grad.data_ptr(), out.data_ptr(), _s())
+    return out
+
+
+OST_MULT, OST_GNORM, OST_OVERFLOW, OST_STEP, OST_STEP_SIZE, OST_LOSS_SCALE, OST_ITER, \
+    OST_LAST_OVERFLOW, OST_LAST_RESCALE, OST_CLIP_COEF, OST_FATAL = range(11)
+OST_SIZE = 16
+
+
+def grad_norm(grad, ost, sample_size=None, nparts=1024):
+    part = torch.empty(nparts, dtype=torch.float32, device=grad.device)
+    call("mms2ut_grad_sqnorm", grad.data_ptr(), grad.numel(), part.data_ptr(), nparts, _s())
+    call("mms2ut_grad_norm_finalize", part.data_ptr(), nparts, ost.data_ptr(), _p(sample_size), _s())
+
+
+def optim_prepare(ost, lr, beta1, beta2, clip, scale_window, min_scale):
+    call("mms2ut_optim_prepare", ost.data_ptr(), float(lr), float(beta1), float(beta2), float(clip),
+         float(scale_window), float(min_scale), _s())
+
+
+def adam(param, grad, master, m, v, ost, lr, beta1, beta2, eps, wd):
+    call("mms2ut_adam_fp16_master", param.data_ptr(), grad.data_ptr(), master.data_ptr(),
+         m.data_ptr(), v.data_ptr(), param.numel(), ost.data_ptr(), float(lr), float(beta1),
+         float(beta2), float(eps), float(wd), _s())
+
+# ============================================================================ fbank
+
+
+def fbank(wave, wave_off, frame_off, total_frames, banks, nbins=80):
+    feats = torch.empty(total_frames, nbins, dtype=torch.float32, device=wave.device)
+    B = wave_off.numel() - 1
+    call("mms2ut_fbank_f32", wave.data_ptr(), wave_off.data_ptr(), frame_off.data_ptr(), B,
+         total_frames, banks.data_ptr(), nbins, feats.data_ptr(), _s())
+    return feats
+
+
+def cmvn_collate(feats, frame_off, B, Tmax, nbins=80, cmvn=True):
+    out = torch.empty(B, Tmax, nbins, dtype=F16, device=feats.device)
+    call("mms2ut_fbank_cmvn_collate", feats.data_ptr(), frame_off.data_ptr(), B, Tmax, nbins,
+         int(cmvn), out.data_ptr(), _s())
+    return out
+
+
+def round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+__all__ = [n for n in dir() if not n.startswith("_")] + ["math"]

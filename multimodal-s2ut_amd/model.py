@@ -1,0 +1,823 @@
+"""MI355X-native mm_s2ut_transformer: parameters, forward and hand-written backward.
+
+The model is restated MI355X-first: all activations are batch-major ``[B*T, C]`` fp16 rows in HBM,
+every op is a libmms2ut_hip kernel (MFMA GEMMs with fused epilogues, wave-reduction LayerNorm /
+softmax, counter-RNG dropout), and the backward pass is written out by hand per layer (no
+autograd tape inside the model).  Parameters live in ONE flat fp16 buffer whose layout is the
+backward-completion order, so gradient buckets become ready front-to-back during backward
+(RCCL all-reduce overlap, see parallel.py).  Key names are those of the reference's
+``MM_S2UTTransformerModel.state_dict()`` (fairseq module tree) so checkpoints interchange.
+
+Reference path restated here:
+  MM_S2UTTransformerModel.forward            mm_s2ut/models/mm_s2s_transformer.py:667-700
+  MM_S2STransformerEncoder.forward           mm_s2s_transformer.py:378-562 (default S2T branch)
+    fairseq S2TTransformerEncoder._forward   (Conv1dSubsampler, sinusoidal pos, 12 pre-LN layers)
+    fusion tail                              mm_s2s_transformer.py:471-560
+    fuse_img_feat                            mm_s2s_transformer.py:594-622
+    SelectiveAttention / MultimodalAttention mm_s2ut/models/fuse.py:35-117 / 120-167
+  fairseq TransformerUnitDecoder             (6 pre-LN layers, tied output projection)
+"""
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .kernels import F16, round_up
+
+# ============================================================================ config
+
+
+def default_cfg(**over):
+    """`s2ut_architecture_base` + textless/1_train.sh flags + shipped fusion YAML
+    (mm_s2ut/config/multimodal_s2ut_transformer.yaml)."""
+    cfg = dict(
+        input_feat_per_channel=80, input_channels=1, conv_kernel_sizes=(5, 5), conv_channels=1024,
+        encoder_embed_dim=768, encoder_ffn_embed_dim=3072, encoder_layers=12,
+        encoder_attention_heads=8, decoder_embed_dim=768, decoder_ffn_embed_dim=3072,
+        decoder_layers=6, decoder_attention_heads=8, dropout=0.1, attention_dropout=0.1,
+        activation_dropout=0.1, vocab_size=1004, padding_idx=1, eos=2, label_smoothing=0.2,
+        fusion=True, multimodal_attention_type="multimodal_attention", use_selective_gate=True,
+        image_feat_dim=768, image_pre_norm=True, SA_image_dropout=0.1, SA_text_dropout=0.0,
+        SA_attention_dropout=0.1, modality_dropout=-0.5, audio_dropout=-0.5,
+        max_source_positions=6000, max_target_positions=3000, no_scale_embedding=False,
+    )
+    cfg.update(over)
+    return cfg
+
+# ============================================================================ parameter layout
+
+
+def param_specs(cfg):
+    """Ordered (name, shape) list in backward-completion order + the never-used params (Q3)."""
+    d, F_, C = cfg["encoder_embed_dim"], cfg["encoder_ffn_embed_dim"], cfg["conv_channels"]
+    dd, Fd, V = cfg["decoder_embed_dim"], cfg["decoder_ffn_embed_dim"], cfg["vocab_size"]
+    cin = cfg["input_feat_per_channel"] * cfg["input_channels"]
+    ks = cfg["conv_kernel_sizes"]
+    S = []
+
+    def mha(p, dm, kd):
+        # q, k, v adjacent (fused QKV / KV GEMMs), then biases q, k, v adjacent
+        S.extend([(f"{p}.q_proj.weight", (dm, dm)), (f"{p}.k_proj.weight", (dm, kd)),
+                  (f"{p}.v_proj.weight", (dm, kd)), (f"{p}.q_proj.bias", (dm,)),
+                  (f"{p}.k_proj.bias", (dm,)), (f"{p}.v_proj.bias", (dm,)),
+                  (f"{p}.out_proj.weight", (dm, dm)), (f"{p}.out_proj.bias", (dm,))])
+
+    def ln(p, n):
+        S.extend([(f"{p}.weight", (n,)), (f"{p}.bias", (n,))])
+
+    ln("decoder.layer_norm", dd)
+    for l in reversed(range(cfg["decoder_layers"])):
+        p = f"decoder.layers.{l}"
+        S.extend([(f"{p}.fc2.weight", (dd, Fd)), (f"{p}.fc2.bias", (dd,)),
+                  (f"{p}.fc1.weight", (Fd, dd)), (f"{p}.fc1.bias", (Fd,))])
+        ln(p + ".final_layer_norm", dd)
+        mha(p + ".encoder_attn", dd, d)
+        ln(p + ".encoder_attn_layer_norm", dd)
+        mha(p + ".self_attn", dd, dd)
+        ln(p + ".self_attn_layer_norm", dd)
+    S.append(("decoder.embed_tokens.weight", (V, dd)))
+    if cfg["fusion"]:
+        Di = cfg["image_feat_dim"]
+        S.extend([("encoder.gate_denses.0.weight", (d, 2 * d)), ("encoder.gate_denses.0.bias", (d,))])
+        if cfg["multimodal_attention_type"] == "multimodal_attention":
+            p = "encoder.multimodal_attns.0"
+            S.extend([(p + ".out_proj.weight", (d, d)), (p + ".out_proj.bias", (d,))])
+            if Di == d:
+                S.append((p + ".in_proj_weight", (3 * d, d)))
+            else:
+                S.extend([(p + ".q_proj_weight", (d, d)), (p + ".k_proj_weight", (d, Di)),
+                          (p + ".v_proj_weight", (d, Di))])
+            S.extend([(p + ".in_proj_bias", (3 * d,)), (p + ".bias_k", (1, 1, d)),
+                      (p + ".bias_v", (1, 1, d))])
+        elif cfg["multimodal_attention_type"] == "selective_attention":
+            p = "encoder.selective_attns.0"
+            S.extend([(p + ".proj.weight", (d, d)), (p + ".proj.bias", (d,)),
+                      (p + ".q_proj.weight", (d, d)), (p + ".k_proj.weight", (d, Di)),
+                      (p + ".v_proj.weight", (d, Di)), (p + ".q_proj.bias", (d,)),
+                      (p + ".k_proj.bias", (d,)), (p + ".v_proj.bias", (d,))])
+        else:
+            raise NotImplementedError(cfg["multimodal_attention_type"])
+        if cfg["image_pre_norm"]:
+            ln("encoder.image_pre_norm_module", Di)
+    ln("encoder.layer_norm", d)
+    for l in reversed(range(cfg["encoder_layers"])):
+        p = f"encoder.transformer_layers.{l}"
+        S.extend([(f"{p}.fc2.weight", (d, F_)), (f"{p}.fc2.bias", (d,)),
+                  (f"{p}.fc1.weight", (F_, d)), (f"{p}.fc1.bias", (F_,))])
+        ln(p + ".final_layer_norm", d)
+        mha(p + ".self_attn", d, d)
+        ln(p + ".self_attn_layer_norm", d)
+    for i in reversed(range(len(ks))):
+        ci = cin if i == 0 else C // 2
+        co = C if i < len(ks) - 1 else 2 * d
+        S.extend([(f"encoder.subsample.conv_layers.{i}.weight", (co, ci, ks[i])),
+                  (f"encoder.subsample.conv_layers.{i}.bias", (co,))])
+    unused = [("encoder.proj_768_to_512.weight", (512, 768)), ("encoder.proj_768_to_512.bias", (512,)),
+              ("encoder.proj_1024_to_512.weight", (512, 1024)), ("encoder.proj_1024_to_512.bias", (512,)),
+              ("encoder.proj_1024_to_768.weight", (768, 1024)), ("encoder.proj_1024_to_768.bias", (768,))]
+    for j in range(3):
+        unused.extend([(f"encoder.wav2vec2_adaptor.layers.{j}.weight", (1536, 1024 if j == 0 else 768, 3)),
+                       (f"encoder.wav2vec2_adaptor.layers.{j}.bias", (1536,))])
+    unused.extend([("encoder.wav2vec2_adaptor.layernorm.weight", (1024,)),
+                   ("encoder.wav2vec2_adaptor.layernorm.bias", (1024,))])
+    return S, unused
+
+
+class ParamStore:
+    """One flat fp16 parameter buffer + one flat fp16 gradient buffer with per-name views."""
+
+    ALIGN = 8  # elements (16 B) per parameter start: vector loads; keeps q|k|v spans contiguous
+
+    def __init__(self, specs, device, unused=()):
+        self.specs = list(specs)
+        self.offsets = OrderedDict()
+        off = 0
+        for name, shape in self.specs:
+            n = int(np.prod(shape))
+            self.offsets[name] = (off, tuple(shape), n)
+            off = round_up(off + n, self.ALIGN)
+        self.numel = off
+        self.flat = torch.zeros(self.numel, dtype=F16, device=device)
+        self.grad = torch.zeros(self.numel, dtype=F16, device=device)
+        self.unused = OrderedDict((n, torch.zeros(s, dtype=F16, device=device)) for n, s in unused)
+        self.p = {k: self.view(k) for k in self.offsets}
+        self.g = {k: self.view(k, grad=True) for k in self.offsets}
+
+    def view(self, name, grad=False):
+        off, shape, n = self.offsets[name]
+        buf = self.grad if grad else self.flat
+        return buf[off:off + n].view(shape)
+
+    def span(self, first, last, grad=False):
+        """Contiguous flat view from param `first` through `last` (inclusive)."""
+        a = self.offsets[first][0]
+        b = self.offsets[last][0] + self.offsets[last][2]
+        buf = self.grad if grad else self.flat
+        return buf[a:b]
+
+    def load_state_dict(self, sd, strict=True):
+        seen = set()
+        for k, v in sd.items():
+            if k in self.offsets:
+                self.p[k].copy_(v.to(self.p[k].dtype).view(self.p[k].shape))
+                seen.add(k)
+            elif k in self.unused:
+                self.unused[k].copy_(v.view(self.unused[k].shape))
+                seen.add(k)
+        missing = [k for k in self.offsets if k not in seen]
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:5]}...")
+        return missing
+
+    def state_dict(self):
+        sd = OrderedDict((k, v.detach().clone()) for k, v in self.p.items())
+        for k, v in self.unused.items():
+            sd[k] = v.detach().clone()
+        sd["decoder.output_projection.weight"] = sd["decoder.embed_tokens.weight"]
+        return sd
+
+
+def sinusoidal_table(num, dim, padding_idx=1):
+    """fairseq SinusoidalPositionalEmbedding.get_embedding (host constant, fp32 -> fp16)."""
+    half = dim // 2
+    emb = math.log(10000) / (half - 1)
+    emb = torch.exp(torch.arange(half, dtype=torch.float) * -emb)
+    emb = torch.arange(num, dtype=torch.float).unsqueeze(1) * emb.unsqueeze(0)
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=1).view(num, -1)
+    if dim % 2 == 1:
+        emb = torch.cat([emb, torch.zeros(num, 1)], dim=1)
+    emb[padding_idx, :] = 0
+    return emb
+
+# ============================================================================ attention core
+
+
+def attn_fwd(q, k, v, ldq, ldk, ldv, B, H, Tq, Tk, hd, scale, out, ldo, *, key_len=None,
+             key_mask=None, causal=False, extra_key=False, p=0.0, drop=None,
+             sq=None, sk=None, so=None):
+    """softmax(scale*q k^T + masks) -> dropout -> @ v, batched over (b, h).
+    q/k/v/out are views whose row r=(b*T + t) and head column offset h*hd; `s*` = batch strides."""
+    ldS = round_up(Tk, 8)
+    sq = sq or Tq * ldq
+    sk = sk or Tk * ldk
+    so = so or Tq * ldo
+    S = torch.empty(B * H * Tq * ldS, dtype=F16, device=q.device)
+    K.gemm(q, k, S, Tq, Tk, hd, lda=ldq, ldb=ldk, ldc=ldS, batch=B * H, bdiv=H,
+           sA=(sq, hd), sB=(sk, hd), sC=(H * Tq * ldS, Tq * ldS), alpha=scale)
+    P, Pd = K.attn_softmax(S, B * H, H, Tq, Tk, ldS, key_len=key_len, key_mask=key_mask,
+                           causal=causal, extra_key=extra_key, p=p, drop=drop)
+    del S
+    K.gemm(Pd, v, out, Tq, hd, Tk, a_kc=True, b_kc=False, lda=ldS, ldb=ldv, ldc=ldo, batch=B * H,
+           bdiv=H, sA=(H * Tq * ldS, Tq * ldS), sB=(Tk * ldv if sk is None else sk, hd), sC=(so, hd))
+    return P, Pd, ldS
+
+
+def attn_bwd(dO, ldo, q, k, v, ldq, ldk, ldv, P, Pd, ldS, B, H, Tq, Tk, hd, scale, dq, dk, dv,
+             lddq, lddk, lddv, *, p=0.0, drop=None, sq=None, sk=None, so=None, sdq=None, sdk=None):
+    sq = sq or Tq * ldq
+    sk = sk or Tk * ldk
+    so = so or Tq * ldo
+    sdq = sdq or Tq * lddq
+    sdk = sdk or Tk * lddk
+    sS = (H * Tq * ldS, Tq * ldS)
+    dPd = torch.empty_like(P)
+    # dPd = dO v^T
+    K.gemm(dO, v, dPd, Tq, Tk, hd, lda=ldo, ldb=ldv, ldc=ldS, batch=B * H, bdiv=H,
+           sA=(so, hd), sB=(sk, hd), sC=sS)
+    # dv = Pd^T dO
+    K.gemm(Pd, dO, dv, Tk, hd, Tq, a_kc=False, b_kc=False, lda=ldS, ldb=ldo, ldc=lddv,
+           batch=B * H, bdiv=H, sA=sS, sB=(so, hd), sC=(sdk, hd))
+    dS = K.attn_softmax_bwd(P, dPd, B * H, H, Tq, Tk, ldS, p=p, drop=drop)
+    # dq = scale * dS k
+    K.gemm(dS, k, dq, Tq, hd, Tk, a_kc=True, b_kc=False, lda=ldS, ldb=ldk, ldc=lddq,
+           batch=B * H, bdiv=H, sA=sS, sB=(sk, hd), sC=(sdq, hd), alpha=scale)
+    # dk = scale * dS^T q
+    K.gemm(dS, q, dk, Tk, hd, Tq, a_kc=False, b_kc=False, lda=ldS, ldb=ldq, ldc=lddk,
+           batch=B * H, bdiv=H, sA=sS, sB=(sq, hd), sC=(sdk, hd), alpha=scale)
+
+# ============================================================================ the model
+
+
+class MMS2UTModel:
+    """Parameters + explicit forward/backward of MM_S2UTTransformerModel on one GPU."""
+
+    def __init__(self, cfg, device="cuda", seed=1):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        specs, unused = param_specs(cfg)
+        self.params = ParamStore(specs, self.device, unused)
+        self.drop = K.Dropout(seed)
+        self.training = True
+        d, dd = cfg["encoder_embed_dim"], cfg["decoder_embed_dim"]
+        self.enc_pos = sinusoidal_table(cfg["max_source_positions"] + 2, d).to(self.device, F16)
+        self.dec_pos = sinusoidal_table(cfg["max_target_positions"] + 2, dd).to(self.device, F16)
+        self.np_rng = np.random  # modality-dropout draws use the global numpy stream (reference)
+        # autograd anchor: the model's output is connected to the graph through this leaf
+        self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
+
+    def init_params(self, seed=1):
+        """Random init with fairseq's schemes (random-init weights of the architecture; no
+        checkpoints are reachable offline): xavier for attention projections (gain 1/sqrt(2) for
+        q/k/v), nn.Linear default for FFN/conv, N(0, d^-0.5) embedding with a zero pad row,
+        LayerNorm (1, 0), zero biases for out_proj."""
+        g = torch.Generator().manual_seed(seed)
+        sd = {}
+        for name, shape in self.params.specs:
+            if name.endswith("layer_norm.weight") or name.endswith("image_pre_norm_module.weight"):
+                t = torch.ones(shape)
+            elif name.endswith(".bias") and ("layer_norm" in name or "out_proj" in name or "image_pre_norm" in name):
+                t = torch.zeros(shape)
+            elif name == "decoder.embed_tokens.weight":
+                t = torch.randn(shape, generator=g) * shape[1] ** -0.5
+                t[self.cfg["padding_idx"]] = 0
+            elif len(shape) >= 2:
+                fan_out, fan_in = shape[0], int(np.prod(shape[1:]))
+                if any(s in name for s in ("q_proj", "k_proj", "v_proj", "in_proj", "out_proj", "gate_denses")):
+                    gain = 1 / math.sqrt(2) if "out_proj" not in name and "gate" not in name else 1.0
+                    a = gain * math.sqrt(6.0 / (fan_in + fan_out))
+                else:
+                    a = 1.0 / math.sqrt(fan_in)
+                t = (torch.rand(shape, generator=g) * 2 - 1) * a
+            elif name.endswith("bias_k") or name.endswith("bias_v"):
+                t = torch.randn(shape, generator=g) * math.sqrt(2.0 / (1 + shape[-1]))
+            else:
+                t = (torch.rand(shape, generator=g) * 2 - 1) * 0.02
+            sd[name] = t
+        for name, t in self.params.unused.items():
+            sd[name] = (torch.rand(t.shape, generator=g) * 2 - 1) * 0.02
+        self.params.load_state_dict(sd)
+        return self
+
+    def train(self, mode=True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    # -------------------------------------------------------------- helpers
+    grad_ready_hook = None  # callable(offset): grads [0, offset) of the flat buffer are final
+
+    def _ready(self, last_param=None):
+        if self.grad_ready_hook is None:
+            return
+        if last_param is None:
+            self.grad_ready_hook(self.params.numel)
+        else:
+            off, _, n = self.params.offsets[last_param]
+            self.grad_ready_hook(off + n)
+
+    def P(self, n):
+        return self.params.p[n]
+
+    def G(self, n):
+        return self.params.g[n]
+
+    def _p(self, key):
+        return self.cfg[key] if self.training else 0.0
+
+    def _drop(self, p, n):
+        return self.drop.take(n) if p > 0 else None
+
+    def _ensure_pos(self, T, which):
+        tab = self.enc_pos if which == "enc" else self.dec_pos
+        if T + 2 > tab.shape[0]:
+            dim = tab.shape[1]
+            tab = sinusoidal_table(T + 2, dim).to(self.device, F16)
+            if which == "enc":
+                self.enc_pos = tab
+            else:
+                self.dec_pos = tab
+        return tab
+
+    # -------------------------------------------------------------- subsampler
+    def subsample_fwd(self, src, lens):
+        """fairseq Conv1dSubsampler: conv(k, s2, p k//2) -> GLU, twice; implicit GEMM."""
+        cfg = self.cfg
+        B, Ts, Cin = src.shape
+        ctx = {"B": B, "Ts": Ts, "layers": []}
+        x = src.reshape(B * Ts, Cin)
+        Tin, C = Ts, Cin
+        for i, k in enumerate(cfg["conv_kernel_sizes"]):
+            W = self.P(f"encoder.subsample.conv_layers.{i}.weight")
+            bias = self.P(f"encoder.subsample.conv_layers.{i}.bias")
+            Tout = (Tin - 1) // 2 + 1
+            col = K.im2col(x, B, Tin, Tout, C, k)
+            y = K.linear(col, W.view(W.shape[0], -1), bias)
+            Cg = W.shape[0] // 2
+            g = K.glu(y, Cg)
+            ctx["layers"].append(dict(col=col, y=y, Tin=Tin, Tout=Tout, C=C, k=k, Cg=Cg))
+            x, Tin, C = g, Tout, Cg
+        return x, Tin, ctx
+
+    def subsample_bwd(self, ctx, dx):
+        B = ctx["B"]
+        for i in reversed(range(len(ctx["layers"]))):
+            L = ctx["layers"][i]
+            W = self.P(f"encoder.subsample.conv_layers.{i}.weight")
+            dy = K.glu_bwd(L["y"], dx, L["Cg"])
+            K.linear_wgrad(dy, L["col"], self.G(f"encoder.subsample.conv_layers.{i}.weight").view(W.shape[0], -1))
+            K.bias_grad(dy, self.G(f"encoder.subsample.conv_layers.{i}.bias"))
+            if i > 0:
+                dcol = K.linear_dgrad(dy, W.view(W.shape[0], -1))
+                dx = K.col2im(dcol, B, L["Tin"], L["Tout"], L["C"], L["k"])
+
+    # -------------------------------------------------------------- encoder layer
+    def enc_layer_fwd(self, l, x, B, T, lens32):
+        cfg = self.cfg
+        p = f"encoder.transformer_layers.{l}"
+        d, H = cfg["encoder_embed_dim"], cfg["encoder_attention_heads"]
+        hd = d // H
+        R = B * T
+        c = {"x": x}
+        h1, c["m1"], c["r1"] = K.layernorm(x, self.P(p + ".self_attn_layer_norm.weight"),
+                                           self.P(p + ".self_attn_layer_norm.bias"))
+        c["h1"] = h1
+        Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
+        bqkv = self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias")
+        qkv = K.linear(h1, Wqkv, bqkv)
+        c["qkv"] = qkv
+        O = torch.empty(R, d, dtype=F16, device=x.device)
+        pa = self._p("attention_dropout")
+        c["drop_attn"] = self._drop(pa, B * H * T * T)
+        c["P"], c["Pd"], c["ldS"] = attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H,
+                                             T, T, hd, hd ** -0.5, O, d, key_len=lens32, p=pa,
+                                             drop=c["drop_attn"])
+        c["O"] = O
+        pd = self._p("dropout")
+        c["drop1"] = self._drop(pd, R * d)
+        x2 = K.linear(O, self.P(p + ".self_attn.out_proj.weight"), self.P(p + ".self_attn.out_proj.bias"),
+                      epi=K.EPI_DROP_RESID, aux=x, p=pd, drop=c["drop1"])
+        c["x2"] = x2
+        h2, c["m2"], c["r2"] = K.layernorm(x2, self.P(p + ".final_layer_norm.weight"),
+                                           self.P(p + ".final_layer_norm.bias"))
+        c["h2"] = h2
+        pact = self._p("activation_dropout")
+        c["drop_act"] = self._drop(pact, R * cfg["encoder_ffn_embed_dim"])
+        f1 = K.linear(h2, self.P(p + ".fc1.weight"), self.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP,
+                      p=pact, drop=c["drop_act"])
+        c["f1"] = f1
+        c["drop2"] = self._drop(pd, R * d)
+        x3 = K.linear(f1, self.P(p + ".fc2.weight"), self.P(p + ".fc2.bias"), epi=K.EPI_DROP_RESID,
+                      aux=x2, p=pd, drop=c["drop2"])
+        c.update(B=B, T=T, lens32=lens32, pd=pd, pa=pa, pact=pact)
+        return x3, c
+
+    def enc_layer_bwd(self, l, c, dx3):
+        cfg = self.cfg
+        p = f"encoder.transformer_layers.{l}"
+        d, H = cfg["encoder_embed_dim"], cfg["encoder_attention_heads"]
+        hd = d // H
+        B, T = c["B"], c["T"]
+        pd, pa, pact = c["pd"], c["pa"], c["pact"]
+        # fc2 / fc1
+        dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
+        K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"))
+        K.bias_grad(dy2, self.G(p + ".fc2.bias"))
+        df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
+        K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"))
+        K.bias_grad(df1, self.G(p + ".fc1.bias"))
+        dh2 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
+        del df1
+        dx2 = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".final_layer_norm.weight"), c["m2"], c["r2"],
+                              self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
+                              dres=dx3)
+        # out proj
+        dyo = K.dropout(dx2, pd, c["drop1"], out=torch.empty_like(dx2)) if pd > 0 else dx2
+        K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"))
+        K.bias_grad(dyo, self.G(p + ".self_attn.out_proj.bias"))
+        dO = K.linear_dgrad(dyo, self.P(p + ".self_attn.out_proj.weight"))
+        qkv = c["qkv"]
+        dqkv = torch.empty_like(qkv)
+        attn_bwd(dO, d, qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, c["P"], c["Pd"], c["ldS"],
+                 B, H, T, T, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
+                 p=pa, drop=c["drop_attn"])
+        Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
+        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
+        K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+        dh1 = K.linear_dgrad(dqkv, Wqkv)
+        dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
+                             self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
+                             dres=dx2)
+        return dx
+
+    # -------------------------------------------------------------- fusion (fuse_img_feat)
+    def fusion_fwd(self, text, img, img_mask, B, Te):
+        """mm_s2s_transformer.py:594-622. text [B*Te, d] (encoder out), img [B, Ti, Di] fp16."""
+        cfg = self.cfg
+        d = cfg["encoder_embed_dim"]
+        _, Ti, Di = img.shape
+        att = cfg["multimodal_attention_type"]
+        extra = att == "multimodal_attention"  # add_bias_kv: one learned key/value row
+        Tk = Ti + 1 if extra else Ti
+        c = {"B": B, "Te": Te, "Ti": Ti, "Di": Di, "Tk": Tk, "extra": extra}
+        # image_pre_norm (+ dropout), laid out [B, Tk, Di] with a zero row per batch for bias_kv
+        img2 = img.reshape(B * Ti, Di)
+        if cfg["image_pre_norm"]:
+            imgn, c["im"], c["ir"] = K.layernorm(img2, self.P("encoder.image_pre_norm_module.weight"),
+                                                 self.P("encoder.image_pre_norm_module.bias"))
+            c["img_in"] = img2
+        else:
+            imgn = img2
+        pimg = self._p("SA_image_dropout")
+        c["drop_img"] = self._drop(pimg, B * Ti * Di)
+        if pimg > 0:
+            imgn = K.dropout(imgn, pimg, c["drop_img"])
+        if extra:
+            imgd = torch.zeros(B, Tk, Di, dtype=F16, device=img.device)
+            K.copy2d(imgn, imgd.view(B, Tk * Di), B, Ti * Di)
+            imgd = imgd.view(B * Tk, Di)
+        else:
+            imgd = imgn
+        c["imgd"] = imgd
+        ptxt = self._p("SA_text_dropout")
+        c["drop_txt"] = self._drop(ptxt, B * Te * d)
+        textd = K.dropout(text, ptxt, c["drop_txt"], out=torch.empty_like(text)) if ptxt > 0 else text
+        c["textd"] = textd
+        if extra:
+            pre = "encoder.multimodal_attns.0"
+            if Di == d:
+                W = self.P(pre + ".in_proj_weight")
+                Wq, Wkv = W[:d], W[d:]
+            else:
+                Wq = self.P(pre + ".q_proj_weight")
+                Wkv = self.params.span(pre + ".k_proj_weight", pre + ".v_proj_weight").view(2 * d, Di)
+            bias = self.P(pre + ".in_proj_bias")
+            bq, bkv = bias[:d], bias[d:]
+            Wo, bo = self.P(pre + ".out_proj.weight"), self.P(pre + ".out_proj.bias")
+        else:
+            pre = "encoder.selective_attns.0"
+            Wq, bq = self.P(pre + ".q_proj.weight"), self.P(pre + ".q_proj.bias")
+            Wkv = self.params.span(pre + ".k_proj.weight", pre + ".v_proj.weight").view(2 * d, Di)
+            bkv = self.params.span(pre + ".k_proj.bias", pre + ".v_proj.bias")
+            Wo, bo = self.P(pre + ".proj.weight"), self.P(pre + ".proj.bias")
+        c["pre"] = pre
+        q = K.linear(textd, Wq, bq)
+        kv = K.linear(imgd, Wkv, bkv)                      # [B*Tk, 2d]
+        if extra:
+            bkv_rows = self.params.span(pre + ".bias_k", pre + ".bias_v").view(1, 2 * d)
+            K.copy2d(bkv_rows.expand(B, 2 * d), kv.view(B, Tk * 2 * d)[:, Ti * 2 * d:], B, 2 * d)
+        c["q"], c["kv"] = q, kv
+        key_mask = img_mask  # uint8 [B, >=Tk] prepared by prepare_batch (1 = padded key)
+        c["key_mask"] = key_mask
+        pat = self._p("SA_attention_dropout")
+        c["drop_attn"] = self._drop(pat, B * Te * Tk)
+        O = torch.empty(B * Te, d, dtype=F16, device=text.device)
+        c["P"], c["Pd"], c["ldS"] = attn_fwd(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, 1, Te, Tk, d,
+                                             d ** -0.5, O, d, key_mask=key_mask, extra_key=extra,
+                                             p=pat, drop=c["drop_attn"])
+        c["O"], c["pat"], c["pimg"], c["ptxt"] = O, pat, pimg, ptxt
+        if cfg["use_selective_gate"]:
+            merge = torch.empty(B * Te, 2 * d, dtype=F16, device=text.device)
+            K.linear(O, Wo, bo, out=merge[:, :d], ldc=2 * d)
+            K.copy2d(textd, merge[:, d:], B * Te, d)
+            g = torch.empty(B * Te, d, dtype=F16, device=text.device)
+            res = K.linear(merge, self.P("encoder.gate_denses.0.weight"), self.P("encoder.gate_denses.0.bias"),
+                           epi=K.EPI_GATE, aux=merge, out2=g)
+            c["merge"], c["g"] = merge, g
+        else:
+            res = K.linear(O, Wo, bo, epi=K.EPI_DROP_RESID, aux=textd)
+        return res, c
+
+    def fusion_bwd(self, c, dres):
+        cfg = self.cfg
+        d = cfg["encoder_embed_dim"]
+        B, Te, Ti, Di, Tk, extra, pre = c["B"], c["Te"], c["Ti"], c["Di"], c["Tk"], c["extra"], c["pre"]
+        if extra:
+            if Di == d:
+                W = self.P(pre + ".in_proj_weight")
+                Wq, Wkv = W[:d], W[d:]
+                gW = self.G(pre + ".in_proj_weight")
+                gWq, gWkv = gW[:d], gW[d:]
+            else:
+                Wq = self.P(pre + ".q_proj_weight")
+                Wkv = self.params.span(pre + ".k_proj_weight", pre + ".v_proj_weight").view(2 * d, Di)
+                gWq = self.G(pre + ".q_proj_weight")
+                gWkv = self.params.span(pre + ".k_proj_weight", pre + ".v_proj_weight", grad=True).view(2 * d, Di)
+            gb = self.G(pre + ".in_proj_bias")
+            gbq, gbkv = gb[:d], gb[d:]
+            Wo, gWo, gbo = self.P(pre + ".out_proj.weight"), self.G(pre + ".out_proj.weight"), self.G(pre + ".out_proj.bias")
+        else:
+            Wq, gWq, gbq = self.P(pre + ".q_proj.weight"), self.G(pre + ".q_proj.weight"), self.G(pre + ".q_proj.bias")
+            Wkv = self.params.span(pre + ".k_proj.weight", pre + ".v_proj.weight").view(2 * d, Di)
+            gWkv = self.params.span(pre + ".k_proj.weight", pre + ".v_proj.weight", grad=True).view(2 * d, Di)
+            gbkv = self.params.span(pre + ".k_proj.bias", pre + ".v_proj.bias", grad=True)
+            Wo, gWo, gbo = self.P(pre + ".proj.weight"), self.G(pre + ".proj.weight"), self.G(pre + ".proj.bias")
+        if cfg["use_selective_gate"]:
+            dpre, dmerge = K.gate_bwd(dres, c["merge"], c["g"])
+            K.linear_wgrad(dpre, c["merge"], self.G("encoder.gate_denses.0.weight"))
+            K.bias_grad(dpre, self.G("encoder.gate_denses.0.bias"))
+            K.linear_dgrad(dpre, self.P("encoder.gate_denses.0.weight"), out=dmerge, accumulate=True)
+            dOp = dmerge[:, :d]
+            dtext = dmerge[:, d:]
+        else:
+            dOp = dres
+            dtext = dres
+        K.linear_wgrad(dOp, c["O"], gWo)
+        K.bias_grad(dOp, gbo)
+        dO = K.linear_dgrad(dOp, Wo)
+        q, kv = c["q"], c["kv"]
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        attn_bwd(dO, d, q, kv, kv[:, d:], d, 2 * d, 2 * d, c["P"], c["Pd"], c["ldS"], B, 1, Te, Tk, d,
+                 d ** -0.5, dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=c["pat"], drop=c["drop_attn"])
+        if extra:
+            # bias_k / bias_v grads = sum over batch of the extra key row; then zero that row
+            rows = dkv.view(B, Tk * 2 * d)[:, Ti * 2 * d:]
+            K.bias_grad(rows, self.params.span(pre + ".bias_k", pre + ".bias_v", grad=True))
+            rows.zero_()
+        K.linear_wgrad(dkv, c["imgd"], gWkv)
+        K.bias_grad(dkv, gbkv)
+        if cfg["image_pre_norm"]:
+            dimgd = K.linear_dgrad(dkv, Wkv)
+            if extra:
+                dimg = torch.empty(B * Ti, Di, dtype=F16, device=dkv.device)
+                K.copy2d(dimgd.view(B, Tk * Di), dimg.view(B, Ti * Di), B, Ti * Di)
+            else:
+                dimg = dimgd
+            if c["pimg"] > 0:
+                dimg = K.dropout(dimg, c["pimg"], c["drop_img"])
+            K.layernorm_bwd(dimg, c["img_in"], self.P("encoder.image_pre_norm_module.weight"), c["im"], c["ir"],
+                            self.params.span("encoder.image_pre_norm_module.weight",
+                                             "encoder.image_pre_norm_module.bias", grad=True),
+                            want_dx=False)
+        K.linear_wgrad(dq, c["textd"], gWq)
+        K.bias_grad(dq, gbq)
+        dtext_total = torch.empty(B * Te, d, dtype=F16, device=dres.device)
+        K.copy2d(dtext, dtext_total, B * Te, d)
+        K.linear_dgrad(dq, Wq, out=dtext_total, accumulate=True)
+        if c["ptxt"] > 0:
+            dtext_total = K.dropout(dtext_total, c["ptxt"], c["drop_txt"])
+        return dtext_total
+
+    # -------------------------------------------------------------- decoder layer
+    def dec_layer_fwd(self, l, x, enc, B, Tt, Te, tgt_mask, enc_len32):
+        cfg = self.cfg
+        p = f"decoder.layers.{l}"
+        d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
+        hd = d // H
+        R = B * Tt
+        pd, pa, pact = self._p("dropout"), self._p("attention_dropout"), self._p("activation_dropout")
+        c = {"x": x, "B": B, "Tt": Tt, "Te": Te, "pd": pd, "pa": pa, "pact": pact}
+        # self attention (causal + target padding)
+        h1, c["m1"], c["r1"] = K.layernorm(x, self.P(p + ".self_attn_layer_norm.weight"), self.P(p + ".self_attn_layer_norm.bias"))
+        c["h1"] = h1
+        Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
+        bqkv = self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias")
+        qkv = K.linear(h1, Wqkv, bqkv)
+        c["qkv"] = qkv
+        O = torch.empty(R, d, dtype=F16, device=x.device)
+        c["drop_sa"] = self._drop(pa, B * H * Tt * Tt)
+        c["sP"], c["sPd"], c["sldS"] = attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Tt, Tt,
+                                                hd, hd ** -0.5, O, d, key_mask=tgt_mask, causal=True, p=pa,
+                                                drop=c["drop_sa"])
+        c["sO"] = O
+        c["drop1"] = self._drop(pd, R * d)
+        x2 = K.linear(O, self.P(p + ".self_attn.out_proj.weight"), self.P(p + ".self_attn.out_proj.bias"),
+                      epi=K.EPI_DROP_RESID, aux=x, p=pd, drop=c["drop1"])
+        c["x2"] = x2
+        # encoder attention
+        h2, c["m2"], c["r2"] = K.layernorm(x2, self.P(p + ".encoder_attn_layer_norm.weight"), self.P(p + ".encoder_attn_layer_norm.bias"))
+        c["h2"] = h2
+        q = K.linear(h2, self.P(p + ".encoder_attn.q_proj.weight"), self.P(p + ".encoder_attn.q_proj.bias"))
+        de = cfg["encoder_embed_dim"]
+        Wkv = self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight").view(2 * d, de)
+        bkv = self.params.span(p + ".encoder_attn.k_proj.bias", p + ".encoder_attn.v_proj.bias")
+        kv = K.linear(enc, Wkv, bkv)
+        c["q"], c["kv"] = q, kv
+        O2 = torch.empty(R, d, dtype=F16, device=x.device)
+        c["drop_ca"] = self._drop(pa, B * H * Tt * Te)
+        c["cP"], c["cPd"], c["cldS"] = attn_fwd(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tt, Te, hd, hd ** -0.5,
+                                                O2, d, key_len=enc_len32, p=pa, drop=c["drop_ca"])
+        c["cO"] = O2
+        c["drop2"] = self._drop(pd, R * d)
+        x3 = K.linear(O2, self.P(p + ".encoder_attn.out_proj.weight"), self.P(p + ".encoder_attn.out_proj.bias"),
+                      epi=K.EPI_DROP_RESID, aux=x2, p=pd, drop=c["drop2"])
+        c["x3"] = x3
+        # FFN
+        h3, c["m3"], c["r3"] = K.layernorm(x3, self.P(p + ".final_layer_norm.weight"), self.P(p + ".final_layer_norm.bias"))
+        c["h3"] = h3
+        c["drop_act"] = self._drop(pact, R * cfg["decoder_ffn_embed_dim"])
+        f1 = K.linear(h3, self.P(p + ".fc1.weight"), self.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP, p=pact,
+                      drop=c["drop_act"])
+        c["f1"] = f1
+        c["drop3"] = self._drop(pd, R * d)
+        x4 = K.linear(f1, self.P(p + ".fc2.weight"), self.P(p + ".fc2.bias"), epi=K.EPI_DROP_RESID, aux=x3,
+                      p=pd, drop=c["drop3"])
+        return x4, c
+
+    def dec_layer_bwd(self, l, c, dx4, denc, enc):
+        """Returns dx; accumulates the cross-attention K/V dgrad into denc [B*Te, de]."""
+        cfg = self.cfg
+        p = f"decoder.layers.{l}"
+        d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
+        hd = d // H
+        B, Tt, Te = c["B"], c["Tt"], c["Te"]
+        pd, pa, pact = c["pd"], c["pa"], c["pact"]
+        dy3 = K.dropout(dx4, pd, c["drop3"], out=torch.empty_like(dx4)) if pd > 0 else dx4
+        K.linear_wgrad(dy3, c["f1"], self.G(p + ".fc2.weight"))
+        K.bias_grad(dy3, self.G(p + ".fc2.bias"))
+        df1 = K.linear_dgrad(dy3, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
+        K.linear_wgrad(df1, c["h3"], self.G(p + ".fc1.weight"))
+        K.bias_grad(df1, self.G(p + ".fc1.bias"))
+        dh3 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
+        del df1
+        dx3 = K.layernorm_bwd(dh3, c["x3"], self.P(p + ".final_layer_norm.weight"), c["m3"], c["r3"],
+                              self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
+                              dres=dx4)
+        # encoder attention
+        dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
+        K.linear_wgrad(dy2, c["cO"], self.G(p + ".encoder_attn.out_proj.weight"))
+        K.bias_grad(dy2, self.G(p + ".encoder_attn.out_proj.bias"))
+        dO2 = K.linear_dgrad(dy2, self.P(p + ".encoder_attn.out_proj.weight"))
+        q, kv = c["q"], c["kv"]
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        attn_bwd(dO2, d, q, kv, kv[:, d:], d, 2 * d, 2 * d, c["cP"], c["cPd"], c["cldS"], B, H, Tt, Te, hd,
+                 hd ** -0.5, dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pa, drop=c["drop_ca"])
+        de = cfg["encoder_embed_dim"]
+        Wkv = self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight").view(2 * d, de)
+        K.linear_wgrad(dkv, enc, self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight", grad=True).view(2 * d, de))
+        K.bias_grad(dkv, self.params.span(p + ".encoder_attn.k_proj.bias", p + ".encoder_attn.v_proj.bias", grad=True))
+        K.linear_dgrad(dkv, Wkv, out=denc, accumulate=True)
+        K.linear_wgrad(dq, c["h2"], self.G(p + ".encoder_attn.q_proj.weight"))
+        K.bias_grad(dq, self.G(p + ".encoder_attn.q_proj.bias"))
+        dh2 = K.linear_dgrad(dq, self.P(p + ".encoder_attn.q_proj.weight"))
+        dx2 = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".encoder_attn_layer_norm.weight"), c["m2"], c["r2"],
+                              self.params.span(p + ".encoder_attn_layer_norm.weight", p + ".encoder_attn_layer_norm.bias", grad=True),
+                              dres=dx3)
+        # self attention
+        dy1 = K.dropout(dx2, pd, c["drop1"], out=torch.empty_like(dx2)) if pd > 0 else dx2
+        K.linear_wgrad(dy1, c["sO"], self.G(p + ".self_attn.out_proj.weight"))
+        K.bias_grad(dy1, self.G(p + ".self_attn.out_proj.bias"))
+        dO = K.linear_dgrad(dy1, self.P(p + ".self_attn.out_proj.weight"))
+        qkv = c["qkv"]
+        dqkv = torch.empty_like(qkv)
+        attn_bwd(dO, d, qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, c["sP"], c["sPd"], c["sldS"], B, H,
+                 Tt, Tt, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pa,
+                 drop=c["drop_sa"])
+        Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
+        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
+        K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+        dh1 = K.linear_dgrad(dqkv, Wqkv)
+        dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
+                             self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
+                             dres=dx2)
+        return dx
+
+    # -------------------------------------------------------------- full model
+    def encoder_forward(self, batch):
+        """Returns (enc [B*Te, d], enc_len32, Te, ctx) for a DeviceBatch (runtime.prepare_batch)."""
+        cfg = self.cfg
+        d = cfg["encoder_embed_dim"]
+        src_tokens = batch.src
+        imgs, img_mask = batch.imgs, batch.img_keymask
+        B = src_tokens.shape[0]
+        ctx = {}
+        h, Te, ctx["sub"] = self.subsample_fwd(src_tokens, None)
+        assert Te == batch.Te, (Te, batch.Te)
+        lens32 = batch.enc_len32
+        ctx["lens32"] = lens32
+        pos = self._ensure_pos(Te, "enc")
+        scale = 1.0 if cfg["no_scale_embedding"] else math.sqrt(d)
+        pd = self._p("dropout")
+        ctx["drop_emb"] = self._drop(pd, B * Te * d)
+        x = K.encoder_embed(h, pos, lens32, B, Te, d, scale, pd, ctx["drop_emb"])
+        ctx["emb"] = (scale, pd)
+        ctx["layers"] = []
+        for l in range(cfg["encoder_layers"]):
+            x, c = self.enc_layer_fwd(l, x, B, Te, lens32)
+            ctx["layers"].append(c)
+        xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("encoder.layer_norm.weight"), self.P("encoder.layer_norm.bias"))
+        ctx["lx"] = x
+        ctx["fusion"] = None
+        out = xl
+        if cfg["fusion"] and imgs is not None:
+            # modality dropout (mm_s2s_transformer.py:496-512): two host draws every training forward
+            if self.training:
+                mod_p, aud_p = self.np_rng.random(), self.np_rng.random()
+                if mod_p < cfg["modality_dropout"]:
+                    if aud_p < cfg["audio_dropout"]:
+                        # reference raises UnboundLocalError here; intent: zero audio
+                        ctx["audio_dropped"] = True
+                        out = torch.zeros_like(xl)
+                    else:
+                        imgs = torch.zeros_like(imgs)   # LN of zeros -> beta (Q5), as reference
+            res, ctx["fusion"] = self.fusion_fwd(out, imgs, img_mask, B, Te)
+            out = res
+        ctx["B"], ctx["Te"] = B, Te
+        return out, lens32, Te, ctx
+
+    def encoder_backward(self, ctx, denc):
+        if ctx["fusion"] is not None:
+            denc = self.fusion_bwd(ctx["fusion"], denc)
+            if ctx.get("audio_dropped"):
+                denc = torch.zeros_like(denc)
+        last_fusion = [n for n, _ in self.params.specs if n.startswith(("encoder.gate", "encoder.multimodal",
+                                                                         "encoder.selective", "encoder.image"))]
+        if last_fusion:
+            self._ready(last_fusion[-1])
+        dx = K.layernorm_bwd(denc, ctx["lx"], self.P("encoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
+                             self.params.span("encoder.layer_norm.weight", "encoder.layer_norm.bias", grad=True))
+        self._ready("encoder.layer_norm.bias")
+        for l in reversed(range(self.cfg["encoder_layers"])):
+            dx = self.enc_layer_bwd(l, ctx["layers"][l], dx)
+            ctx["layers"][l] = None
+            self._ready(f"encoder.transformer_layers.{l}.self_attn_layer_norm.bias")
+        scale, pd = ctx["emb"]
+        dh = K.scale_dropout_bwd(dx, scale, pd, ctx["drop_emb"])
+        self.subsample_bwd(ctx["sub"], dh)
+        self._ready(None)
+
+    def decoder_forward(self, batch, enc, enc_len32, Te):
+        cfg = self.cfg
+        d, V, pad = cfg["decoder_embed_dim"], cfg["vocab_size"], cfg["padding_idx"]
+        tok = batch.prev
+        B, Tt = tok.shape
+        ctx = {"B": B, "Tt": Tt}
+        pos = self._ensure_pos(Tt, "dec")
+        scale = 1.0 if cfg["no_scale_embedding"] else math.sqrt(d)
+        pd = self._p("dropout")
+        ctx["drop_emb"] = self._drop(pd, B * Tt * d)
+        ctx["tok"] = tok
+        x = K.token_embed(tok, self.P("decoder.embed_tokens.weight"), pos, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
+        ctx["emb"] = (scale, pd)
+        tgt_mask = batch.tgt_mask  # uint8 [B, round8(Tt)] or None (no target padding in the batch)
+        ctx["layers"] = []
+        for l in range(cfg["decoder_layers"]):
+            x, c = self.dec_layer_fwd(l, x, enc, B, Tt, Te, tgt_mask, enc_len32)
+            ctx["layers"].append(c)
+        xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("decoder.layer_norm.weight"), self.P("decoder.layer_norm.bias"))
+        ctx["lx"], ctx["xl"] = x, xl
+        Vp = round_up(V, 8)
+        logits = torch.empty(B * Tt, Vp, dtype=F16, device=x.device)
+        E = self.P("decoder.embed_tokens.weight")
+        K.gemm(xl, E, logits, B * Tt, V, d, lda=d, ldb=d, ldc=Vp)
+        ctx["Vp"] = Vp
+        return logits, ctx
+
+    def decoder_backward(self, ctx, dlogits, enc, denc):
+        cfg = self.cfg
+        d, V, pad = cfg["decoder_embed_dim"], cfg["vocab_size"], cfg["padding_idx"]
+        B, Tt = ctx["B"], ctx["Tt"]
+        E = self.P("decoder.embed_tokens.weight")
+        dE32 = torch.zeros(V, d, dtype=torch.float32, device=E.device)
+        # tied output projection: dE += dlogits^T xl ; dxl = dlogits E
+        K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32)
+        dxl = torch.empty(B * Tt, d, dtype=F16, device=E.device)
+        K.gemm(dlogits, E, dxl, B * Tt, d, V, a_kc=True, b_kc=False, lda=ctx["Vp"], ldb=d, ldc=d)
+        dx = K.layernorm_bwd(dxl, ctx["lx"], self.P("decoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
+                             self.params.span("decoder.layer_norm.weight", "decoder.layer_norm.bias", grad=True))
+        self._ready("decoder.layer_norm.bias")
+        for l in reversed(range(cfg["decoder_layers"])):
+            dx = self.dec_layer_bwd(l, ctx["layers"][l], dx, denc, enc)
+            ctx["layers"][l] = None
+            self._ready(f"decoder.layers.{l}.self_attn_layer_norm.bias")
+        scale, pd = ctx["emb"]
+        K.token_embed_bwd(ctx["tok"], dx, dE32, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
+        gE = self.G("decoder.embed_tokens.weight")
+        K.call("mms2ut_splitk_reduce", dE32.data_ptr(), 1, dE32.numel(), V, d, gE.data_ptr(), d, 1, 1.0,
+               K._s())
+        self._ready("decoder.embed_tokens.weight")

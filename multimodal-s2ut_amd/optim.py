@@ -1,0 +1,69 @@
+"""fairseq FP16Optimizer + Adam + inverse_sqrt, MI355X-native and device-resident.
+
+Flat fp32 master / exp_avg / exp_avg_sq mirror the flat fp16 parameter buffer.  Per step:
+grad_sqnorm -> grad_norm_finalize (multiply factor 1/(loss_scale*sample_size), overflow flag) ->
+optim_prepare (Adam step count + step size, clip coefficient, DynamicLossScaler) -> adam.  No host
+synchronisation: the loss scale the next backward uses is read from device memory.
+
+Reference semantics (fairseq, invoked by textless/1_train.sh:105-125):
+  --optimizer adam --adam-betas '(0.9,0.98)' --clip-norm 10.0 --lr-scheduler inverse_sqrt
+  --warmup-init-lr 1e-7 --warmup-updates 10000 --fp16 (init scale 128, scale window 2^14/world).
+"""
+import math
+
+import torch
+
+from . import kernels as K
+
+
+class FP16Adam:
+    def __init__(self, params, lr=5e-4, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.0, clip_norm=10.0,
+                 init_scale=128.0, scale_window=None, min_loss_scale=1e-4, world_size=1, update_freq=1,
+                 warmup_updates=10000, warmup_init_lr=1e-7):
+        self.params = params
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.clip = clip_norm
+        self.master = params.flat.float()
+        self.exp_avg = torch.zeros_like(self.master)
+        self.exp_avg_sq = torch.zeros_like(self.master)
+        self.scale_window = scale_window or max(1, int(2 ** 14 / world_size / update_freq))
+        self.min_loss_scale = min_loss_scale
+        self.warmup_updates, self.warmup_init_lr = warmup_updates, warmup_init_lr
+        self.num_updates = 0
+        ost = torch.zeros(K.OST_SIZE, dtype=torch.float32)
+        ost[K.OST_LOSS_SCALE] = init_scale
+        ost[K.OST_LAST_OVERFLOW] = -1.0
+        ost[K.OST_CLIP_COEF] = 1.0
+        self.ost = ost.to(params.flat.device)
+
+    def resync_master(self):
+        """After loading fp16 weights: master := fp32 copy of the fp16 params."""
+        self.master.copy_(self.params.flat)
+
+    def loss_scale(self):
+        """0-dim device tensor: the gradient fed to loss.backward()."""
+        return self.ost[K.OST_LOSS_SCALE]
+
+    def get_lr(self):
+        """fairseq inverse_sqrt schedule at the current update count."""
+        if self.warmup_updates > 0 and self.num_updates < self.warmup_updates:
+            step = (self.lr - self.warmup_init_lr) / self.warmup_updates
+            return self.warmup_init_lr + self.num_updates * step
+        wu = max(self.warmup_updates, 1)
+        return self.lr * math.sqrt(wu) * max(self.num_updates, 1) ** -0.5
+
+    def step(self, sample_size):
+        """sample_size: device fp32 tensor [1] (all-reduced ntokens)."""
+        lr = self.get_lr()
+        b1, b2 = self.betas
+        K.grad_norm(self.params.grad, self.ost, sample_size)
+        K.optim_prepare(self.ost, lr, b1, b2, self.clip, self.scale_window, self.min_loss_scale)
+        K.adam(self.params.flat, self.params.grad, self.master, self.exp_avg, self.exp_avg_sq, self.ost,
+               lr, b1, b2, self.eps, self.wd)
+        self.num_updates += 1
+
+    def stats(self):
+        o = self.ost.cpu()
+        return {"gnorm": float(o[K.OST_GNORM]), "overflow": bool(o[K.OST_OVERFLOW]),
+                "loss_scale": float(o[K.OST_LOSS_SCALE]), "step": int(o[K.OST_STEP]),
+                "fatal": bool(o[K.OST_FATAL])}

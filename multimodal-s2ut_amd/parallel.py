@@ -1,0 +1,74 @@
+"""Data parallelism over RCCL (torch.distributed backend "nccl" on ROCm = RCCL over xGMI).
+
+Replaces fairseq's DDP wrap (distributed_fairseq_model.py: torch DDP, bucket_cap_mb=25).  The
+parameter layout is in backward-completion order (model.param_specs), so the flat fp16 gradient
+buffer fills front-to-back during the hand-written backward; the model calls ``ready(offset)``
+after each layer and every bucket wholly below ``offset`` is all-reduced (SUM) at once,
+asynchronously on RCCL's stream, overlapping the rest of the backward.  Never-used parameters
+ live outside the flat buffer, so they are never communicated.  The fairseq per-step
+``all_gather_list`` of logging outputs becomes one summed all-reduce of fixed scalars.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend=None):
+    """One process per GPU, launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+        kw = {}
+        if backend == "nccl" and torch.cuda.is_available():
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    return rank, world, local
+
+
+class GradAllReducer:
+    """Bucketed, backward-overlapped SUM all-reduce of a flat gradient buffer."""
+
+    def __init__(self, grad_flat, bucket_mb=64.0, group=None):
+        self.grad = grad_flat
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        n = grad_flat.numel()
+        per = max(1, int(bucket_mb * 2 ** 20 // grad_flat.element_size()))
+        per = (per + 7) // 8 * 8
+        self.bounds = [(a, min(n, a + per)) for a in range(0, n, per)]
+        self.reset()
+
+    def reset(self):
+        self.next = 0
+        self.handles = []
+
+    def ready(self, upto):
+        if self.world == 1:
+            return
+        while self.next < len(self.bounds) and self.bounds[self.next][1] <= upto:
+            a, b = self.bounds[self.next]
+            self.handles.append(dist.all_reduce(self.grad[a:b], op=dist.ReduceOp.SUM, group=self.group,
+                                                async_op=True))
+            self.next += 1
+
+    def finish(self):
+        if self.world == 1:
+            return
+        self.ready(self.grad.numel())
+        for h in self.handles:
+            h.wait()
+        self.reset()
+
+
+def all_reduce_scalars(t, group=None):
+    """Summed all-reduce of a small fp32 vector (replaces fairseq all_gather_list logging)."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t

@@ -1,0 +1,139 @@
+"""Host runtime: batch preparation (sample dict -> device buffers), the autograd boundary of the
+model and of the label-smoothed CE criterion.
+
+The autograd graph has exactly two nodes per step — the whole model and the loss — because the
+model's backward is hand-written (model.py); PyTorch only carries the upstream loss-scale
+gradient between them.
+"""
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .kernels import F16, round_up
+
+
+@dataclass
+class DeviceBatch:
+    src: torch.Tensor                 # [B, Ts, C] fp16
+    src_lengths: torch.Tensor         # [B] int64 (host)
+    enc_len32: torch.Tensor           # [B] int32 (device) subsampled lengths
+    Te: int
+    prev: torch.Tensor                # [B, Tt] int64 (device)
+    tgt_mask: Optional[torch.Tensor]  # [B, round8(Tt)] uint8 or None
+    target: torch.Tensor              # [B, Tt] int64 (device)
+    imgs: Optional[torch.Tensor]      # [B, Ti, Di] fp16 or None
+    img_keymask: Optional[torch.Tensor]  # [B, round8(Ti+1)] uint8 or None
+    ntokens: int
+    nsentences: int
+    n_src_frames: int                 # sum of src lengths (the benchmark's unit of work)
+
+
+def subsampled_lengths(lengths, n_layers=2):
+    """fairseq Conv1dSubsampler.get_out_seq_lens_tensor: floor((L-1)/2)+1 per conv layer."""
+    out = np.asarray(lengths, dtype=np.int64).copy()
+    for _ in range(n_layers):
+        out = (out - 1) // 2 + 1
+    return out
+
+
+def prepare_batch(sample, cfg, device="cuda", src_override=None):
+    """fairseq Trainer._prepare_sample (move_to_cuda + apply_half) for the reference's sample
+    contract (speech_to_speech_dataset.py:446-468).  Masks/lengths are derived on the host."""
+    dev = torch.device(device)
+    ni = sample["net_input"]
+    lens = ni["src_lengths"].cpu().numpy()
+    nl = len(cfg["conv_kernel_sizes"])
+    if src_override is not None:
+        src = src_override
+    else:
+        src = ni["src_tokens"].to(dev, non_blocking=True).to(F16)
+    Ts = src.shape[1]
+    Te = int(subsampled_lengths([Ts], nl)[0])
+    enc_len = subsampled_lengths(lens, nl).astype(np.int32)
+    prev_cpu = ni["prev_output_tokens"].cpu()
+    B, Tt = prev_cpu.shape
+    pad = cfg["padding_idx"]
+    padm = prev_cpu.eq(pad)
+    tgt_mask = None
+    if bool(padm.any()):
+        tm = torch.zeros(B, round_up(Tt, 8), dtype=torch.uint8)
+        tm[:, :Tt] = padm.to(torch.uint8)
+        tgt_mask = tm.to(dev, non_blocking=True)
+    imgs = img_keymask = None
+    imgs_list = ni.get("imgs_list") or []
+    if cfg["fusion"] and len(imgs_list) > 0:
+        if len(imgs_list) > 1:
+            raise NotImplementedError("one image-feature type (SURVEY Q8)")
+        imgs = imgs_list[0].to(dev, non_blocking=True).to(F16)
+        masks = ni.get("img_masks_list") or []
+        if len(masks) > 0 and masks[0] is not None:
+            Ti = imgs.shape[1]
+            km = torch.zeros(B, round_up(Ti + 1, 8), dtype=torch.uint8)
+            km[:, :Ti] = masks[0].cpu().to(torch.uint8)
+            img_keymask = km.to(dev, non_blocking=True)
+    return DeviceBatch(
+        src=src.contiguous(), src_lengths=torch.as_tensor(lens), Te=Te,
+        enc_len32=torch.from_numpy(enc_len).to(dev, non_blocking=True),
+        prev=prev_cpu.to(dev, non_blocking=True).contiguous(), tgt_mask=tgt_mask,
+        target=sample["target"].to(dev, non_blocking=True).contiguous(), imgs=imgs,
+        img_keymask=img_keymask, ntokens=int(sample["ntokens"]),
+        nsentences=int(sample.get("nsentences", B)), n_src_frames=int(lens.sum()))
+
+
+class _ModelFn(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, anchor, model, batch):
+        enc, len32, Te, ectx = model.encoder_forward(batch)
+        logits, dctx = model.decoder_forward(batch, enc, len32, Te)
+        fctx.model = model
+        fctx.saved = (ectx, dctx, enc, batch)
+        return logits
+
+    @staticmethod
+    def backward(fctx, dlogits):
+        model = fctx.model
+        ectx, dctx, enc, batch = fctx.saved
+        fctx.saved = None
+        d = model.cfg["encoder_embed_dim"]
+        denc = torch.zeros(enc.shape[0], d, dtype=F16, device=enc.device)
+        model.decoder_backward(dctx, dlogits.contiguous(), enc, denc)
+        del dctx
+        model.encoder_backward(ectx, denc)
+        return None, None, None
+
+
+def model_logits(model, batch):
+    """Padded logits [B*Tt, round8(V)] fp16 (autograd-connected through the hand-written bwd)."""
+    return _ModelFn.apply(model.anchor, model, batch)
+
+
+class _LSXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, logits, target, V, eps, pad):
+        rows, ld = logits.shape
+        out = torch.zeros(2, dtype=torch.float32, device=logits.device)
+        lse = K.ls_xent_fwd(logits, ld, target, rows, V, eps, pad, out)
+        fctx.saved = (logits, target, lse, V, eps, pad)
+        fctx.mark_non_differentiable(out)
+        loss = out[0].clone()
+        nll = out[1].clone()
+        fctx.mark_non_differentiable(nll)
+        return loss, nll
+
+    @staticmethod
+    def backward(fctx, gloss, gnll):
+        logits, target, lse, V, eps, pad = fctx.saved
+        fctx.saved = None
+        rows, ld = logits.shape
+        g = gloss.reshape(1).to(torch.float32).contiguous()
+        # in place: the logits are dead after this point
+        K.ls_xent_bwd(logits, ld, target, rows, V, eps, pad, lse, g, logits)
+        return logits, None, None, None, None
+
+
+def label_smoothed_ce(logits, target, V, eps, pad):
+    """fairseq label_smoothed_nll_loss(lprobs=log_softmax(logits.float()), reduce=sum)."""
+    return _LSXentFn.apply(logits, target.reshape(-1), V, eps, pad)

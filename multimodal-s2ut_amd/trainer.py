@@ -1,0 +1,62 @@
+"""Trainer: one optimizer update per batch (update-freq 1), fairseq Trainer.train_step semantics.
+
+  zero grads -> fwd (model + LS-CE) -> loss.backward(loss_scale) [hand-written bwd, bucketed RCCL
+  all-reduce overlapped] -> sample_size all-reduce -> FP16Optimizer/Adam (device-side overflow skip
+  + loss-scale update) -> lr schedule.
+
+fairseq reference: Trainer.train_step (multiply_grads(world/sample_size) after DDP's averaging
+== SUM all-reduce then 1/sample_size), FP16Optimizer.clip_grad_norm(10), DynamicLossScaler.
+"""
+import torch
+
+from . import runtime
+from .optim import FP16Adam
+from .parallel import GradAllReducer, all_reduce_scalars
+
+
+class Trainer:
+    def __init__(self, model, lr=5e-4, betas=(0.9, 0.98), clip_norm=10.0, warmup_updates=10000,
+                 warmup_init_lr=1e-7, init_scale=128.0, bucket_mb=64.0, world_size=1):
+        self.model = model
+        self.cfg = model.cfg
+        self.opt = FP16Adam(model.params, lr=lr, betas=betas, clip_norm=clip_norm, init_scale=init_scale,
+                            world_size=world_size, warmup_updates=warmup_updates,
+                            warmup_init_lr=warmup_init_lr)
+        self.reducer = GradAllReducer(model.params.grad, bucket_mb) if world_size > 1 else None
+        self.world = world_size
+        self.log = torch.zeros(4, dtype=torch.float32, device=model.params.flat.device)
+
+    def train_step(self, batch):
+        cfg = self.cfg
+        m = self.model
+        m.train()
+        m.params.grad.zero_()
+        if self.reducer is not None:
+            self.reducer.reset()
+            m.grad_ready_hook = self.reducer.ready
+        logits = runtime.model_logits(m, batch)
+        loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
+                                              cfg["label_smoothing"], cfg["padding_idx"])
+        del logits
+        loss.backward(self.opt.loss_scale())
+        m.grad_ready_hook = None
+        if self.reducer is not None:
+            self.reducer.finish()
+        # logging / sample-size sync: [loss, nll, ntokens, nsentences] summed over ranks
+        self.log[0] = loss.detach()
+        self.log[1] = nll.detach()
+        self.log[2] = float(batch.ntokens)
+        self.log[3] = float(batch.nsentences)
+        all_reduce_scalars(self.log)
+        self.opt.step(self.log[2:3])
+        return self.log
+
+    def valid_step(self, batch):
+        m = self.model
+        m.eval()
+        with torch.no_grad():
+            logits = runtime.model_logits(m, batch)
+            loss, nll = runtime.label_smoothed_ce(logits, batch.target, self.cfg["vocab_size"],
+                                                  self.cfg["label_smoothing"], self.cfg["padding_idx"])
+        m.train()
+        return loss, nll

@@ -1,0 +1,172 @@
+"""CPU: C-ABI library loads and exports every declared symbol; host-side logic (collater, batching,
+parameter layout/state-dict names, fbank oracle cross-check, optimizer restatement)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, pkg
+from oracle import ref_fbank as RF
+from oracle import ref_model as R
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "mms2ut.h")).read()
+    return sorted(set(re.findall(r"\b(mms2ut_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    mm = pkg()
+    lib = mm._lib.load()
+    syms = header_symbols()
+    assert len(syms) > 30
+    for s in syms:
+        assert s in mm._lib.SIGNATURES, f"{s} declared in include/mms2ut.h but not bound in _lib.py"
+        assert getattr(lib, s) is not None
+    raw = ctypes.CDLL(mm._lib.LIB_PATH)
+    for s in syms:
+        getattr(raw, s)
+    assert lib.mms2ut_version() == 1
+    assert set(mm._lib.SIGNATURES) == set(syms)
+
+
+def test_library_error_path_without_gpu():
+    """A bad call fails loudly with a message (validation happens before any device work)."""
+    mm = pkg()
+    a = mm._lib.GemmArgs()
+    a.M, a.N, a.K, a.batch, a.lda, a.ldb = 4, 4, 4, 1, 3, 8
+    with pytest.raises(mm._lib.HipError, match="multiples of 8"):
+        mm._lib.call("mms2ut_gemm_f16", a, None)
+
+
+def test_param_layout_matches_reference_state_dict():
+    mm = pkg()
+    for cfg_o in (R.base_config(), R.tiny_config(image_feat_dim=768),
+                  R.base_config(multimodal_attention_type="selective_attention")):
+        specs, unused = mm.param_specs(mm.default_cfg(**cfg_o))
+        names = {n for n, _ in specs} | {n for n, _ in unused}
+        ref = R.init_params(cfg_o, include_unused=True)
+        assert names == set(ref), set(ref) ^ names
+        shapes = dict(specs + unused)
+        for k, v in ref.items():
+            assert tuple(v.shape) == tuple(shapes[k]), k
+    specs, unused = mm.param_specs(mm.default_cfg())
+    n_used = sum(int(np.prod(s)) for _, s in specs)
+    n_unused = sum(int(np.prod(s)) for _, s in unused)
+    assert 149e6 < n_used < 152e6 and 13e6 < n_unused < 14e6   # ~164M total
+
+
+def test_flat_layout_spans_contiguous():
+    mm = pkg()
+    ps = mm.model.ParamStore(mm.param_specs(mm.default_cfg())[0], "cpu")
+    p = "encoder.transformer_layers.3.self_attn"
+    qkv = ps.span(p + ".q_proj.weight", p + ".v_proj.weight")
+    assert qkv.numel() == 3 * 768 * 768
+    assert ps.span(p + ".q_proj.bias", p + ".v_proj.bias").numel() == 3 * 768
+    for name, (off, shape, n) in ps.offsets.items():
+        assert off % 8 == 0
+
+
+def test_collater_contract():
+    mm = pkg()
+    s = mm.data.make_sample([30, 50, 40], [5, 9, 7], img_tokens=4, img_dim=8, img_mask=True)
+    ni = s["net_input"]
+    assert ni["src_lengths"].tolist() == [50, 40, 30]
+    assert ni["src_tokens"].shape == (3, 50, 80)
+    assert torch.all(ni["src_tokens"][2, 30:] == 0)
+    assert s["target"][0, -1] == 2 and s["target"][2, 5:].eq(1).all()
+    assert ni["prev_output_tokens"][0, 0] == 2
+    assert torch.equal(ni["prev_output_tokens"][0, 1:], s["target"][0, :-1])
+    assert s["ntokens"] == 21
+    assert ni["imgs_list"][0].shape == (3, 4, 8) and ni["img_masks_list"][0].dtype == torch.bool
+    assert s["id"].tolist() == [1, 2, 0]
+
+
+def test_batch_by_size_max_tokens():
+    mm = pkg()
+    rng = np.random.default_rng(0)
+    lens = mm.data.synth_lengths(5000, rng)
+    assert lens.min() >= 150 and lens.max() <= 1000
+    batches = mm.data.batch_by_size(lens, 40000)
+    assert sorted(i for b in batches for i in b) == list(range(5000))
+    for b in batches:
+        assert len(b) * max(lens[b]) <= 40000
+
+
+def test_prepare_batch_host_masks():
+    mm = pkg()
+    cfg = mm.default_cfg()
+    s = mm.data.make_sample([93, 80, 61], [30, 25, 19], img_tokens=5, img_dim=768, img_mask=True)
+    b = mm.runtime.prepare_batch(s, cfg, device="cpu")
+    assert b.Te == 24 and b.enc_len32.tolist() == [24, 20, 16]
+    assert b.tgt_mask.shape == (3, 32) and b.tgt_mask[2, 19:30].all() and not b.tgt_mask[0, :30].any()
+    assert b.img_keymask.shape == (3, 8) and b.img_keymask[:, 5:].eq(0).all()
+    assert b.n_src_frames == 234 and b.ntokens == 74
+
+
+def test_fbank_oracle_vs_transformers_kaldi():
+    """ref_fbank (restating torchaudio.compliance.kaldi.fbank) vs transformers.audio_utils'
+    independent Kaldi-compatible implementation."""
+    au = pytest.importorskip("transformers.audio_utils")
+    rng = np.random.default_rng(0)
+    for T in (1, 7, 150):
+        w = RF.synth_wave(T, rng)
+        a = RF.fbank(w)
+        mf = au.mel_filter_bank(num_frequency_bins=257, num_mel_filters=80, min_frequency=20,
+                                max_frequency=8000, sampling_rate=16000, norm=None, mel_scale="kaldi",
+                                triangularize_in_mel_space=True)
+        win = au.window_function(400, "povey", periodic=False)
+        b = au.spectrogram(w, win, frame_length=400, hop_length=160, fft_length=512, power=2.0,
+                           center=False, preemphasis=0.97, mel_filters=mf, log_mel="log",
+                           mel_floor=1.192092955078125e-07, remove_dc_offset=True).T
+        assert a.shape == b.shape == (T, 80)
+        np.testing.assert_allclose(a, b, atol=2e-4, rtol=1e-5)
+
+
+def test_fbank_known_answers():
+    rng = np.random.default_rng(1)
+    assert RF.num_frames(399) == 0 and RF.num_frames(400) == 1 and RF.num_frames(560) == 2
+    # a pure tone puts its energy in the mel bin whose centre is nearest the tone
+    n = 16000
+    t = np.arange(n) / 16000.0
+    w = (0.5 * np.sin(2 * np.pi * 1000.0 * t) * 2 ** 15).astype(np.float32)
+    f = RF.fbank(w)
+    banks = RF.mel_banks()
+    centre = banks.argmax(1) * 16000 / 512
+    assert abs(centre[f.mean(0).argmax()] - 1000.0) < 80.0
+    c = RF.utterance_cmvn(f + rng.standard_normal(f.shape).astype(np.float32))
+    np.testing.assert_allclose(c.mean(0), 0, atol=1e-4)
+    np.testing.assert_allclose(c.std(0), 1, atol=1e-3)
+
+
+def test_product_mel_banks_match_oracle():
+    mm = pkg()
+    np.testing.assert_array_equal(mm.frontend.mel_banks()[:, :256], RF.mel_banks())
+
+
+def test_optimizer_restatement_adam_known_answer():
+    p = torch.tensor([1.0, -2.0])
+    g = torch.tensor([0.5, 0.25])
+    m, v = torch.zeros(2), torch.zeros(2)
+    R.adam_step(p, g, m, v, 1, lr=0.1)
+    # first Adam step moves each coordinate by ~lr*sign(g)
+    torch.testing.assert_close(p, torch.tensor([0.9, -2.1]), atol=1e-6, rtol=0)
+
+
+def test_lr_schedule_inverse_sqrt():
+    mm = pkg()
+
+    class FakeParams:
+        flat = torch.zeros(8, dtype=torch.float16)
+        grad = torch.zeros(8, dtype=torch.float16)
+
+    opt = mm.optim.FP16Adam(FakeParams(), lr=5e-4, warmup_updates=10000, warmup_init_lr=1e-7)
+    assert abs(opt.get_lr() - 1e-7) < 1e-12
+    opt.num_updates = 5000
+    assert abs(opt.get_lr() - (1e-7 + 5000 * (5e-4 - 1e-7) / 10000)) < 1e-12
+    opt.num_updates = 40000
+    assert abs(opt.get_lr() - 5e-4 * (10000 / 40000) ** 0.5) < 1e-12
+    assert opt.scale_window == 16384

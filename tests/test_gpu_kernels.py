@@ -1,0 +1,234 @@
+"""GPU: HIP kernels vs plain PyTorch fp32 references (floating-point kernels), via the C-ABI."""
+import math
+
+import pytest
+import torch
+
+from conftest import pkg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return pkg().kernels
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _mat(rows, cols, ld=None, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    ld = ld or cols
+    buf = torch.randn(rows, ld, generator=g, device="cuda").half()
+    return buf[:, :cols]
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K_", [(130, 200, 100), (257, 96, 768), (64, 1004, 72), (1, 8, 8)])
+def test_gemm_layouts(K, a_kc, b_kc, M, N, K_):
+    A = _mat(M, K_, seed=1) if a_kc else _mat(K_, M, seed=1)
+    B = _mat(N, K_, seed=2) if b_kc else _mat(K_, N, seed=2)
+    Af = A.float() if a_kc else A.float().t()
+    Bf = B.float() if b_kc else B.float().t()
+    ref = Af @ Bf.t()
+    ldc = (N + 7) // 8 * 8
+    C = torch.zeros(M, ldc, dtype=torch.float16, device="cuda")
+    K.gemm(A.contiguous(), B.contiguous(), C, M, N, K_, a_kc=a_kc, b_kc=b_kc,
+           lda=A.contiguous().stride(0), ldb=B.contiguous().stride(0), ldc=ldc)
+    torch.cuda.synchronize()
+    assert rel(C[:, :N], ref) < 2e-3
+
+
+def test_gemm_identity_asymmetric(K):
+    # A = I with asymmetric B catches a transposed C-write (guide §3)
+    n = 128
+    A = torch.eye(n, device="cuda").half()
+    B = (torch.arange(n * n, device="cuda").view(n, n) % 97).half()
+    C = torch.empty(n, n, dtype=torch.float16, device="cuda")
+    K.gemm(A, B, C, n, n, n, lda=n, ldb=n, ldc=n)
+    torch.cuda.synchronize()
+    assert torch.equal(C, B)
+
+
+def test_gemm_batched_strided_alpha(K):
+    Bt, H, T, hd = 3, 4, 37, 64
+    d = H * hd
+    qkv = torch.randn(Bt * T, 3 * d, device="cuda").half()
+    ldS = 40
+    S = torch.zeros(Bt * H * T * ldS, dtype=torch.float16, device="cuda")
+    K.gemm(qkv, qkv[:, d:], S, T, T, hd, lda=3 * d, ldb=3 * d, ldc=ldS, batch=Bt * H, bdiv=H,
+           sA=(T * 3 * d, hd), sB=(T * 3 * d, hd), sC=(H * T * ldS, T * ldS), alpha=0.125)
+    torch.cuda.synchronize()
+    q = qkv[:, :d].float().view(Bt, T, H, hd).permute(0, 2, 1, 3)
+    k = qkv[:, d:2 * d].float().view(Bt, T, H, hd).permute(0, 2, 1, 3)
+    ref = 0.125 * q @ k.transpose(-1, -2)
+    got = S.view(Bt, H, T, ldS)[..., :T]
+    assert rel(got, ref) < 2e-3
+
+
+def test_gemm_epilogues(K):
+    M, N, K_ = 300, 256, 192
+    x = torch.randn(M, K_, device="cuda").half()
+    W = (0.05 * torch.randn(N, K_, device="cuda")).half()
+    b = torch.randn(N, device="cuda").half()
+    res = torch.randn(M, N, device="cuda").half()
+    pre = x.float() @ W.float().t() + b.float()
+    y = K.linear(x, W, b, epi=K.EPI_RELU_DROP)
+    assert rel(y, pre.relu()) < 2e-3
+    y = K.linear(x, W, b, epi=K.EPI_DROP_RESID, aux=res)
+    assert rel(y, pre + res.float()) < 2e-3
+    # dropout: replay the mask through the C-ABI
+    seed, off = 1234, 4096
+    y = K.linear(x, W, b, epi=K.EPI_RELU_DROP, p=0.25, drop=(seed, off))
+    m = K.dropout_mask(M * N, 0.25, seed, off, "cuda").view(M, N).float()
+    assert rel(y, pre.relu() * m / 0.75) < 2e-3
+    assert 0.70 < m.mean().item() < 0.80
+    # gate
+    merge = torch.randn(M, 2 * N, device="cuda").half()
+    Wg = (0.05 * torch.randn(N, 2 * N, device="cuda")).half()
+    g = torch.empty(M, N, dtype=torch.float16, device="cuda")
+    out = K.linear(merge, Wg, b, epi=K.EPI_GATE, aux=merge, out2=g)
+    gr = torch.sigmoid(merge.float() @ Wg.float().t() + b.float())
+    o, t = merge[:, :N].float(), merge[:, N:].float()
+    torch.cuda.synchronize()
+    assert rel(g, gr) < 2e-3
+    assert rel(out, (1 - gr) * t + gr * o) < 2e-3
+
+
+def test_wgrad_splitk(K):
+    M, N, K_ = 5000, 96, 200
+    dy = torch.randn(M, N, device="cuda").half()
+    x = torch.randn(M, K_, device="cuda").half()
+    dW = torch.empty(N, K_, dtype=torch.float16, device="cuda")
+    K.linear_wgrad(dy, x, dW)
+    torch.cuda.synchronize()
+    assert rel(dW, dy.float().t() @ x.float()) < 2e-3
+
+
+def test_layernorm_fwd_bwd(K):
+    for R, D in ((1000, 768), (37, 256), (5, 96)):
+        x = (3 * torch.randn(R, D, device="cuda") + 1).half()
+        g = (1 + 0.1 * torch.randn(D, device="cuda")).half()
+        b = (0.1 * torch.randn(D, device="cuda")).half()
+        y, mean, rstd = K.layernorm(x, g, b)
+        xf = x.float().requires_grad_(True)
+        gf, bf = g.float().requires_grad_(True), b.float().requires_grad_(True)
+        yr = torch.nn.functional.layer_norm(xf, (D,), gf, bf, 1e-5)
+        assert rel(y, yr) < 2e-3
+        dy = torch.randn(R, D, device="cuda").half()
+        dres = torch.randn(R, D, device="cuda").half()
+        dgb = torch.empty(2 * D, dtype=torch.float16, device="cuda")
+        dx = K.layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=dres)
+        yr.backward(dy.float())
+        torch.cuda.synchronize()
+        assert rel(dx, xf.grad + dres.float()) < 3e-3
+        assert rel(dgb[:D], gf.grad) < 3e-3
+        assert rel(dgb[D:], bf.grad) < 3e-3
+
+
+@pytest.mark.parametrize("causal,extra", [(False, False), (True, False), (False, True)])
+def test_attn_softmax(K, causal, extra):
+    Bt, H, Tq, Tk = 3, 2, 19, 23 if not causal else 19
+    if extra:
+        Tk += 1
+    ldS = (Tk + 7) // 8 * 8
+    S = torch.randn(Bt * H * Tq * ldS, device="cuda").half()
+    lens = torch.tensor([Tk - (1 if extra else 0), 11, 5], dtype=torch.int32, device="cuda")
+    P, Pd = K.attn_softmax(S, Bt * H, H, Tq, Tk, ldS, key_len=lens, causal=causal, extra_key=extra)
+    s = S.view(Bt, H, Tq, ldS)[..., :Tk].float()
+    j = torch.arange(Tk, device="cuda")
+    mask = j[None, None, None, :] >= lens.long()[:, None, None, None]
+    if extra:
+        mask = mask & (j != Tk - 1)
+    if causal:
+        mask = mask | (j[None, None, None, :] > torch.arange(Tq, device="cuda")[None, None, :, None])
+    sf = s.masked_fill(mask, float("-inf")).requires_grad_(True)
+    pr = torch.softmax(sf, -1)
+    assert rel(P.view(Bt, H, Tq, ldS)[..., :Tk], pr) < 2e-3
+    dP = torch.randn(Bt * H * Tq * ldS, device="cuda").half()
+    pr.backward(dP.view(Bt, H, Tq, ldS)[..., :Tk].float())
+    dS = K.attn_softmax_bwd(P, dP.clone(), Bt * H, H, Tq, Tk, ldS)
+    torch.cuda.synchronize()
+    assert rel(dS.view(Bt, H, Tq, ldS)[..., :Tk], sf.grad.nan_to_num(0.0)) < 3e-3
+
+
+def test_attn_softmax_dropout_replay(K):
+    Z, Tq, Tk = 4, 16, 30
+    ldS = 32
+    S = torch.randn(Z * Tq * ldS, device="cuda").half()
+    P, Pd = K.attn_softmax(S, Z, 1, Tq, Tk, ldS, p=0.2, drop=(7, 0))
+    m = K.dropout_mask(Z * Tq * Tk, 0.2, 7, 0, "cuda").view(Z, Tq, Tk).float()
+    pv = P.view(Z, Tq, ldS)[..., :Tk].float()
+    torch.cuda.synchronize()
+    assert rel(Pd.view(Z, Tq, ldS)[..., :Tk], pv * m / 0.8) < 2e-3
+    # backward with the same mask
+    pf = torch.softmax(S.view(Z, Tq, ldS)[..., :Tk].float(), -1).requires_grad_(True)
+    out = pf * m / 0.8
+    g = torch.randn(Z * Tq * ldS, device="cuda").half()
+    out.backward(g.view(Z, Tq, ldS)[..., :Tk].float())
+    # d(softmax) from d(pf)
+    pr = torch.softmax(S.view(Z, Tq, ldS)[..., :Tk].float(), -1)
+    dS_ref = pr * (pf.grad - (pf.grad * pr).sum(-1, keepdim=True))
+    dS = K.attn_softmax_bwd(P, g.clone(), Z, 1, Tq, Tk, ldS, p=0.2, drop=(7, 0))
+    torch.cuda.synchronize()
+    assert rel(dS.view(Z, Tq, ldS)[..., :Tk], dS_ref) < 3e-3
+
+
+def test_ls_xent(K):
+    rows, V, eps, pad = 333, 1004, 0.2, 1
+    Vp = 1008
+    logits = torch.randn(rows, Vp, device="cuda").half()
+    target = torch.randint(0, V, (rows,), device="cuda")
+    target[::7] = pad
+    out = torch.zeros(2, device="cuda")
+    lse = K.ls_xent_fwd(logits, Vp, target, rows, V, eps, pad, out)
+    z = logits[:, :V].float().requires_grad_(True)
+    lp = torch.log_softmax(z, -1)
+    keep = target != pad
+    nll = -lp[keep, target[keep]].sum()
+    smooth = -lp[keep].sum()
+    ei = eps / (V - 1)
+    loss = (1 - eps - ei) * nll + ei * smooth
+    torch.cuda.synchronize()
+    assert abs(out[0].item() - loss.item()) / loss.item() < 1e-4
+    assert abs(out[1].item() - nll.item()) / nll.item() < 1e-4
+    loss.backward()
+    g = torch.tensor([3.0], device="cuda")
+    dz = torch.empty_like(logits)
+    K.ls_xent_bwd(logits, Vp, target, rows, V, eps, pad, lse, g, dz)
+    torch.cuda.synchronize()
+    assert rel(dz[:, :V], 3 * z.grad) < 2e-3
+
+
+def test_glu_im2col_col2im(K):
+    B, Tin, C, k = 2, 23, 16, 5
+    Tout = (Tin - 1) // 2 + 1
+    x = torch.randn(B * Tin, C, device="cuda").half()
+    col = K.im2col(x, B, Tin, Tout, C, k)
+    W = torch.randn(8, C, k, device="cuda")
+    ref = torch.nn.functional.conv1d(x.float().view(B, Tin, C).transpose(1, 2), W, stride=2, padding=2)
+    got = (col.float() @ W.view(8, -1).t()).view(B, Tout, 8).transpose(1, 2)
+    assert rel(got, ref) < 2e-3
+    dcol = torch.randn_like(col)
+    dx = K.col2im(dcol, B, Tin, Tout, C, k)
+    xf = x.float().requires_grad_(True)
+    col_ref = torch.nn.functional.unfold(xf.view(B, Tin, C).transpose(1, 2).unsqueeze(-1), (k, 1),
+                                         padding=(2, 0), stride=(2, 1))  # [B, C*k, Tout]
+    col_ref.backward(dcol.float().view(B, Tout, C * k).transpose(1, 2))
+    torch.cuda.synchronize()
+    assert rel(dx, xf.grad) < 2e-3
+    h = torch.randn(50, 64, device="cuda").half()
+    y = K.glu(h, 32)
+    hf = h.float().requires_grad_(True)
+    yr = torch.nn.functional.glu(hf, -1)
+    assert rel(y, yr) < 2e-3
+    dy = torch.randn(50, 32, device="cuda").half()
+    dh = K.glu_bwd(h, dy, 32)
+    yr.backward(dy.float())
+    torch.cuda.synchronize()
+    assert rel(dh, hf.grad) < 3e-3

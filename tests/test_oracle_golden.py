@@ -1,0 +1,44 @@
+"""CPU: pin the oracle's fusion restatement to golden vectors produced by the REFERENCE's own
+fusion code (oracle/gen_golden.py, shimmed import of mm_s2ut/models/{fuse,mm_s2s_transformer}.py)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files
+from oracle import ref_model as R
+
+
+def load_case(path):
+    z = np.load(path)
+    P = {k[len("param."):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param.")}
+    P = {"encoder." + k: v for k, v in P.items()}
+    d = int(z["d"])
+    cfg = R.base_config(
+        encoder_embed_dim=d, image_feat_dim=int(z["Di"]),
+        multimodal_attention_type=str(z["att"]), use_selective_gate=bool(z["gate"]),
+        SA_image_dropout=float(z["p_img"]), SA_text_dropout=float(z["p_txt"]),
+        SA_attention_dropout=float(z["p_attn"]))
+    masks = {"fusion.img": torch.from_numpy(z["img_keep"]),
+             "fusion.txt": torch.from_numpy(z["txt_keep"]),
+             "fusion.attn": torch.from_numpy(z["attn_keep"])}
+    img_mask = torch.from_numpy(z["img_mask"]) if z["img_mask"].size else None
+    return z, P, cfg, masks, img_mask
+
+
+@pytest.mark.parametrize("path", golden_files("fusion_"), ids=lambda p: p.split("/")[-1])
+def test_fusion_oracle_matches_reference(path):
+    z, P, cfg, masks, img_mask = load_case(path)
+    P = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    text = torch.from_numpy(z["text"]).clone().requires_grad_(True)
+    img = torch.from_numpy(z["img"])
+    text_mask = torch.from_numpy(z["text_mask"])
+    res = R.fuse_img_feat(P, text, img, img_mask, text_mask, cfg, masks, dtype=torch.float64)
+    np.testing.assert_allclose(res.detach().numpy(), z["res"], rtol=1e-10, atol=1e-10)
+    (res * torch.from_numpy(z["gout"])).sum().backward()
+    np.testing.assert_allclose(text.grad.numpy(), z["grad_text"], rtol=1e-9, atol=1e-10)
+    for k in z.files:
+        if k.startswith("grad.") and k != "grad_text":
+            name = "encoder." + k[len("grad."):]
+            g = P[name].grad
+            g = np.zeros_like(z[k]) if g is None else g.numpy()
+            np.testing.assert_allclose(g, z[k], rtol=1e-9, atol=1e-10, err_msg=name)
