@@ -467,7 +467,7 @@ class MMS2UTModel:
             imgn = K.dropout(imgn, pimg, c["drop_img"])
         if extra:
             imgd = torch.zeros(B, Tk, Di, dtype=F16, device=img.device)
-            K.copy2d(imgn, imgd.view(B, Tk * Di), B, Ti * Di)
+            K.copy2d(imgn.view(B, Ti * Di), imgd.view(B, Tk * Di), B, Ti * Di)
             imgd = imgd.view(B * Tk, Di)
         else:
             imgd = imgn

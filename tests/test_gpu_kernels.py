@@ -29,7 +29,7 @@ def _mat(rows, cols, ld=None, seed=0):
 
 
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K_", [(130, 200, 100), (257, 96, 768), (64, 1004, 72), (1, 8, 8)])
+@pytest.mark.parametrize("M,N,K_", [(130, 200, 104), (257, 96, 768), (64, 1004, 72), (1, 8, 8), (136, 24, 17)])
 def test_gemm_layouts(K, a_kc, b_kc, M, N, K_):
     A = _mat(M, K_, seed=1) if a_kc else _mat(K_, M, seed=1)
     B = _mat(N, K_, seed=2) if b_kc else _mat(K_, N, seed=2)
