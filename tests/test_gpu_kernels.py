@@ -31,15 +31,15 @@ def _mat(rows, cols, ld=None, seed=0):
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K_", [(130, 200, 104), (257, 96, 768), (64, 1004, 72), (1, 8, 8), (136, 24, 17)])
 def test_gemm_layouts(K, a_kc, b_kc, M, N, K_):
-    A = _mat(M, K_, seed=1) if a_kc else _mat(K_, M, seed=1)
-    B = _mat(N, K_, seed=2) if b_kc else _mat(K_, N, seed=2)
+    r8 = lambda x: (x + 7) // 8 * 8
+    A = _mat(M, K_, ld=r8(K_), seed=1) if a_kc else _mat(K_, M, ld=r8(M), seed=1)
+    B = _mat(N, K_, ld=r8(K_), seed=2) if b_kc else _mat(K_, N, ld=r8(N), seed=2)
     Af = A.float() if a_kc else A.float().t()
     Bf = B.float() if b_kc else B.float().t()
     ref = Af @ Bf.t()
-    ldc = (N + 7) // 8 * 8
+    ldc = r8(N)
     C = torch.zeros(M, ldc, dtype=torch.float16, device="cuda")
-    K.gemm(A.contiguous(), B.contiguous(), C, M, N, K_, a_kc=a_kc, b_kc=b_kc,
-           lda=A.contiguous().stride(0), ldb=B.contiguous().stride(0), ldc=ldc)
+    K.gemm(A, B, C, M, N, K_, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=ldc)
     torch.cuda.synchronize()
     assert rel(C[:, :N], ref) < 2e-3
 

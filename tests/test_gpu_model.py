@@ -70,6 +70,12 @@ def _check(model, lg, lgo, loss, lo, nll, nllo, Pg, sample, grad_tol=5e-2):
         if v.grad is None or v.grad.norm() == 0:
             assert g.norm() == 0, k
             continue
+        if k.endswith("k_proj.bias"):
+            # mathematically zero (softmax is shift-invariant along keys): fp rounding noise only;
+            # bound it by the matching value-bias gradient instead of a relative error
+            vb = Pg[k.replace("k_proj", "v_proj")].grad
+            assert g.norm() <= 1e-2 * vb.norm() + 1e-3, (k, g.norm(), vb.norm())
+            continue
         e = rel(g, v.grad)
         if e > grad_tol:
             bad.append((k, e))
