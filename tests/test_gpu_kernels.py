@@ -50,7 +50,10 @@ def test_gemm_identity_asymmetric(K):
     A = torch.eye(n, device="cuda").half()
     B = (torch.arange(n * n, device="cuda").view(n, n) % 97).half()
     C = torch.empty(n, n, dtype=torch.float16, device="cuda")
-    K.gemm(A, B, C, n, n, n, lda=n, ldb=n, ldc=n)
+    K.gemm(A, B, C, n, n, n, lda=n, ldb=n, ldc=n)   # C = A B^T (B is [N, K])
+    torch.cuda.synchronize()
+    assert torch.equal(C, B.t().contiguous())
+    K.gemm(A, B, C, n, n, n, b_kc=False, lda=n, ldb=n, ldc=n)  # B as [K, N] -> C = A B
     torch.cuda.synchronize()
     assert torch.equal(C, B)
 

@@ -162,6 +162,9 @@ def test_fusion_matches_reference_golden(mm, path):
     for k in z.files:
         if k.startswith("grad.") and k != "grad_text":
             name = "encoder." + k[len("grad."):]
+            if name.endswith("selective_attns.0.k_proj.bias"):   # mathematically zero (shift-invariant softmax)
+                assert model.params.g[name].float().norm() < 1e-2 * np.linalg.norm(z["grad.selective_attns.0.v_proj.bias"]) + 1e-3
+                continue
             assert rel(model.params.g[name], torch.from_numpy(z[k])) < 2e-2, name
 
 
