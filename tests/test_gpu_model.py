@@ -201,4 +201,7 @@ def test_fusion_dropout_replay_vs_oracle(mm):
     torch.cuda.synchronize()
     assert rel(dtext, t_o.grad.transpose(0, 1).reshape(B * Te, d)) < 1e-2
     for k, v in Pg.items():
+        if k.endswith("k_proj.bias"):  # mathematically zero (shift-invariant softmax)
+            assert model.params.g[k].float().norm().item() < 1e-2 * Pg[k.replace("k_proj", "v_proj")].grad.norm().item() + 1e-3
+            continue
         assert rel(model.params.g[k], v.grad) < 2e-2, k
