@@ -14,6 +14,8 @@
 //     gfx950 transpose read ds_read_b64_tr_b16 (two per fragment), conflict-free per half-wave.
 // The MFMA is issued with (B,A) swapped so each lane owns 4 consecutive output columns -> 8-B
 // vector stores and 4-wide epilogue math.
+#include <stdlib.h>
+
 #include "common.h"
 #include "../../include/mms2ut.h"
 
@@ -270,6 +272,144 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int t
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS-DMA pipelined variant: operands go global -> LDS with buffer_load ... lds (16 B / lane,
+// 1 KiB per wave-instruction, no VGPR staging), STAGES-deep ring, counted vmcnt + raw s_barrier
+// so the next tiles' DMA stays in flight across the barrier.  The XOR swizzle moves to the
+// per-lane SOURCE address (the DMA writes lane-linear LDS), the fragment reads are unchanged.
+// Out-of-range rows/k-rows read as zero through the buffer descriptor's range check, so tails
+// need no predication; a K-contiguous operand needs K % 64 == 0 (host routing).
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <bool KC>
+MMS_DEV void dma_tile(__amdgpu_buffer_rsrc_t rs, char* lds, long ld, int row0, int k0rel, int wid, int lane) {
+  // 16 wave-instructions per 16 KiB tile: wave `wid` issues 4 of them
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ins = wid * 4 + i;
+    int voff;
+    if (KC) {
+      const int row = ins * 8 + (lane >> 3), slot = lane & 7;
+      const int c = slot ^ (row & 7);
+      voff = (int)(((long)(row0 + row) * ld + k0rel + c * 8) * 2);
+    } else {
+      const int kr = ins * 4 + (lane >> 4), slot = lane & 15;
+      const int c = slot ^ swz_mn(kr);
+      voff = (int)(((long)(k0rel + kr) * ld + row0 + c * 8) * 2);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+template <int N>
+MMS_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool A_KC, bool B_KC, int EPI, int STAGES>
+__global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
+  const int ntiles = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int z = blockIdx.y;
+  const int zb = z / P.splitk, zs = z % P.splitk;
+  const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
+  const int kbeg = zs * P.kchunk;
+  const int kend = min(P.K, kbeg + P.kchunk);
+  const int bm = tm * BM, bn = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  // buffer descriptors (block-uniform): K-contig base = operand, MN-contig base = row kbeg
+  const h16* Ab = P.A + z1 * P.sA1 + z2 * P.sA2 + (A_KC ? 0 : (long)kbeg * P.lda);
+  const h16* Bb = P.B + z1 * P.sB1 + z2 * P.sB2 + (B_KC ? 0 : (long)kbeg * P.ldb);
+  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2 : ((long)(kend - kbeg - 1) * P.lda + P.M) * 2;
+  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2 : ((long)(kend - kbeg - 1) * P.ldb + P.N) * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)a_ext, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)b_ext, 0x00020000);
+#define SA(s) (smem + (2 * (s)) * TILE_BYTES)
+#define SB(s) (smem + (2 * (s) + 1) * TILE_BYTES)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  // k offset of stage t relative to the descriptor base
+  auto k_rel = [&](int t, bool kc) { return kc ? kbeg + t * BK : t * BK; };
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (s < nk) {
+      dma_tile<A_KC>(ra, SA(s), P.lda, bm, k_rel(s, A_KC), wid, lane);
+      dma_tile<B_KC>(rb, SB(s), P.ldb, bn, k_rel(s, B_KC), wid, lane);
+    }
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt must have landed; leave the younger stages (issued earlier) in flight
+    const int younger = min(STAGES - 2, nk - 1 - kt);
+    if (STAGES >= 3 && younger >= 1) wait_vm<8>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    const int nxt = kt + STAGES - 1;
+    if (nxt < nk) {
+      const int sb = nxt % STAGES;
+      dma_tile<A_KC>(ra, SA(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
+      dma_tile<B_KC>(rb, SB(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
+    }
+    const int cur = kt % STAGES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      h16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef SA
+#undef SB
+  char* Cz;
+  if (EPI == MMS_EPI_F32)
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
+  else
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
+  const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = bm + wm * 64 + i * 16 + (lane & 15);
+      const int n = bn + wn * 64 + j * 16 + 4 * (lane >> 4);
+      epilogue_store<EPI>(P, Cz, auxz, m, n, acc[i][j]);
+    }
+}
+
+constexpr int DMA_STAGES = 3;
+
+template <bool A_KC, bool B_KC>
+int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
+  dim3 grid(tm * tn, nz), block(NT);
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, DMA_STAGES>), grid, block, 0, s, P, tm, tn); break;
+    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+#undef CASE
+    default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
+  }
+  return mms::check_launch("gemm_dma");
+}
+
 template <bool A_KC, bool B_KC>
 int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   dim3 grid(tm * tn, nz), block(NT);
@@ -319,6 +459,19 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   const int nz = a->batch * splitk;
   MMS_REQUIRE(nz <= 65535, "gemm: batch*splitk too large (%d)", nz);
   hipStream_t s = stream;
+  // LDS-DMA pipeline when every K-contiguous operand has whole 64-wide k-tiles and the operand
+  // extents fit a buffer descriptor; otherwise the register-staged kernel (predicated tails)
+  const char* path_env = getenv("MMS2UT_GEMM_PATH");  // "reg" forces the register-staged kernel (A/B)
+  const bool force_reg = path_env && path_env[0] == 'r';
+  const bool k_ok = (!a_kc || a->K % BK == 0) && (!b_kc || a->K % BK == 0);
+  const long a_ext = a_kc ? (long)a->M * a->lda : (long)a->K * a->lda;
+  const long b_ext = b_kc ? (long)a->N * a->ldb : (long)a->K * a->ldb;
+  if (!force_reg && k_ok && a_ext * 2 < (1L << 31) && b_ext * 2 < (1L << 31)) {
+    if (a_kc && b_kc) return launch_dma<true, true>(a->epi, P, tm, tn, nz, s);
+    if (a_kc && !b_kc) return launch_dma<true, false>(a->epi, P, tm, tn, nz, s);
+    if (!a_kc && b_kc) return launch_dma<false, true>(a->epi, P, tm, tn, nz, s);
+    return launch_dma<false, false>(a->epi, P, tm, tn, nz, s);
+  }
   if (a_kc && b_kc) return launch_epi<true, true>(a->epi, P, tm, tn, nz, s);
   if (a_kc && !b_kc) return launch_epi<true, false>(a->epi, P, tm, tn, nz, s);
   if (!a_kc && b_kc) return launch_epi<false, true>(a->epi, P, tm, tn, nz, s);

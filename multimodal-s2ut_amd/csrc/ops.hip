@@ -154,30 +154,52 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy,
   }
 }
 
-__global__ void colsum_parts_kernel(const float* __restrict__ part, int nparts, int ncol,
-                                    h16* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncol) return;
+// [nparts][ncol] fp32 -> ncol: a block owns 64 columns, its 16 waves split the parts; fixed
+// summation order (deterministic).
+__global__ void __launch_bounds__(1024) colsum_parts_kernel(const float* __restrict__ part, int nparts, int ncol,
+                                                            h16* __restrict__ out, int accumulate) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(long)p * ncol + c];
-  if (accumulate) s += (float)out[c];
-  out[c] = (h16)s;
+  if (c < ncol) {
+#pragma unroll 4
+    for (int p = w; p < nparts; p += 16) s += part[(long)p * ncol + c];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < ncol) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    if (accumulate) t += (float)out[c];
+    out[c] = (h16)t;
+  }
 }
 
-constexpr int COLSUM_ROWS = 64;
-__global__ void colsum_f16_kernel(const h16* __restrict__ x, long rows, int cols, long ld,
-                                  float* __restrict__ part) {
-  const long r0 = (long)blockIdx.x * COLSUM_ROWS;
-  const long r1 = min(rows, r0 + COLSUM_ROWS);
-  for (int c4 = threadIdx.x; c4 * 4 < cols; c4 += blockDim.x) {
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    for (long r = r0; r < r1; ++r) {
-      h16x4 v = ld4(x + r * ld + c4 * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[e] += (float)v[e];
+// column sums of an fp16 [rows][cols] matrix: grid (cols/256, splits); 4 waves stride the
+// split's rows, each lane sums 4 adjacent columns (8-byte loads); LDS combine -> part[split][cols]
+constexpr int COLSUM_MAX_SPLITS = 64;
+__global__ void __launch_bounds__(256) colsum_f16_kernel(const h16* __restrict__ x, long rows, int cols, long ld,
+                                                         float* __restrict__ part, int splits) {
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 4;
+  const long per = (rows + splits - 1) / splits;
+  const long r0 = (long)blockIdx.y * per, r1 = min(rows, r0 + per);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+#pragma unroll 4
+    for (long r = r0 + w; r < r1; r += 4) {
+      h16x4 v = ld4(x + r * ld + c);
+      s += f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) part[(long)blockIdx.x * cols + c4 * 4 + e] = s[e];
+  }
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    const f32x4 t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    *reinterpret_cast<f32x4*>(part + (long)blockIdx.y * cols + c) = t;
   }
 }
 
@@ -565,19 +587,24 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
 extern "C" int mms2ut_colsum_parts(const float* part, int nparts, int ncol, h16* out, int accumulate,
                                    hipStream_t s) {
   if (ncol == 0) return 0;
-  hipLaunchKernelGGL(colsum_parts_kernel, dim3((ncol + 255) / 256), dim3(256), 0, s, part, nparts,
+  hipLaunchKernelGGL(colsum_parts_kernel, dim3((ncol + 63) / 64), dim3(1024), 0, s, part, nparts,
                      ncol, out, accumulate);
   return mms::check_launch("colsum_parts");
 }
 
-extern "C" int mms2ut_colsum_nparts(int64_t rows) { return (int)((rows + COLSUM_ROWS - 1) / COLSUM_ROWS); }
+extern "C" int mms2ut_colsum_nparts(int64_t rows) {
+  long sp = (rows + 63) / 64;
+  if (sp > COLSUM_MAX_SPLITS) sp = COLSUM_MAX_SPLITS;
+  return sp < 1 ? 1 : (int)sp;
+}
 
 extern "C" int mms2ut_colsum_f16(const h16* x, int64_t rows, int cols, int64_t ld, float* part,
                                  int nparts, hipStream_t s) {
   MMS_REQUIRE(cols % 4 == 0 && ld % 4 == 0, "colsum_f16: cols/ld must be multiples of 4");
   MMS_REQUIRE(nparts == mms2ut_colsum_nparts(rows), "colsum_f16: nparts mismatch");
   if (rows == 0) return 0;
-  hipLaunchKernelGGL(colsum_f16_kernel, dim3(nparts), dim3(256), 0, s, x, (long)rows, cols, (long)ld, part);
+  dim3 grid((cols / 4 + 63) / 64, nparts);
+  hipLaunchKernelGGL(colsum_f16_kernel, grid, dim3(256), 0, s, x, (long)rows, cols, (long)ld, part, nparts);
   return mms::check_launch("colsum_f16");
 }
 

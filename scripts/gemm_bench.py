@@ -1,0 +1,60 @@
+"""Micro-benchmark of the HIP GEMM on the training step's shapes (interleaved A/B of the two
+paths in one process; random operands).  Usage: python scripts/gemm_bench.py"""
+import importlib
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+mm = importlib.import_module("multimodal-s2ut_amd")
+K = mm.kernels
+
+M = 10000
+SHAPES = [  # name, M, N, K, a_kc, b_kc, splitk
+    ("qkv fwd", M, 2304, 768, True, True, 1),
+    ("fc1 fwd", M, 3072, 768, True, True, 1),
+    ("fc2 fwd", M, 768, 3072, True, True, 1),
+    ("out fwd", M, 768, 768, True, True, 1),
+    ("fc2 dgrad", M, 3072, 768, True, False, 1),
+    ("fc1 dgrad", M, 768, 3072, True, False, 1),
+    ("wgrad 3072x768", 3072, 768, M, False, False, 4),
+    ("wgrad 768x768", 768, 768, M, False, False, 15),
+    ("conv2 fwd", 10000, 1536, 2560, True, True, 1),
+]
+
+
+def run(name, m, n, k, a_kc, b_kc, s, reps=20):
+    A = torch.randn(m, k, device="cuda").half() if a_kc else torch.randn(k, m, device="cuda").half()
+    B = torch.randn(n, k, device="cuda").half() if b_kc else torch.randn(k, n, device="cuda").half()
+    if s > 1:
+        C = torch.empty(s, m, n, dtype=torch.float32, device="cuda")
+        epi = K.EPI_F32
+    else:
+        C = torch.empty(m, n, dtype=torch.float16, device="cuda")
+        epi = K.EPI_F16
+    res = {}
+    for rnd in range(3):
+        for path in ("reg", "dma"):
+            os.environ["MMS2UT_GEMM_PATH"] = path
+            for _ in range(2):
+                K.gemm(A, B, C, m, n, k, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=n,
+                       epi=epi, splitk=s, sCsplit=m * n)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                K.gemm(A, B, C, m, n, k, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=n,
+                       epi=epi, splitk=s, sCsplit=m * n)
+            e1.record()
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) / reps
+            res[path] = min(res.get(path, 1e9), t)
+    fl = 2.0 * m * n * k
+    print(f"{name:18s} M={m:6d} N={n:5d} K={k:6d}  reg {res['reg']*1e3:7.1f}us {fl/res['reg']/1e9:6.0f} TF"
+          f"   dma {res['dma']*1e3:7.1f}us {fl/res['dma']/1e9:6.0f} TF", flush=True)
+    os.environ.pop("MMS2UT_GEMM_PATH", None)
+
+
+if __name__ == "__main__":
+    for sh in SHAPES:
+        run(*sh)
