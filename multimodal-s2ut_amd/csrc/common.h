@@ -33,21 +33,48 @@ int check_launch(const char* what);
 // counter-based dropout RNG: keep(i) is a pure function of (seed, offset + i) so the backward
 // pass regenerates the forward mask without storing it.  Same stream for every kernel.
 // ------------------------------------------------------------------------------------------
-MMS_DEV uint32_t mms_hash(uint64_t seed, uint64_t ctr) {
-  uint64_t z = seed ^ (ctr * 0x9E3779B97F4A7C15ull);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+// 32-bit integer mixer (lowbias32: two 32-bit multiplies) — cheap enough for GEMM epilogues.
+MMS_DEV uint32_t mms_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
 }
-// keep with probability 1-p: hash >= p * 2^32
+// one 32-bit draw per PAIR of counters (ctr>>1); element ctr takes the low/high 16 bits.
+// keep(ctr) <=> u16 >= thresh16 with thresh16 = round(p * 65536): P(drop) = p to 1.5e-5.
+MMS_DEV uint32_t mms_hash(uint64_t seed, uint64_t ctr) {
+  const uint64_t pair = ctr >> 1;
+  const uint32_t s = (uint32_t)seed ^ mms_mix32((uint32_t)(seed >> 32) + 0x9e3779b9U);
+  const uint32_t h = mms_mix32((uint32_t)pair ^ mms_mix32((uint32_t)(pair >> 32) ^ s));
+  return (ctr & 1) ? (h >> 16) : (h & 0xffffU);
+}
 MMS_DEV bool mms_keep(uint64_t seed, uint64_t ctr, uint32_t thresh) {
   return mms_hash(seed, ctr) >= thresh;
 }
+// keep-flags of 4 consecutive counters ctr0..ctr0+3 (2 hashes when ctr0 is even)
+MMS_DEV void mms_keep4(uint64_t seed, uint64_t ctr0, uint32_t thresh, bool (&k)[4]) {
+  if ((ctr0 & 1) == 0) {
+    const uint32_t s = (uint32_t)seed ^ mms_mix32((uint32_t)(seed >> 32) + 0x9e3779b9U);
+    const uint64_t p0 = ctr0 >> 1;
+    const uint32_t h0 = mms_mix32((uint32_t)p0 ^ mms_mix32((uint32_t)(p0 >> 32) ^ s));
+    const uint64_t p1 = p0 + 1;
+    const uint32_t h1 = mms_mix32((uint32_t)p1 ^ mms_mix32((uint32_t)(p1 >> 32) ^ s));
+    k[0] = (h0 & 0xffffU) >= thresh;
+    k[1] = (h0 >> 16) >= thresh;
+    k[2] = (h1 & 0xffffU) >= thresh;
+    k[3] = (h1 >> 16) >= thresh;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) k[e] = mms_keep(seed, ctr0 + e, thresh);
+  }
+}
 static inline uint32_t mms_drop_thresh(float p) {
   if (p <= 0.f) return 0u;
-  double t = (double)p * 4294967296.0;
-  if (t >= 4294967295.0) return 4294967295u;
+  double t = (double)p * 65536.0 + 0.5;
+  if (t >= 65536.0) return 65536u;
+  if (t < 1.0) t = 1.0;
   return (uint32_t)t;
 }
 

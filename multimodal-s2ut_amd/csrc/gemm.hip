@@ -138,47 +138,73 @@ MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, in
     }
     return;
   }
+  const bool full = n + 3 < N;
   if (P.bias && EPI != MMS_EPI_RELU_DROP_BWD) {
+    if (full) {
+      const h16x4 bv = *reinterpret_cast<const h16x4*>(P.bias + n);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) if (n + r < N) x[r] += (float)P.bias[n + r];
+      for (int r = 0; r < 4; ++r) x[r] += (float)bv[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) if (n + r < N) x[r] += (float)P.bias[n + r];
+    }
   }
   h16* C = reinterpret_cast<h16*>(Cz) + (long)m * P.ldc;
-  float o[4];
+  // 4-wide operand fetches (aux row / existing C), zero beyond N
+  auto ld4 = [&](const h16* row, int col, float (&v)[4]) {
+    if (full) {
+      const h16x4 t = *reinterpret_cast<const h16x4*>(row + col);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float y = x[r];
-    const int nn = n + r;
-    if (EPI == MMS_EPI_RELU_DROP) {
-      y = fmaxf(y, 0.f);
-      if (P.thresh) {
-        const bool keep = mms_keep(P.seed, P.offset + (uint64_t)m * P.ld_rng + nn, P.thresh);
-        y = keep ? y * (1.f / (1.f - P.p)) : 0.f;
-      }
-    } else if (EPI == MMS_EPI_DROP_RESID) {
-      if (P.thresh) {
-        const bool keep = mms_keep(P.seed, P.offset + (uint64_t)m * P.ld_rng + nn, P.thresh);
-        y = keep ? y * (1.f / (1.f - P.p)) : 0.f;
-      }
-      if (nn < N) y += (float)auxz[(long)m * P.ldaux + nn];
-    } else if (EPI == MMS_EPI_GATE) {
-      if (nn < N) {
-        const float g = sigmoidf_(y);
-        const float ov = (float)auxz[(long)m * P.ldaux + nn];
-        const float tv = (float)auxz[(long)m * P.ldaux + nn + N];
-        P.out2[(long)m * P.ldo2 + nn] = (h16)g;
-        y = tv + g * (ov - tv);
-      }
-    } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
-      if (nn < N) {
-        const float h = (float)auxz[(long)m * P.ldaux + nn];
-        y = h > 0.f ? y * (P.thresh ? 1.f / (1.f - P.p) : 1.f) : 0.f;
-      }
-    } else if (EPI == MMS_EPI_F16_ACC) {
-      if (nn < N) y += (float)C[nn];
+      for (int r = 0; r < 4; ++r) v[r] = (float)t[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (n + r < N) ? (float)row[col + r] : 0.f;
     }
-    o[r] = y;
+  };
+  bool keep[4] = {true, true, true, true};
+  if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID) && P.thresh)
+    mms_keep4(P.seed, P.offset + (uint64_t)m * P.ld_rng + n, P.thresh, keep);
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  float o[4];
+  if (EPI == MMS_EPI_RELU_DROP) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = keep[r] ? fmaxf(x[r], 0.f) * dscale : 0.f;
+  } else if (EPI == MMS_EPI_DROP_RESID) {
+    float a[4];
+    ld4(auxz + (long)m * P.ldaux, n, a);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = a[r] + (keep[r] ? x[r] * dscale : 0.f);
+  } else if (EPI == MMS_EPI_GATE) {
+    float ov[4], tv[4];
+    ld4(auxz + (long)m * P.ldaux, n, ov);
+    ld4(auxz + (long)m * P.ldaux + N, n, tv);
+    float g[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      g[r] = sigmoidf_(x[r]);
+      o[r] = tv[r] + g[r] * (ov[r] - tv[r]);
+    }
+    h16* g_row = P.out2 + (long)m * P.ldo2;
+    if (full) {
+      *reinterpret_cast<h16x4*>(g_row + n) = h16x4{(h16)g[0], (h16)g[1], (h16)g[2], (h16)g[3]};
+    } else {
+      for (int r = 0; r < 4; ++r) if (n + r < N) g_row[n + r] = (h16)g[r];
+    }
+  } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
+    float h[4];
+    ld4(auxz + (long)m * P.ldaux, n, h);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
+  } else if (EPI == MMS_EPI_F16_ACC) {
+    float c[4];
+    ld4(C, n, c);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = c[r] + x[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = x[r];
   }
-  if (n + 3 < N) {
+  if (full) {
     *reinterpret_cast<h16x4*>(C + n) = h16x4{(h16)o[0], (h16)o[1], (h16)o[2], (h16)o[3]};
   } else {
     for (int r = 0; r < 4; ++r) if (n + r < N) C[n + r] = (h16)o[r];
@@ -329,8 +355,12 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   // buffer descriptors (block-uniform): K-contig base = operand, MN-contig base = row kbeg
   const h16* Ab = P.A + z1 * P.sA1 + z2 * P.sA2 + (A_KC ? 0 : (long)kbeg * P.lda);
   const h16* Bb = P.B + z1 * P.sB1 + z2 * P.sB2 + (B_KC ? 0 : (long)kbeg * P.ldb);
-  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2 : ((long)(kend - kbeg - 1) * P.lda + P.M) * 2;
-  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2 : ((long)(kend - kbeg - 1) * P.ldb + P.N) * 2;
+  // exact extents; MN-contiguous rows rounded up to whole 16-B chunks (a chunk straddling the
+  // range end would be dropped whole by the range check)
+  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.lda + ((P.M + 7) & ~7)) * 2;
+  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.ldb + ((P.N + 7) & ~7)) * 2;
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)a_ext, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)b_ext, 0x00020000);
 #define SA(s) (smem + (2 * (s)) * TILE_BYTES)
@@ -461,8 +491,12 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   hipStream_t s = stream;
   // LDS-DMA pipeline when every K-contiguous operand has whole 64-wide k-tiles and the operand
   // extents fit a buffer descriptor; otherwise the register-staged kernel (predicated tails)
-  const char* path_env = getenv("MMS2UT_GEMM_PATH");  // "reg" forces the register-staged kernel (A/B)
-  const bool force_reg = path_env && path_env[0] == 'r';
+  // default: register-staged kernel (measured faster on this step's shapes, round 1);
+  // MMS2UT_GEMM_PATH=dma selects the LDS-DMA pipeline for A/B measurements
+  const char* path_env = getenv("MMS2UT_GEMM_PATH");
+  const bool force_reg = !(path_env && path_env[0] == 'd');
+  MMS_REQUIRE(!a->aux || (a->ldaux % 4 == 0 && ((uintptr_t)a->aux & 7) == 0), "gemm: aux must be 8-B aligned with ldaux %% 4 == 0");
+  MMS_REQUIRE(!a->bias || ((uintptr_t)a->bias & 7) == 0, "gemm: bias must be 8-B aligned");
   const bool k_ok = (!a_kc || a->K % BK == 0) && (!b_kc || a->K % BK == 0);
   const long a_ext = a_kc ? (long)a->M * a->lda : (long)a->K * a->lda;
   const long b_ext = b_kc ? (long)a->N * a->ldb : (long)a->K * a->ldb;

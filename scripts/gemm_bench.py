@@ -55,6 +55,32 @@ def run(name, m, n, k, a_kc, b_kc, s, reps=20):
     os.environ.pop("MMS2UT_GEMM_PATH", None)
 
 
+def epilogues(m=10000, n=768, k=768, reps=20):
+    """Cost of the fused epilogues on the out-proj shape (register path)."""
+    x = torch.randn(m, k, device="cuda").half()
+    W = torch.randn(n, k, device="cuda").half()
+    b = torch.randn(n, device="cuda").half()
+    res = torch.randn(m, n, device="cuda").half()
+    out = torch.empty(m, n, dtype=torch.float16, device="cuda")
+    cases = [("plain", dict(epi=K.EPI_F16)), ("bias", dict(epi=K.EPI_F16, bias=b)),
+             ("resid p=0", dict(epi=K.EPI_DROP_RESID, bias=b, aux=res)),
+             ("resid p=.1", dict(epi=K.EPI_DROP_RESID, bias=b, aux=res, p=0.1, drop=(1, 0))),
+             ("relu p=.1", dict(epi=K.EPI_RELU_DROP, bias=b, p=0.1, drop=(1, 0)))]
+    for name, kw in cases:
+        for _ in range(2):
+            K.linear(x, W, out=out, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            K.linear(x, W, out=out, **kw)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / reps
+        print(f"epilogue {name:12s} {t*1e3:7.1f}us {2.0*m*n*k/t/1e9:6.0f} TF", flush=True)
+
+
 if __name__ == "__main__":
     for sh in SHAPES:
         run(*sh)
+    epilogues()
+    epilogues(n=3072)
