@@ -425,13 +425,22 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
     }
 }
 
-constexpr int DMA_STAGES = 3;
-
 template <bool A_KC, bool B_KC>
 int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   dim3 grid(tm * tn, nz), block(NT);
+  const char* st = getenv("MMS2UT_DMA_STAGES");
+  if (st && st[0] == '2') {
+    switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 2>), grid, block, 0, s, P, tm, tn); break;
+      CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
+      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+#undef CASE
+      default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
+    }
+    return mms::check_launch("gemm_dma2");
+  }
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, DMA_STAGES>), grid, block, 0, s, P, tm, tn); break;
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 3>), grid, block, 0, s, P, tm, tn); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
     CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
 #undef CASE

@@ -35,8 +35,9 @@ def run(name, m, n, k, a_kc, b_kc, s, reps=20):
         epi = K.EPI_F16
     res = {}
     for rnd in range(3):
-        for path in ("reg", "dma"):
+        for path in ("reg", "dma", "dma2"):
             os.environ["MMS2UT_GEMM_PATH"] = path
+            os.environ["MMS2UT_DMA_STAGES"] = "2" if path == "dma2" else "3"
             for _ in range(2):
                 K.gemm(A, B, C, m, n, k, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=n,
                        epi=epi, splitk=s, sCsplit=m * n)
@@ -51,7 +52,8 @@ def run(name, m, n, k, a_kc, b_kc, s, reps=20):
             res[path] = min(res.get(path, 1e9), t)
     fl = 2.0 * m * n * k
     print(f"{name:18s} M={m:6d} N={n:5d} K={k:6d}  reg {res['reg']*1e3:7.1f}us {fl/res['reg']/1e9:6.0f} TF"
-          f"   dma {res['dma']*1e3:7.1f}us {fl/res['dma']/1e9:6.0f} TF", flush=True)
+          f"   dma {res['dma']*1e3:7.1f}us {fl/res['dma']/1e9:6.0f} TF"
+          f"   dma2 {res['dma2']*1e3:7.1f}us {fl/res['dma2']/1e9:6.0f} TF", flush=True)
     os.environ.pop("MMS2UT_GEMM_PATH", None)
 
 
