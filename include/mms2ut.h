@@ -206,9 +206,10 @@ int mms2ut_adam_fp16_master(mms2ut_half* param, const mms2ut_half* grad, float* 
  * (data-config feature transform) and zero-padded fp16 collation [B][Tmax][nbins]
  * (_collate_frames).  wave: concatenated fp32 samples (x 2^15), wave_off[B+1].              */
 int mms2ut_fbank_frames(const int64_t* wave_off, int B, int32_t* n_frames_out, hipStream_t stream);
+/* mel_range[2*m], mel_range[2*m+1]: first / one-past-last nonzero FFT bin of filter m */
 int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, const int32_t* frame_off, int B,
-                     int total_frames, const float* mel_banks, int nbins, float* feats,
-                     hipStream_t stream);
+                     int total_frames, const float* mel_banks, const int32_t* mel_range, int nbins,
+                     float* feats, hipStream_t stream);
 int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
                               int nbins, int cmvn, mms2ut_half* out, hipStream_t stream);
 

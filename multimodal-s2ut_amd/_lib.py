@@ -72,7 +72,7 @@ SIGNATURES = {
     "mms2ut_optim_prepare": (i32, [vp, f32, f32, f32, f32, f32, f32, vp]),
     "mms2ut_adam_fp16_master": (i32, [vp, vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, f32, vp]),
     "mms2ut_fbank_frames": (i32, [vp, i32, vp, vp]),
-    "mms2ut_fbank_f32": (i32, [vp, vp, vp, i32, i32, vp, i32, vp, vp]),
+    "mms2ut_fbank_f32": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
     "mms2ut_fbank_cmvn_collate": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
 }
 

@@ -23,7 +23,8 @@ MMS_DEV int bitrev9(int x) { return (int)(__builtin_bitreverse32((unsigned)x) >>
 
 __global__ void __launch_bounds__(256) fbank_kernel(const float* __restrict__ wave, const int64_t* __restrict__ wave_off,
                                                     const int* __restrict__ frame_off, int B, int total,
-                                                    const float* __restrict__ banks, int nbins,
+                                                    const float* __restrict__ banks,
+                                                    const int* __restrict__ mel_range, int nbins,
                                                     float* __restrict__ feats) {
   __shared__ float s_re[4][NFFT], s_im[4][NFFT], s_x[4][WIN + 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -96,10 +97,8 @@ __global__ void __launch_bounds__(256) fbank_kernel(const float* __restrict__ wa
   for (int m = lane; m < nbins; m += 64) {
     const float* bk = banks + (long)m * NBIN;
     float acc = 0.f;
-    for (int k = 0; k < NBIN; ++k) {
-      const float wgt = bk[k];
-      if (wgt != 0.f) acc += wgt * X[k];
-    }
+    const int k0 = mel_range[2 * m], k1 = mel_range[2 * m + 1];  // triangle support only
+    for (int k = k0; k < k1; ++k) acc += bk[k] * X[k];
     feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
   }
 }
@@ -169,13 +168,14 @@ extern "C" int mms2ut_fbank_frames(const int64_t* wave_off, int B, int32_t* n_fr
 }
 
 extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, const int32_t* frame_off, int B,
-                                int total_frames, const float* mel_banks, int nbins, float* feats,
-                                hipStream_t s) {
+                                int total_frames, const float* mel_banks, const int32_t* mel_range, int nbins,
+                                float* feats, hipStream_t s) {
   MMS_REQUIRE(nbins > 0 && nbins <= 256, "fbank: nbins must be in (0, 256]");
+  MMS_REQUIRE(mel_range != nullptr, "fbank: mel_range required");
   if (init_consts(s)) return 1;
   if (total_frames == 0) return 0;
   hipLaunchKernelGGL(fbank_kernel, dim3((total_frames + 3) / 4), dim3(256), 0, s, wave, wave_off, frame_off, B,
-                     total_frames, mel_banks, nbins, feats);
+                     total_frames, mel_banks, mel_range, nbins, feats);
   return mms::check_launch("fbank");
 }
 

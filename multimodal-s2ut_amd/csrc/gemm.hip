@@ -428,8 +428,9 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
 template <bool A_KC, bool B_KC>
 int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   dim3 grid(tm * tn, nz), block(NT);
+  // 2 stages (64 KiB LDS, 2 blocks/CU) measured fastest on this step's shapes; 3 = 1 block/CU
   const char* st = getenv("MMS2UT_DMA_STAGES");
-  if (st && st[0] == '2') {
+  if (!(st && st[0] == '3')) {
     switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 2>), grid, block, 0, s, P, tm, tn); break;
       CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
@@ -500,10 +501,10 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   hipStream_t s = stream;
   // LDS-DMA pipeline when every K-contiguous operand has whole 64-wide k-tiles and the operand
   // extents fit a buffer descriptor; otherwise the register-staged kernel (predicated tails)
-  // default: register-staged kernel (measured faster on this step's shapes, round 1);
-  // MMS2UT_GEMM_PATH=dma selects the LDS-DMA pipeline for A/B measurements
+  // default: LDS-DMA pipeline (2 stages); MMS2UT_GEMM_PATH=reg forces the register-staged
+  // kernel for A/B measurements (scripts/gemm_bench.py)
   const char* path_env = getenv("MMS2UT_GEMM_PATH");
-  const bool force_reg = !(path_env && path_env[0] == 'd');
+  const bool force_reg = path_env && path_env[0] == 'r';
   MMS_REQUIRE(!a->aux || (a->ldaux % 4 == 0 && ((uintptr_t)a->aux & 7) == 0), "gemm: aux must be 8-B aligned with ldaux %% 4 == 0");
   MMS_REQUIRE(!a->bias || ((uintptr_t)a->bias & 7) == 0, "gemm: bias must be 8-B aligned");
   const bool k_ok = (!a_kc || a->K % BK == 0) && (!b_kc || a->K % BK == 0);

@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, 
   }
 }
 
-constexpr int LN_BWD_ROWS = 32;  // rows per block (8 per wave)
+constexpr int LN_BWD_ROWS = 16;  // rows per block (4 per wave): ~600 blocks for 10k rows
 
 template <int CPL>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy, const h16* __restrict__ x,

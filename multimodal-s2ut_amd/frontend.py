@@ -47,7 +47,14 @@ class FbankFrontend:
         self.device = torch.device(device)
         self.num_bins = num_bins
         self.cmvn = cmvn
-        self.banks = torch.from_numpy(mel_banks(num_bins)).to(self.device)
+        banks = mel_banks(num_bins)
+        self.banks = torch.from_numpy(banks).to(self.device)
+        nz = banks > 0
+        lo = nz.argmax(1)
+        hi = banks.shape[1] - nz[:, ::-1].argmax(1)
+        lo[~nz.any(1)] = hi[~nz.any(1)] = 0
+        rng = np.stack([lo, hi], 1).astype(np.int32)
+        self.mel_range = torch.from_numpy(rng.reshape(-1)).to(self.device)
 
     def upload(self, waves):
         """waves: list of 1-D float32 arrays already in int16 range (get_waveform(normalization=False)).
@@ -69,9 +76,11 @@ class FbankFrontend:
         }
 
     def __call__(self, wb):
-        feats = K.fbank(wb["wave"], wb["wave_off"], wb["frame_off"], wb["total"], self.banks, self.num_bins)
+        feats = K.fbank(wb["wave"], wb["wave_off"], wb["frame_off"], wb["total"], self.banks, self.mel_range,
+                        self.num_bins)
         return K.cmvn_collate(feats, wb["frame_off"], wb["B"], wb["Tmax"], self.num_bins, self.cmvn)
 
     def features_f32(self, wb):
         """Raw log-mel features [total_frames, nbins] fp32 (no CMVN) — for parity tests."""
-        return K.fbank(wb["wave"], wb["wave_off"], wb["frame_off"], wb["total"], self.banks, self.num_bins)
+        return K.fbank(wb["wave"], wb["wave_off"], wb["frame_off"], wb["total"], self.banks, self.mel_range,
+                       self.num_bins)

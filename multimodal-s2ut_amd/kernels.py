@@ -337,11 +337,11 @@ def adam(param, grad, master, m, v, ost, lr, beta1, beta2, eps, wd):
 # ============================================================================ fbank
 
 
-def fbank(wave, wave_off, frame_off, total_frames, banks, nbins=80):
+def fbank(wave, wave_off, frame_off, total_frames, banks, mel_range, nbins=80):
     feats = torch.empty(total_frames, nbins, dtype=torch.float32, device=wave.device)
     B = wave_off.numel() - 1
     call("mms2ut_fbank_f32", wave.data_ptr(), wave_off.data_ptr(), frame_off.data_ptr(), B,
-         total_frames, banks.data_ptr(), nbins, feats.data_ptr(), _s())
+         total_frames, banks.data_ptr(), mel_range.data_ptr(), nbins, feats.data_ptr(), _s())
     return feats
 
 

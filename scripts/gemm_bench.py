@@ -37,7 +37,7 @@ def run(name, m, n, k, a_kc, b_kc, s, reps=20):
     for rnd in range(3):
         for path in ("reg", "dma", "dma2"):
             os.environ["MMS2UT_GEMM_PATH"] = path
-            os.environ["MMS2UT_DMA_STAGES"] = "2" if path == "dma2" else "3"
+            os.environ["MMS2UT_DMA_STAGES"] = "3" if path == "dma" else "2"
             for _ in range(2):
                 K.gemm(A, B, C, m, n, k, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=n,
                        epi=epi, splitk=s, sCsplit=m * n)

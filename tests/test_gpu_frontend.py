@@ -1,0 +1,56 @@
+"""GPU: fbank front end (HIP) vs the numpy oracle restating torchaudio.compliance.kaldi.fbank
+(oracle/ref_fbank.py, itself cross-checked against transformers' Kaldi implementation).
+Tolerance: |log-mel difference| <= 2e-3 (fp32 FFT summation order), CMVN output <= 5e-3 (fp16)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg
+from oracle import ref_fbank as RF
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fe():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return pkg().frontend.FbankFrontend("cuda")
+
+
+def test_fbank_matches_oracle(fe):
+    rng = np.random.default_rng(3)
+    frames = [1, 2, 57, 300, 133]
+    waves = [RF.synth_wave(T, rng) for T in frames]
+    waves.append(rng.standard_normal(399).astype(np.float32) * 1000)   # < 1 frame -> 0 frames
+    waves.append((rng.standard_normal(160 * 40 + 300) * 3000).astype(np.float32))  # ragged tail
+    wb = fe.upload(waves)
+    feats = fe.features_f32(wb).cpu().numpy()
+    off = wb["frame_off"].cpu().numpy()
+    for j, i in enumerate(wb["order"]):
+        ref = RF.fbank(waves[i])
+        got = feats[off[j]:off[j + 1]]
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        if ref.size:
+            assert np.abs(got - ref).max() < 2e-3, np.abs(got - ref).max()
+
+
+def test_fbank_cmvn_collate(fe):
+    rng = np.random.default_rng(4)
+    frames = [80, 120, 31]
+    waves = [RF.synth_wave(T, rng) for T in frames]
+    wb = fe.upload(waves)
+    out = fe(wb).float().cpu().numpy()
+    assert out.shape == (3, 120, 80)
+    for j, i in enumerate(wb["order"]):
+        ref = RF.utterance_cmvn(RF.fbank(waves[i]))
+        T = ref.shape[0]
+        assert np.abs(out[j, :T] - ref).max() < 5e-3
+        assert np.all(out[j, T:] == 0)
+
+
+def test_fbank_silence_floor(fe):
+    """All-zero input: power 0 -> log(FLT_EPSILON) everywhere (the reference's epsilon floor)."""
+    wb = fe.upload([np.zeros(160 * 5 + 240, np.float32)])
+    f = fe.features_f32(wb).cpu().numpy()
+    np.testing.assert_allclose(f, np.log(np.float32(np.finfo(np.float32).eps)), rtol=1e-6)
