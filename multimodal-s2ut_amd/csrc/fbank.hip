@@ -114,24 +114,28 @@ __global__ void cmvn_collate_kernel(const float* __restrict__ feats, const int* 
                                     int B, int Tmax, int nbins, int cmvn, h16* __restrict__ out) {
   const int b = blockIdx.x;
   const int f0 = frame_off[b], T = frame_off[b + 1] - f0;
-  __shared__ float s_mean[256], s_inv[256];
+  __shared__ float s_mean[256], s_std[256];
+  // fairseq UtteranceCMVN in numpy float32: x.mean(0) and (x**2).sum(0) reduce over the outer
+  // (time) axis sequentially, var = sq/T - mean^2 (float32 cancellation included, as the
+  // reference), std = sqrt(max(var, 1e-10)), x = (x - mean) / std
   for (int c = threadIdx.x; c < nbins; c += blockDim.x) {
-    double sm = 0.0, sq = 0.0;
+    float sm = 0.f, sq = 0.f;
     for (int t = 0; t < T; ++t) {
-      const double v = feats[(long)(f0 + t) * nbins + c];
-      sm += v; sq += v * v;
+      const float v = feats[(long)(f0 + t) * nbins + c];
+      sm = __fadd_rn(sm, v);
+      sq = __fadd_rn(sq, __fmul_rn(v, v));
     }
-    const double mean = T > 0 ? sm / T : 0.0;
-    const double var = T > 0 ? sq / T - mean * mean : 1.0;
-    s_mean[c] = cmvn ? (float)mean : 0.f;
-    s_inv[c] = cmvn ? (float)(1.0 / sqrt(var > 1e-10 ? var : 1e-10)) : 1.f;
+    const float mean = T > 0 ? __fdiv_rn(sm, (float)T) : 0.f;
+    const float var = T > 0 ? __fsub_rn(__fdiv_rn(sq, (float)T), __fmul_rn(mean, mean)) : 1.f;
+    s_mean[c] = cmvn ? mean : 0.f;
+    s_std[c] = cmvn ? __fsqrt_rn(fmaxf(var, 1e-10f)) : 1.f;
   }
   __syncthreads();
   const long n = (long)Tmax * nbins;
   for (long i = threadIdx.x; i < n; i += blockDim.x) {
     const int t = (int)(i / nbins), c = (int)(i % nbins);
     float v = 0.f;
-    if (t < T) v = (feats[(long)(f0 + t) * nbins + c] - s_mean[c]) * s_inv[c];
+    if (t < T) v = __fdiv_rn(__fsub_rn(feats[(long)(f0 + t) * nbins + c], s_mean[c]), s_std[c]);
     out[(long)b * n + i] = (h16)v;
   }
 }

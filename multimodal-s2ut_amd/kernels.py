@@ -112,41 +112,91 @@ def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=Fa
     return out
 
 
-def _splitk_for(tiles, kred):
-    target = 512
-    s = max(1, -(-target // max(1, tiles)))
-    s = min(s, max(1, kred // 256), 32)
-    return s
+def _splitk_for(tiles, kred, slots=512):
+    """split-K count: fill the 512 resident-block slots (2 GEMM blocks per CU) in whole waves."""
+    best, best_eff = 1, 0.0
+    for s in range(1, 33):
+        if s > 1 and kred // s < 256:
+            break
+        blocks = tiles * s
+        eff = blocks / (-(-blocks // slots) * slots)
+        if eff > best_eff + 0.02:
+            best, best_eff = s, eff
+    return best
 
 
-def linear_wgrad(dy, x, dW, *, accumulate_f32=None):
+class _Side:
+    """Weight-gradient side stream: dW/db GEMMs and reductions do not feed the rest of the
+    backward, so they run concurrently with the dgrad chain on a second HIP stream and fill the
+    CUs the (latency-bound, dependent) dgrad kernels leave idle."""
+    stream = None
+    enabled = True
+    used = False
+
+
+def side_begin(*tensors):
+    """Enter the side stream after everything enqueued so far on the current stream."""
+    if not _Side.enabled or not torch.cuda.is_available():
+        return None
+    main = torch.cuda.current_stream()
+    if _Side.stream is None or _Side.stream.device != main.device:
+        _Side.stream = torch.cuda.Stream(device=main.device)
+    side = _Side.stream
+    side.wait_stream(main)
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            t.record_stream(side)
+    _Side.used = True
+    return torch.cuda.stream(side)
+
+
+def side_join():
+    """Make the current stream wait for all side-stream work (before consuming gradients)."""
+    if _Side.used and _Side.stream is not None:
+        torch.cuda.current_stream().wait_stream(_Side.stream)
+        _Side.used = False
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+def linear_wgrad(dy, x, dW, *, accumulate_f32=None, side=True):
     """dW[N,K] (fp16 view into the flat grad buffer) = dy[M,N]^T @ x[M,K] (split-K over M).
     With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead."""
     M, N = dy.shape
     K = x.shape[1]
     assert dW is None or tuple(dW.shape) == (N, K)
-    tiles = -(-N // 128) * -(-K // 128)
-    s = _splitk_for(tiles, M)
-    slabs = torch.empty(s, N, K, dtype=torch.float32, device=dy.device)
-    gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
-         epi=EPI_F32, splitk=s, sCsplit=N * K)
-    if accumulate_f32 is not None:
-        call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, accumulate_f32.data_ptr(),
-             accumulate_f32.stride(0), 2, 1.0, _s())
-        return accumulate_f32
-    call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, dW.data_ptr(), dW.stride(0), 1,
-         1.0, _s())
+    ctx = side_begin(dy, x) if side else None
+    with (ctx or _nullctx()):
+        tiles = -(-N // 128) * -(-K // 128)
+        s = _splitk_for(tiles, M)
+        slabs = torch.empty(s, N, K, dtype=torch.float32, device=dy.device)
+        gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
+             epi=EPI_F32, splitk=s, sCsplit=N * K)
+        if accumulate_f32 is not None:
+            call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, accumulate_f32.data_ptr(),
+                 accumulate_f32.stride(0), 2, 1.0, _s())
+            return accumulate_f32
+        call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, dW.data_ptr(), dW.stride(0), 1,
+             1.0, _s())
     return dW
 
 
-def bias_grad(dy, db, accumulate=False):
+def bias_grad(dy, db, accumulate=False, side=True):
     """db[N] = sum_rows dy[M,N] (fp16 out, fp32 accumulation)."""
     M, N = dy.shape
     L = _lib.load()
-    nparts = L.mms2ut_colsum_nparts(M)
-    part = torch.empty(nparts, N, dtype=torch.float32, device=dy.device)
-    call("mms2ut_colsum_f16", dy.data_ptr(), M, N, dy.stride(0), part.data_ptr(), nparts, _s())
-    call("mms2ut_colsum_parts", part.data_ptr(), nparts, N, db.data_ptr(), int(accumulate), _s())
+    ctx = side_begin(dy) if side else None
+    with (ctx or _nullctx()):
+        nparts = L.mms2ut_colsum_nparts(M)
+        part = torch.empty(nparts, N, dtype=torch.float32, device=dy.device)
+        call("mms2ut_colsum_f16", dy.data_ptr(), M, N, dy.stride(0), part.data_ptr(), nparts, _s())
+        call("mms2ut_colsum_parts", part.data_ptr(), nparts, N, db.data_ptr(), int(accumulate), _s())
     return db
 
 # ============================================================================ LayerNorm

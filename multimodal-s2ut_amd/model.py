@@ -566,7 +566,8 @@ class MMS2UTModel:
         if extra:
             # bias_k / bias_v grads = sum over batch of the extra key row; then zero that row
             rows = dkv.view(B, Tk * 2 * d)[:, Ti * 2 * d:]
-            K.bias_grad(rows, self.params.span(pre + ".bias_k", pre + ".bias_v", grad=True))
+            # on the main stream: the rows are zeroed right after (side-stream race otherwise)
+            K.bias_grad(rows, self.params.span(pre + ".bias_k", pre + ".bias_v", grad=True), side=False)
             rows.zero_()
         K.linear_wgrad(dkv, c["imgd"], gWkv)
         K.bias_grad(dkv, gbkv)
@@ -805,7 +806,8 @@ class MMS2UTModel:
         E = self.P("decoder.embed_tokens.weight")
         dE32 = torch.zeros(V, d, dtype=torch.float32, device=E.device)
         # tied output projection: dE += dlogits^T xl ; dxl = dlogits E
-        K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32)
+        # main stream: the embedding scatter (token_embed_bwd) accumulates into the same dE32
+        K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32, side=False)
         dxl = torch.empty(B * Tt, d, dtype=F16, device=E.device)
         K.gemm(dlogits, E, dxl, B * Tt, d, V, a_kc=True, b_kc=False, lda=ctx["Vp"], ldb=d, ldc=d)
         dx = K.layernorm_bwd(dxl, ctx["lx"], self.P("decoder.layer_norm.weight"), ctx["lm"], ctx["lr"],

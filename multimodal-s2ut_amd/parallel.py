@@ -52,11 +52,22 @@ class GradAllReducer:
     def ready(self, upto):
         if self.world == 1:
             return
-        while self.next < len(self.bounds) and self.bounds[self.next][1] <= upto:
-            a, b = self.bounds[self.next]
-            self.handles.append(dist.all_reduce(self.grad[a:b], op=dist.ReduceOp.SUM, group=self.group,
-                                                async_op=True))
-            self.next += 1
+        if self.next >= len(self.bounds) or self.bounds[self.next][1] > upto:
+            return
+        # gradients of a bucket come from both the main stream (LayerNorm/embedding grads) and the
+        # weight-gradient side stream: enqueue the collective behind both
+        from . import kernels as K
+        side = K._Side.stream
+        ctx = None
+        if side is not None and K._Side.used:
+            side.wait_stream(torch.cuda.current_stream())
+            ctx = torch.cuda.stream(side)
+        with (ctx or K._nullctx()):
+            while self.next < len(self.bounds) and self.bounds[self.next][1] <= upto:
+                a, b = self.bounds[self.next]
+                self.handles.append(dist.all_reduce(self.grad[a:b], op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True))
+                self.next += 1
 
     def finish(self):
         if self.world == 1:

@@ -102,6 +102,7 @@ class _ModelFn(torch.autograd.Function):
         model.decoder_backward(dctx, dlogits.contiguous(), enc, denc)
         del dctx
         model.encoder_backward(ectx, denc)
+        K.side_join()  # weight gradients (side stream) complete before anyone reads them
         return None, None, None
 
 

@@ -43,9 +43,15 @@ def test_fbank_cmvn_collate(fe):
     out = fe(wb).float().cpu().numpy()
     assert out.shape == (3, 120, 80)
     for j, i in enumerate(wb["order"]):
-        ref = RF.utterance_cmvn(RF.fbank(waves[i]))
+        raw = RF.fbank(waves[i])
+        ref = RF.utterance_cmvn(raw)
         T = ref.shape[0]
-        assert np.abs(out[j, :T] - ref).max() < 5e-3
+        # fairseq's float32 var = E[x^2] - mean^2 is ill-conditioned when mean^2/var is large
+        # (e.g. the pure-tone bin: mean 24, std 0.06 -> cond 1.6e5): there the reference itself
+        # is only good to ~cond * 2^-24; elsewhere the HIP kernel must agree to fp16 precision
+        cond = raw.mean(0).astype(np.float64) ** 2 / np.maximum(raw.var(0, dtype=np.float64), 1e-10)
+        tol = np.where(cond > 1e4, 0.2, 5e-3)
+        assert np.all(np.abs(out[j, :T] - ref) <= tol[None, :])
         assert np.all(out[j, T:] == 0)
 
 
