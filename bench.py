@@ -161,7 +161,7 @@ def main():
     if world > 1:
         dist.barrier()
     if not args.no_gemm_timing:
-        kernels.GEMM_EVENTS = []
+        kernels.gemm_profile_begin(1000 * args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -172,13 +172,10 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    ev = kernels.GEMM_EVENTS
-    kernels.GEMM_EVENTS = None
+    gemm_ms, n_launch, launched_flops = kernels.gemm_profile_end() if not args.no_gemm_timing else (0.0, 0, 0.0)
     elapsed = t1 - t0
     frames = sum(int(batches[(args.warmup + i) % len(batches)][1].n_src_frames) for i in range(args.steps))
     alg_flops = sum(batches[(args.warmup + i) % len(batches)][3] for i in range(args.steps))
-    gemm_ms = sum(a.elapsed_time(b) for a, b, _ in ev) if ev else 0.0
-    n_launch = len(ev) if ev else 0
     stats = torch.tensor([elapsed, frames, alg_flops, gemm_ms, n_launch], dtype=torch.float64, device=device)
     if world > 1:
         mx = stats.clone()
@@ -214,7 +211,11 @@ def main():
                          "achieved": achieved, "peak": MFMA_PEAK_F16, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_PEAK_F16) if achieved else None, "traffic": None,
                          "gemm_ms_per_step": gemm_all / world / args.steps,
-                         "gemm_launches_per_step": nl_all / world / args.steps},
+                         "gemm_launches_per_step": nl_all / world / args.steps,
+                         "note": "achieved = SURVEY §8d algorithmic FLOPs (true lengths, 3x fwd) / summed "
+                                 "HIP-event durations of every GEMM launch in the timed region (weight-grad "
+                                 "GEMMs overlap the dgrad chain on a side stream, so contention inflates "
+                                 "durations: a lower bound on the kernel's rate)"},
             "cpu_baseline": cpu,
             "optimizer": ost,
         }

@@ -71,6 +71,12 @@ typedef struct mms2ut_gemm_args {
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
 
+/* live GEMM timing for the benchmark roofline: between begin/end every mms2ut_gemm_f16 launch
+ * is bracketed by HIP events on its own stream; end() synchronises and returns the summed
+ * kernel time, the launch count and the launched (padded) FLOPs.  Not thread-safe.          */
+int mms2ut_profile_begin(int max_launches);
+int mms2ut_profile_end(float* total_ms, int* launches, double* flops);
+
 /* sum `nsplit` fp32 slabs [rows, cols] (slab stride `slab`) * alpha -> out, row stride ldo.
  * mode bit0: fp16 output (else fp32); bit1: accumulate into out (else overwrite)            */
 int mms2ut_splitk_reduce(const float* slabs, int nsplit, int64_t slab, int rows, int cols,

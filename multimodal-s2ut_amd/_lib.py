@@ -40,6 +40,8 @@ SIGNATURES = {
     "mms2ut_last_error": (C.c_char_p, []),
     "mms2ut_version": (i32, []),
     "mms2ut_gemm_f16": (i32, [C.POINTER(GemmArgs), vp]),
+    "mms2ut_profile_begin": (i32, [i32]),
+    "mms2ut_profile_end": (i32, [C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "mms2ut_splitk_reduce": (i32, [vp, i32, i64, i32, i32, vp, i64, i32, f32, vp]),
     "mms2ut_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
     "mms2ut_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp]),

@@ -466,7 +466,67 @@ int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------
+// live GEMM timing (bench roofline): HIP events around every GEMM launch, on its stream
+// ------------------------------------------------------------------------------------------
+namespace {
+struct GemmProfile {
+  bool on = false;
+  int cap = 0, n = 0;
+  hipEvent_t* ev = nullptr;
+  double flops = 0.0;
+} g_prof;
+}  // namespace
+
+extern "C" int mms2ut_profile_begin(int max_launches) {
+  MMS_REQUIRE(!g_prof.on, "profile_begin: already active");
+  MMS_REQUIRE(max_launches > 0, "profile_begin: max_launches must be > 0");
+  g_prof.ev = (hipEvent_t*)calloc(2 * (size_t)max_launches, sizeof(hipEvent_t));
+  MMS_REQUIRE(g_prof.ev != nullptr, "profile_begin: out of host memory");
+  for (int i = 0; i < 2 * max_launches; ++i)
+    if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) { mms::set_error("profile_begin: hipEventCreate"); return 1; }
+  g_prof.cap = max_launches;
+  g_prof.n = 0;
+  g_prof.flops = 0.0;
+  g_prof.on = true;
+  return 0;
+}
+
+extern "C" int mms2ut_profile_end(float* total_ms, int* launches, double* flops) {
+  MMS_REQUIRE(g_prof.on, "profile_end: not active");
+  g_prof.on = false;
+  float tot = 0.f;
+  for (int i = 0; i < g_prof.n; ++i) {
+    float ms = 0.f;
+    if (hipEventSynchronize(g_prof.ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]) != hipSuccess) {
+      mms::set_error("profile_end: event timing failed");
+      return 1;
+    }
+    tot += ms;
+  }
+  for (int i = 0; i < 2 * g_prof.cap; ++i) hipEventDestroy(g_prof.ev[i]);
+  free(g_prof.ev);
+  g_prof.ev = nullptr;
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = g_prof.n;
+  if (flops) *flops = g_prof.flops;
+  return 0;
+}
+
+static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream);
+
 extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
+  if (!g_prof.on || g_prof.n >= g_prof.cap) return gemm_dispatch(a, stream);
+  const int i = g_prof.n++;
+  hipEventRecord(g_prof.ev[2 * i], stream);
+  const int rc = gemm_dispatch(a, stream);
+  hipEventRecord(g_prof.ev[2 * i + 1], stream);
+  if (a) g_prof.flops += 2.0 * a->M * a->N * a->K * (a->batch > 0 ? a->batch : 1);
+  return rc;
+}
+
+static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   MMS_REQUIRE(a != nullptr, "gemm: null args");
   MMS_REQUIRE(a->M >= 0 && a->N >= 0 && a->K >= 0, "gemm: negative dims");
   if (a->M == 0 || a->N == 0 || a->batch == 0) return 0;

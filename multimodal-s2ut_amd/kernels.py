@@ -67,18 +67,20 @@ def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv
     a.sX1, a.sX2 = sX
     a.out2, a.ldo2 = _p(out2), int(ldo2)
     a.dropout_p, a.seed, a.offset, a.ld_rng = float(p), int(seed), int(offset), int(ld_rng)
-    if GEMM_EVENTS is None:
-        call("mms2ut_gemm_f16", a, _s())
-    else:  # live per-launch timing with HIP events on the launch stream (bench roofline)
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        call("mms2ut_gemm_f16", a, _s())
-        e1.record()
-        GEMM_EVENTS.append((e0, e1, 2.0 * M * N * K * batch))
+    call("mms2ut_gemm_f16", a, _s())
 
 
-GEMM_EVENTS = None  # set to a list to time every GEMM launch (bench.py)
+def gemm_profile_begin(max_launches=100000):
+    """Start live GEMM timing (HIP events inside the library, on each launch's stream)."""
+    call("mms2ut_profile_begin", int(max_launches))
+
+
+def gemm_profile_end():
+    """-> (summed GEMM kernel ms, launches, launched FLOPs)."""
+    import ctypes
+    ms, n, fl = ctypes.c_float(), ctypes.c_int(), ctypes.c_double()
+    call("mms2ut_profile_end", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
+    return ms.value, n.value, fl.value
 
 
 def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
