@@ -120,6 +120,36 @@ int mms2ut_attn_softmax_bwd(const mms2ut_half* P, const mms2ut_half* dPd, mms2ut
                             int extra_key, float p, uint64_t seed, uint64_t offset,
                             hipStream_t stream);
 
+/* ---------------------------------------------------------------- fused multi-head attention
+ * Flash-style fwd/bwd (scores stay on chip) for fairseq MultiheadAttention in the encoder
+ * (self, key padding), decoder (causal self + target padding) and decoder cross attention
+ * (encoder padding): softmax(scale * q k^T + masks) -> dropout(p) -> @ v, per (b, h).
+ * Element (b, h, t, d) of X lives at X[b*sXb + t*ldX + h*hd + d] (sXb = 0 -> T*ldX).
+ * Padding: keys j >= key_len[b] masked (key_len may be null).  head_dim in {64, 96, 128}.
+ * lse[z*Tq + t] (z = b*H + h) receives the row log-sum-exp for the backward pass.          */
+typedef struct mms2ut_attn_args {
+  const mms2ut_half* q;
+  const mms2ut_half* k;
+  const mms2ut_half* v;
+  mms2ut_half* o;
+  int64_t ldq, ldk, ldv, ldo;
+  int64_t sqb, skb, svb, sob;
+  int B, H, Tq, Tk, hd;
+  const int32_t* key_len;
+  int causal;
+  float scale;
+  float p;
+  uint64_t seed, offset;
+  float* lse;
+} mms2ut_attn_args;
+
+int mms2ut_mha_varlen_fwd(const mms2ut_attn_args* args, hipStream_t stream);
+/* dq/dk/dv written (not accumulated); Dd: fp32 workspace [B*H*Tq]                          */
+int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* args, const mms2ut_half* dout, int64_t lddo,
+                          int64_t sdob, float* Dd, mms2ut_half* dq, int64_t lddq, int64_t sdqb,
+                          mms2ut_half* dk, int64_t lddk, int64_t sdkb, mms2ut_half* dv,
+                          int64_t lddv, int64_t sdvb, hipStream_t stream);
+
 /* ---------------------------------------------------------------- elementwise / embedding */
 /* y = dropout(x) elementwise (n elements, counter offset) ; y may alias x                   */
 int mms2ut_dropout_fwd(const mms2ut_half* x, mms2ut_half* y, int64_t n, float p, uint64_t seed,

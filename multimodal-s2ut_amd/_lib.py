@@ -35,6 +35,21 @@ class GemmArgs(C.Structure):
     ]
 
 
+class AttnArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("k", vp), ("v", vp), ("o", vp),
+        ("ldq", i64), ("ldk", i64), ("ldv", i64), ("ldo", i64),
+        ("sqb", i64), ("skb", i64), ("svb", i64), ("sob", i64),
+        ("B", i32), ("H", i32), ("Tq", i32), ("Tk", i32), ("hd", i32),
+        ("key_len", vp),
+        ("causal", i32),
+        ("scale", f32),
+        ("p", f32),
+        ("seed", u64), ("offset", u64),
+        ("lse", vp),
+    ]
+
+
 # name -> (restype, argtypes); every symbol include/mms2ut.h declares
 SIGNATURES = {
     "mms2ut_last_error": (C.c_char_p, []),
@@ -53,6 +68,9 @@ SIGNATURES = {
                                       f32, u64, u64, vp]),
     "mms2ut_attn_softmax_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i64, vp, i32, i32, f32, u64,
                                       u64, vp]),
+    "mms2ut_mha_varlen_fwd": (i32, [C.POINTER(AttnArgs), vp]),
+    "mms2ut_mha_varlen_bwd": (i32, [C.POINTER(AttnArgs), vp, i64, i64, vp, vp, i64, i64, vp, i64, i64,
+                                    vp, i64, i64, vp]),
     "mms2ut_dropout_fwd": (i32, [vp, vp, i64, f32, u64, u64, vp]),
     "mms2ut_dropout_mask": (i32, [vp, i64, f32, u64, u64, vp]),
     "mms2ut_encoder_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, u64, vp]),

@@ -1,0 +1,448 @@
+// Fused multi-head attention (flash-style, online softmax) for the encoder self-attention,
+// decoder causal self-attention and decoder cross-attention of mm_s2ut_transformer
+// (fairseq MultiheadAttention -> F.multi_head_attention_forward: softmax(q k^T * hd^-0.5 +
+// masks) -> dropout -> @ v).  Scores never touch HBM: per (batch, head) a workgroup of 4 waves
+// streams 64-key K/V blocks through LDS; each wave owns 16 query rows.
+//
+// MFMA orientation (v_mfma_f32_16x16x32_f16, D[row][col] with lane l owning col l&15 and rows
+// 4(l>>4)+r): the forward computes S^T[key][q] so lane l owns query l&15 and 4 keys per tile;
+// exp(S) is converted in registers and fed straight back as the B operand of O^T = V^T P^T,
+// with the key order of the two 16-key tiles of a 32-key step permuted identically on the V side
+// (two ds_read_b64_tr_b16 at key rows 4g.. and 16+4g..).  Row statistics are lane-local + two
+// xor-shuffles; the O rescale is lane-local.  Dropout on the probabilities uses the same counter
+// RNG as the unfused path: counter = offset + (z*Tq + q)*Tk + key.
+//
+// Backward: D = rowsum(dO*O) (prep kernel); dK/dV with keys stationary (kernel A), dQ with queries
+// stationary (kernel B); both recompute P from the saved log-sum-exp — no atomics, deterministic.
+#include "common.h"
+#include "../../include/mms2ut.h"
+
+namespace {
+
+constexpr int QB = 64, KB = 64;  // query rows / key rows per workgroup block
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct AttnP {
+  const h16* q; const h16* k; const h16* v; h16* o;
+  long ldq, ldk, ldv, ldo;          // row strides (elements)
+  long sqb, skb, svb, sob;          // batch strides (elements); head stride = hd
+  int H, Tq, Tk;
+  const int* key_len;               // [B] or null
+  int causal;
+  float scale;
+  float p; uint32_t thresh; uint64_t seed, offset;
+  float* lse;                       // [Z*Tq]
+  // backward
+  const h16* dout; long lddo, sdob;
+  const float* Dd;                  // [Z*Tq] rowsum(dO*O)
+  h16* dq; h16* dk; h16* dv;
+  long lddq, lddk, lddv, sdqb, sdkb, sdvb;
+};
+
+template <int HD>
+struct Tile {
+  static constexpr int LD = HD + 8;  // padded LDS row (halves): 16 rows of a ds_read_b128 hit distinct banks
+  static constexpr int CH = HD / 8;  // 16-B chunks per row
+};
+
+// cooperative global -> LDS copy of `rows` rows (zero beyond `valid`)
+template <int HD>
+MMS_DEV void load_rows(h16* lds, const h16* g, long ld, int row0, int valid, int rows) {
+  constexpr int CH = Tile<HD>::CH, LD = Tile<HD>::LD;
+  for (int i = threadIdx.x; i < rows * CH; i += blockDim.x) {
+    const int r = i / CH, c = i % CH;
+    s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (row0 + r < valid) v = *reinterpret_cast<const s16x8*>(g + (long)(row0 + r) * ld + c * 8);
+    *reinterpret_cast<s16x8*>(lds + r * LD + c * 8) = v;
+  }
+}
+
+// A/B fragment with rows along LDS rows: lane l -> X[row0 + (l&15)][k0 + 8(l>>4) .. +7]
+template <int HD>
+MMS_DEV h16x8 frag_rows(const h16* lds, int row0, int k0, int lane) {
+  const h16* p = lds + (row0 + (lane & 15)) * Tile<HD>::LD + k0 + 8 * (lane >> 4);
+  return __builtin_bit_cast(h16x8, *reinterpret_cast<const s16x8*>(p));
+}
+
+// transposed fragment over a 32-row step with the (4g.., 16+4g..) row permutation:
+// lane l (group g, i = l&15) -> X[row0 + 4g + j][col0 + i] (j<4), X[row0 + 16 + 4g + j-4][col0 + i]
+template <int HD>
+MMS_DEV h16x8 frag_tr(const h16* lds, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const h16* a1 = lds + (row0 + 4 * g + q) * Tile<HD>::LD + col0 + 4 * pp;
+  const h16* a2 = a1 + 16 * Tile<HD>::LD;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a2));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(h16x8, v);
+}
+
+MMS_DEV f32x4 mfma(h16x8 a, h16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+
+MMS_DEV h16x8 pack8(f32x4 a, f32x4 b) {
+  return h16x8{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3], (h16)b[0], (h16)b[1], (h16)b[2], (h16)b[3]};
+}
+
+MMS_DEV float xmax16_32(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+MMS_DEV float xsum16_32(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// ============================================================================ forward
+template <int HD>
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP P) {
+  constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
+  __shared__ __attribute__((aligned(16))) h16 sK[KB * LD];
+  __shared__ __attribute__((aligned(16))) h16 sV[KB * LD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int z = blockIdx.y, b = z / P.H, h = z % P.H;
+  const int qblk = blockIdx.x * QB;
+  const int q_own = qblk + w * 16 + (lane & 15);  // this lane's query row
+  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+  int kmax = klen;
+  if (P.causal) kmax = min(kmax, qblk + QB);
+  const h16* Q = P.q + b * P.sqb + h * HD;
+  const h16* K = P.k + b * P.skb + h * HD;
+  const h16* V = P.v + b * P.svb + h * HD;
+  // Q^T fragments (B operand): lane -> Q[q_own][kk*32 + 8g .. +7]
+  h16x8 qf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    s16x8 t = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (q_own < P.Tq) t = *reinterpret_cast<const s16x8*>(Q + (long)q_own * P.ldq + kk * 32 + 8 * g);
+    qf[kk] = __builtin_bit_cast(h16x8, t);
+  }
+  f32x4 o[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
+  for (int kb = 0; kb < kmax; kb += KB) {
+    __syncthreads();
+    load_rows<HD>(sK, K, P.ldk, kb, kmax, KB);
+    load_rows<HD>(sV, V, P.ldv, kb, kmax, KB);
+    __syncthreads();
+    // S^T for 4 tiles of 16 keys: lane -> S[q_own][kb + 16t + 4g + r]
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) s[t] = mfma(frag_rows<HD>(sK, 16 * t, kk * 32, lane), qf[kk], s[t]);
+    }
+    float bmax = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb + 16 * t + 4 * g + r;
+        const bool ok = key < kmax && (!P.causal || key <= q_own);
+        const float x = ok ? s[t][r] * P.scale : -INFINITY;
+        s[t][r] = x;
+        bmax = fmaxf(bmax, x);
+      }
+    bmax = xmax16_32(bmax);
+    const float mn = fmaxf(m, bmax);
+    const float alpha = (mn == -INFINITY) ? 1.f : __expf(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bool keep[4] = {true, true, true, true};
+      if (P.thresh) mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = (s[t][r] == -INFINITY) ? 0.f : __expf(s[t][r] - mn);
+        rs += e;
+        s[t][r] = keep[r] ? e * dscale : 0.f;
+      }
+    }
+    rs = xsum16_32(rs);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) o[i] *= alpha;
+    // O^T[d][q] += V^T[d][keys] P^T[keys][q], two 32-key steps
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const h16x8 pf = pack8(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) o[i] = mfma(frag_tr<HD>(sV, 32 * c, 16 * i, lane), pf, o[i]);
+    }
+  }
+  if (q_own < P.Tq) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    h16* O = P.o + b * P.sob + h * HD + (long)q_own * P.ldo;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i)
+      *reinterpret_cast<h16x4*>(O + 16 * i + 4 * g) =
+          h16x4{(h16)(o[i][0] * inv), (h16)(o[i][1] * inv), (h16)(o[i][2] * inv), (h16)(o[i][3] * inv)};
+    if (g == 0 && P.lse) P.lse[(long)z * P.Tq + q_own] = (l > 0.f) ? m + __logf(l) : -INFINITY;
+  }
+}
+
+// ============================================================================ backward prep
+template <int HD>
+__global__ void attn_bwd_prep_kernel(AttnP P, int Z) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)Z * P.Tq) return;
+  const int z = (int)(row / P.Tq), t = (int)(row % P.Tq);
+  const int b = z / P.H, h = z % P.H;
+  const h16* O = P.o + b * P.sob + h * HD + (long)t * P.ldo;
+  const h16* dO = P.dout + b * P.sdob + h * HD + (long)t * P.lddo;
+  float s = 0.f;
+  for (int d = lane * 2; d < HD; d += 128) {
+    s += (float)O[d] * (float)dO[d];
+    if (d + 1 < HD) s += (float)O[d + 1] * (float)dO[d + 1];
+  }
+  s = wave_sum(s);
+  if (lane == 0) const_cast<float*>(P.Dd)[row] = s;
+}
+
+// ============================================================================ backward: dK, dV
+template <int HD>
+__global__ void __launch_bounds__(256) attn_bwd_kv_kernel(AttnP P) {
+  constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
+  __shared__ __attribute__((aligned(16))) h16 sQ[QB * LD];
+  __shared__ __attribute__((aligned(16))) h16 sDO[QB * LD];
+  __shared__ float sL[QB], sD[QB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int z = blockIdx.y, b = z / P.H, h = z % P.H;
+  const int kblk = blockIdx.x * KB;
+  const int key_own = kblk + w * 16 + (lane & 15);
+  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+  const h16* Q = P.q + b * P.sqb + h * HD;
+  const h16* K = P.k + b * P.skb + h * HD;
+  const h16* V = P.v + b * P.svb + h * HD;
+  const h16* DO = P.dout + b * P.sdob + h * HD;
+  // K^T, V^T fragments of this wave's 16 keys (B operands): lane -> X[key_own][kk*32 + 8g ..]
+  h16x8 kf[NKK], vf[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    s16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
+    if (key_own < klen) {
+      a = *reinterpret_cast<const s16x8*>(K + (long)key_own * P.ldk + kk * 32 + 8 * g);
+      c = *reinterpret_cast<const s16x8*>(V + (long)key_own * P.ldv + kk * 32 + 8 * g);
+    }
+    kf[kk] = __builtin_bit_cast(h16x8, a);
+    vf[kk] = __builtin_bit_cast(h16x8, c);
+  }
+  f32x4 dk[NDT], dv[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) { dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[i] = dk[i]; }
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  const int q_begin = P.causal ? (kblk / QB) * QB : 0;
+  if (kblk < klen) {
+    for (int qb = q_begin; qb < P.Tq; qb += QB) {
+      __syncthreads();
+      load_rows<HD>(sQ, Q, P.ldq, qb, P.Tq, QB);
+      load_rows<HD>(sDO, DO, P.lddo, qb, P.Tq, QB);
+      for (int i = threadIdx.x; i < QB; i += blockDim.x) {
+        const bool ok = qb + i < P.Tq;
+        sL[i] = ok ? P.lse[(long)z * P.Tq + qb + i] : 0.f;
+        sD[i] = ok ? P.Dd[(long)z * P.Tq + qb + i] : 0.f;
+      }
+      __syncthreads();
+      // per 16-query tile: S[q][key], dP'[q][key]; lane -> (q = qb + 16t + 4g + r, key_own)
+      f32x4 pt[4], dst[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) {
+          s = mfma(frag_rows<HD>(sQ, 16 * t, kk * 32, lane), kf[kk], s);
+          dp = mfma(frag_rows<HD>(sDO, 16 * t, kk * 32, lane), vf[kk], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = 16 * t + 4 * g + r, q = qb + qi;
+          const bool ok = q < P.Tq && key_own < klen && (!P.causal || key_own <= q);
+          const float pr = ok ? __expf(s[r] * P.scale - sL[qi]) : 0.f;
+          float mk = dscale;
+          if (P.thresh && ok)
+            mk = mms_keep(P.seed, P.offset + ((uint64_t)z * P.Tq + q) * (uint64_t)P.Tk + key_own, P.thresh) ? dscale : 0.f;
+          pt[t][r] = pr * mk;                              // P' (dropped)
+          dst[t][r] = pr * (dp[r] * mk - sD[qi]);          // dS
+        }
+      }
+      // dV^T[d][key] += dO^T[d][q] P'[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const h16x8 pf = pack8(pt[2 * c], pt[2 * c + 1]);
+        const h16x8 sf = pack8(dst[2 * c], dst[2 * c + 1]);
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) {
+          dv[i] = mfma(frag_tr<HD>(sDO, 32 * c, 16 * i, lane), pf, dv[i]);
+          dk[i] = mfma(frag_tr<HD>(sQ, 32 * c, 16 * i, lane), sf, dk[i]);
+        }
+      }
+    }
+  }
+  if (key_own < P.Tk) {
+    h16* DK = P.dk + b * P.sdkb + h * HD + (long)key_own * P.lddk;
+    h16* DV = P.dv + b * P.sdvb + h * HD + (long)key_own * P.lddv;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) {
+      const f32x4 a = dk[i] * P.scale, c = dv[i];
+      *reinterpret_cast<h16x4*>(DK + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+      *reinterpret_cast<h16x4*>(DV + 16 * i + 4 * g) = h16x4{(h16)c[0], (h16)c[1], (h16)c[2], (h16)c[3]};
+    }
+  }
+}
+
+// ============================================================================ backward: dQ
+template <int HD>
+__global__ void __launch_bounds__(256) attn_bwd_q_kernel(AttnP P) {
+  constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
+  __shared__ __attribute__((aligned(16))) h16 sK[KB * LD];
+  __shared__ __attribute__((aligned(16))) h16 sV[KB * LD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int z = blockIdx.y, b = z / P.H, h = z % P.H;
+  const int qblk = blockIdx.x * QB;
+  const int q_own = qblk + w * 16 + (lane & 15);
+  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+  int kmax = klen;
+  if (P.causal) kmax = min(kmax, qblk + QB);
+  const h16* Q = P.q + b * P.sqb + h * HD;
+  const h16* K = P.k + b * P.skb + h * HD;
+  const h16* V = P.v + b * P.svb + h * HD;
+  const h16* DO = P.dout + b * P.sdob + h * HD;
+  const bool qok = q_own < P.Tq;
+  h16x8 qf[NKK], df[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    s16x8 a = {0, 0, 0, 0, 0, 0, 0, 0}, c = a;
+    if (qok) {
+      a = *reinterpret_cast<const s16x8*>(Q + (long)q_own * P.ldq + kk * 32 + 8 * g);
+      c = *reinterpret_cast<const s16x8*>(DO + (long)q_own * P.lddo + kk * 32 + 8 * g);
+    }
+    qf[kk] = __builtin_bit_cast(h16x8, a);
+    df[kk] = __builtin_bit_cast(h16x8, c);
+  }
+  const float L = qok ? P.lse[(long)z * P.Tq + q_own] : 0.f;
+  const float Dq = qok ? P.Dd[(long)z * P.Tq + q_own] : 0.f;
+  f32x4 dq[NDT];
+#pragma unroll
+  for (int i = 0; i < NDT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
+  for (int kb = 0; kb < kmax; kb += KB) {
+    __syncthreads();
+    load_rows<HD>(sK, K, P.ldk, kb, kmax, KB);
+    load_rows<HD>(sV, V, P.ldv, kb, kmax, KB);
+    __syncthreads();
+    f32x4 ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        s = mfma(frag_rows<HD>(sK, 16 * t, kk * 32, lane), qf[kk], s);
+        dp = mfma(frag_rows<HD>(sV, 16 * t, kk * 32, lane), df[kk], dp);
+      }
+      bool keep[4] = {true, true, true, true};
+      if (P.thresh) mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb + 16 * t + 4 * g + r;
+        const bool ok = qok && key < kmax && (!P.causal || key <= q_own);
+        const float pr = ok ? __expf(s[r] * P.scale - L) : 0.f;
+        const float mk = keep[r] ? dscale : 0.f;
+        ds[t][r] = pr * (dp[r] * mk - Dq);
+      }
+    }
+    // dQ^T[d][q] += K^T[d][keys] dS^T[keys][q]
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const h16x8 sf = pack8(ds[2 * c], ds[2 * c + 1]);
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) dq[i] = mfma(frag_tr<HD>(sK, 32 * c, 16 * i, lane), sf, dq[i]);
+    }
+  }
+  if (qok) {
+    h16* DQ = P.dq + b * P.sdqb + h * HD + (long)q_own * P.lddq;
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) {
+      const f32x4 a = dq[i] * P.scale;
+      *reinterpret_cast<h16x4*>(DQ + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+    }
+  }
+}
+
+template <typename F>
+int pick_hd(int hd, F&& f) {
+  switch (hd) {
+    case 64: return f(std::integral_constant<int, 64>{});
+    case 96: return f(std::integral_constant<int, 96>{});
+    case 128: return f(std::integral_constant<int, 128>{});
+    default: mms::set_error("flash attention: head_dim %d not supported (64/96/128)", hd); return 1;
+  }
+}
+
+int check_common(const mms2ut_attn_args* a) {
+  MMS_REQUIRE(a && a->q && a->k && a->v && a->o, "attention: null pointers");
+  MMS_REQUIRE(a->B > 0 && a->H > 0 && a->Tq > 0 && a->Tk > 0, "attention: bad sizes");
+  MMS_REQUIRE(a->ldq % 8 == 0 && a->ldk % 8 == 0 && a->ldv % 8 == 0 && a->ldo % 4 == 0,
+              "attention: row strides must be multiples of 8 (q/k/v) and 4 (o)");
+  MMS_REQUIRE(a->p < 1.f, "attention: dropout p must be < 1");
+  return 0;
+}
+
+AttnP make_params(const mms2ut_attn_args* a) {
+  AttnP P{};
+  P.q = a->q; P.k = a->k; P.v = a->v; P.o = a->o;
+  P.ldq = a->ldq; P.ldk = a->ldk; P.ldv = a->ldv; P.ldo = a->ldo;
+  P.sqb = a->sqb ? a->sqb : (long)a->Tq * a->ldq;
+  P.skb = a->skb ? a->skb : (long)a->Tk * a->ldk;
+  P.svb = a->svb ? a->svb : (long)a->Tk * a->ldv;
+  P.sob = a->sob ? a->sob : (long)a->Tq * a->ldo;
+  P.H = a->H; P.Tq = a->Tq; P.Tk = a->Tk;
+  P.key_len = a->key_len; P.causal = a->causal; P.scale = a->scale;
+  P.p = a->p; P.thresh = mms_drop_thresh(a->p); P.seed = a->seed; P.offset = a->offset;
+  P.lse = a->lse;
+  return P;
+}
+
+}  // namespace
+
+extern "C" int mms2ut_mha_varlen_fwd(const mms2ut_attn_args* a, hipStream_t s) {
+  if (check_common(a)) return 1;
+  MMS_REQUIRE(a->lse != nullptr, "attention fwd: lse buffer required");
+  AttnP P = make_params(a);
+  dim3 grid((a->Tq + QB - 1) / QB, a->B * a->H);
+  return pick_hd(a->hd, [&](auto HDc) {
+    hipLaunchKernelGGL((attn_fwd_kernel<decltype(HDc)::value>), grid, dim3(256), 0, s, P);
+    return mms::check_launch("mha_varlen_fwd");
+  });
+}
+
+extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_half* dout, int64_t lddo,
+                                     int64_t sdob, float* Dd, mms2ut_half* dq, int64_t lddq, int64_t sdqb,
+                                     mms2ut_half* dk, int64_t lddk, int64_t sdkb, mms2ut_half* dv,
+                                     int64_t lddv, int64_t sdvb, hipStream_t s) {
+  if (check_common(a)) return 1;
+  MMS_REQUIRE(a->lse && dout && Dd && dq && dk && dv, "attention bwd: null buffers");
+  MMS_REQUIRE(lddo % 8 == 0 && lddq % 4 == 0 && lddk % 4 == 0 && lddv % 4 == 0, "attention bwd: bad strides");
+  AttnP P = make_params(a);
+  P.dout = dout; P.lddo = lddo; P.sdob = sdob ? sdob : (long)a->Tq * lddo;
+  P.Dd = Dd;
+  P.dq = dq; P.lddq = lddq; P.sdqb = sdqb ? sdqb : (long)a->Tq * lddq;
+  P.dk = dk; P.lddk = lddk; P.sdkb = sdkb ? sdkb : (long)a->Tk * lddk;
+  P.dv = dv; P.lddv = lddv; P.sdvb = sdvb ? sdvb : (long)a->Tk * lddv;
+  const int Z = a->B * a->H;
+  return pick_hd(a->hd, [&](auto HDc) {
+    constexpr int HD = decltype(HDc)::value;
+    hipLaunchKernelGGL((attn_bwd_prep_kernel<HD>), dim3(((long)Z * a->Tq + 3) / 4), dim3(256), 0, s, P, Z);
+    if (int rc = mms::check_launch("mha_varlen_bwd_prep")) return rc;
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<HD>), dim3((a->Tk + KB - 1) / KB, Z), dim3(256), 0, s, P);
+    if (int rc = mms::check_launch("mha_varlen_bwd_kv")) return rc;
+    hipLaunchKernelGGL((attn_bwd_q_kernel<HD>), dim3((a->Tq + QB - 1) / QB, Z), dim3(256), 0, s, P);
+    return mms::check_launch("mha_varlen_bwd_q");
+  });
+}

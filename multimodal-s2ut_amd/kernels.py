@@ -247,6 +247,42 @@ def attn_softmax_bwd(P, dPd, Z, H, Tq, Tk, ldS, p=0.0, drop=None, out=None):
          None, 0, 0, float(p), seed, off, _s())
     return dS
 
+FLASH_HD = (64, 96, 128)
+
+
+def _attn_args(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len, causal, p, drop, lse,
+               sq=0, sk=0, sv=0, so=0):
+    from ._lib import AttnArgs
+    a = AttnArgs()
+    a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
+    a.ldq, a.ldk, a.ldv, a.ldo = int(ldq), int(ldk), int(ldv), int(ldo)
+    a.sqb, a.skb, a.svb, a.sob = int(sq), int(sk), int(sv), int(so)
+    a.B, a.H, a.Tq, a.Tk, a.hd = int(B), int(H), int(Tq), int(Tk), int(hd)
+    a.key_len = _p(key_len)
+    a.causal = int(causal)
+    a.scale = float(scale)
+    seed, off = drop if p > 0 else (0, 0)
+    a.p, a.seed, a.offset = float(p), int(seed), int(off)
+    a.lse = lse.data_ptr()
+    return a
+
+
+def mha_fwd(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len=None, causal=False,
+            p=0.0, drop=None):
+    """Fused attention forward; returns the row log-sum-exp [B*H*Tq] (fp32) for the backward."""
+    lse = torch.empty(B * H * Tq, dtype=torch.float32, device=q.device)
+    a = _attn_args(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len, causal, p, drop, lse)
+    call("mms2ut_mha_varlen_fwd", a, _s())
+    return lse
+
+
+def mha_bwd(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len, causal, p, drop, lse,
+            dout, lddo, dq, lddq, dk, lddk, dv, lddv):
+    a = _attn_args(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len, causal, p, drop, lse)
+    Dd = torch.empty(B * H * Tq, dtype=torch.float32, device=q.device)
+    call("mms2ut_mha_varlen_bwd", a, dout.data_ptr(), int(lddo), 0, Dd.data_ptr(), dq.data_ptr(),
+         int(lddq), 0, dk.data_ptr(), int(lddk), 0, dv.data_ptr(), int(lddv), 0, _s())
+
 # ============================================================================ elementwise
 
 

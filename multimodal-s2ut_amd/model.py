@@ -194,10 +194,50 @@ def sinusoidal_table(num, dim, padding_idx=1):
 # ============================================================================ attention core
 
 
+import os as _os
+
+# fused flash attention for the multi-head paths (head_dim 64/96/128, length-style padding);
+# MMS2UT_ATTN=unfused selects the materialised-scores path (A/B, and the reference check)
+FLASH = _os.environ.get("MMS2UT_ATTN", "flash") != "unfused"
+
+
+class AttnCtx:
+    """What an attention forward saves for its backward (flash: lse; unfused: P, Pd)."""
+    __slots__ = ("flash", "P", "Pd", "ldS", "lse", "key_len", "causal")
+
+
+def attn_forward(q, k, v, ldq, ldk, ldv, B, H, Tq, Tk, hd, scale, out, ldo, *, key_len=None,
+                 key_mask=None, causal=False, extra_key=False, p=0.0, drop=None):
+    ctx = AttnCtx()
+    ctx.key_len, ctx.causal = key_len, causal
+    ctx.flash = FLASH and key_mask is None and not extra_key and hd in K.FLASH_HD
+    if ctx.flash:
+        ctx.lse = K.mha_fwd(q, k, v, out, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len=key_len,
+                            causal=causal, p=p, drop=drop)
+        ctx.P = ctx.Pd = None
+        ctx.ldS = 0
+    else:
+        ctx.P, ctx.Pd, ctx.ldS = attn_fwd(q, k, v, ldq, ldk, ldv, B, H, Tq, Tk, hd, scale, out, ldo,
+                                          key_len=key_len, key_mask=key_mask, causal=causal,
+                                          extra_key=extra_key, p=p, drop=drop)
+        ctx.lse = None
+    return ctx
+
+
+def attn_backward(ctx, dO, ldo, o, q, k, v, ldq, ldk, ldv, B, H, Tq, Tk, hd, scale, dq, dk, dv,
+                  lddq, lddk, lddv, *, p=0.0, drop=None):
+    if ctx.flash:
+        K.mha_bwd(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, ctx.key_len, ctx.causal, p,
+                  drop, ctx.lse, dO, ldo, dq, lddq, dk, lddk, dv, lddv)
+    else:
+        attn_bwd(dO, ldo, q, k, v, ldq, ldk, ldv, ctx.P, ctx.Pd, ctx.ldS, B, H, Tq, Tk, hd, scale, dq, dk,
+                 dv, lddq, lddk, lddv, p=p, drop=drop)
+
+
 def attn_fwd(q, k, v, ldq, ldk, ldv, B, H, Tq, Tk, hd, scale, out, ldo, *, key_len=None,
              key_mask=None, causal=False, extra_key=False, p=0.0, drop=None,
              sq=None, sk=None, so=None):
-    """softmax(scale*q k^T + masks) -> dropout -> @ v, batched over (b, h).
+    """softmax(scale*q k^T + masks) -> dropout -> @ v, batched over (b, h), scores materialised.
     q/k/v/out are views whose row r=(b*T + t) and head column offset h*hd; `s*` = batch strides."""
     ldS = round_up(Tk, 8)
     sq = sq or Tq * ldq
@@ -382,9 +422,8 @@ class MMS2UTModel:
         O = torch.empty(R, d, dtype=F16, device=x.device)
         pa = self._p("attention_dropout")
         c["drop_attn"] = self._drop(pa, B * H * T * T)
-        c["P"], c["Pd"], c["ldS"] = attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H,
-                                             T, T, hd, hd ** -0.5, O, d, key_len=lens32, p=pa,
-                                             drop=c["drop_attn"])
+        c["attn"] = attn_forward(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, T, T, hd,
+                                 hd ** -0.5, O, d, key_len=lens32, p=pa, drop=c["drop_attn"])
         c["O"] = O
         pd = self._p("dropout")
         c["drop1"] = self._drop(pd, R * d)
@@ -431,9 +470,9 @@ class MMS2UTModel:
         dO = K.linear_dgrad(dyo, self.P(p + ".self_attn.out_proj.weight"))
         qkv = c["qkv"]
         dqkv = torch.empty_like(qkv)
-        attn_bwd(dO, d, qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, c["P"], c["Pd"], c["ldS"],
-                 B, H, T, T, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
-                 p=pa, drop=c["drop_attn"])
+        attn_backward(c["attn"], dO, d, c["O"], qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
+                      B, H, T, T, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
+                      p=pa, drop=c["drop_attn"])
         Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
         K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
         K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
@@ -594,7 +633,7 @@ class MMS2UTModel:
         return dtext_total
 
     # -------------------------------------------------------------- decoder layer
-    def dec_layer_fwd(self, l, x, enc, B, Tt, Te, tgt_mask, enc_len32):
+    def dec_layer_fwd(self, l, x, enc, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None):
         cfg = self.cfg
         p = f"decoder.layers.{l}"
         d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
@@ -611,9 +650,11 @@ class MMS2UTModel:
         c["qkv"] = qkv
         O = torch.empty(R, d, dtype=F16, device=x.device)
         c["drop_sa"] = self._drop(pa, B * H * Tt * Tt)
-        c["sP"], c["sPd"], c["sldS"] = attn_fwd(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Tt, Tt,
-                                                hd, hd ** -0.5, O, d, key_mask=tgt_mask, causal=True, p=pa,
-                                                drop=c["drop_sa"])
+        # right-padded targets: padding == key length (flash path); otherwise the explicit mask
+        tgt_len, tmask = (tgt_len32, None) if tgt_len32 is not None else (None, tgt_mask)
+        c["sattn"] = attn_forward(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Tt, Tt, hd,
+                                  hd ** -0.5, O, d, key_len=tgt_len, key_mask=tmask, causal=True, p=pa,
+                                  drop=c["drop_sa"])
         c["sO"] = O
         c["drop1"] = self._drop(pd, R * d)
         x2 = K.linear(O, self.P(p + ".self_attn.out_proj.weight"), self.P(p + ".self_attn.out_proj.bias"),
@@ -630,8 +671,8 @@ class MMS2UTModel:
         c["q"], c["kv"] = q, kv
         O2 = torch.empty(R, d, dtype=F16, device=x.device)
         c["drop_ca"] = self._drop(pa, B * H * Tt * Te)
-        c["cP"], c["cPd"], c["cldS"] = attn_fwd(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tt, Te, hd, hd ** -0.5,
-                                                O2, d, key_len=enc_len32, p=pa, drop=c["drop_ca"])
+        c["cattn"] = attn_forward(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tt, Te, hd, hd ** -0.5, O2, d,
+                                  key_len=enc_len32, p=pa, drop=c["drop_ca"])
         c["cO"] = O2
         c["drop2"] = self._drop(pd, R * d)
         x3 = K.linear(O2, self.P(p + ".encoder_attn.out_proj.weight"), self.P(p + ".encoder_attn.out_proj.bias"),
@@ -676,8 +717,8 @@ class MMS2UTModel:
         q, kv = c["q"], c["kv"]
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
-        attn_bwd(dO2, d, q, kv, kv[:, d:], d, 2 * d, 2 * d, c["cP"], c["cPd"], c["cldS"], B, H, Tt, Te, hd,
-                 hd ** -0.5, dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pa, drop=c["drop_ca"])
+        attn_backward(c["cattn"], dO2, d, c["cO"], q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tt, Te, hd,
+                      hd ** -0.5, dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pa, drop=c["drop_ca"])
         de = cfg["encoder_embed_dim"]
         Wkv = self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight").view(2 * d, de)
         K.linear_wgrad(dkv, enc, self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight", grad=True).view(2 * d, de))
@@ -696,9 +737,9 @@ class MMS2UTModel:
         dO = K.linear_dgrad(dy1, self.P(p + ".self_attn.out_proj.weight"))
         qkv = c["qkv"]
         dqkv = torch.empty_like(qkv)
-        attn_bwd(dO, d, qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, c["sP"], c["sPd"], c["sldS"], B, H,
-                 Tt, Tt, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pa,
-                 drop=c["drop_sa"])
+        attn_backward(c["sattn"], dO, d, c["sO"], qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H,
+                      Tt, Tt, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pa,
+                      drop=c["drop_sa"])
         Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
         K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
         K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
@@ -788,7 +829,7 @@ class MMS2UTModel:
         tgt_mask = batch.tgt_mask  # uint8 [B, round8(Tt)] or None (no target padding in the batch)
         ctx["layers"] = []
         for l in range(cfg["decoder_layers"]):
-            x, c = self.dec_layer_fwd(l, x, enc, B, Tt, Te, tgt_mask, enc_len32)
+            x, c = self.dec_layer_fwd(l, x, enc, B, Tt, Te, tgt_mask, enc_len32, batch.tgt_len32)
             ctx["layers"].append(c)
         xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("decoder.layer_norm.weight"), self.P("decoder.layer_norm.bias"))
         ctx["lx"], ctx["xl"] = x, xl

@@ -23,6 +23,7 @@ class DeviceBatch:
     Te: int
     prev: torch.Tensor                # [B, Tt] int64 (device)
     tgt_mask: Optional[torch.Tensor]  # [B, round8(Tt)] uint8 or None
+    tgt_len32: Optional[torch.Tensor]  # [B] int32 non-pad target lengths when right-padded, else None
     target: torch.Tensor              # [B, Tt] int64 (device)
     imgs: Optional[torch.Tensor]      # [B, Ti, Di] fp16 or None
     img_keymask: Optional[torch.Tensor]  # [B, round8(Ti+1)] uint8 or None
@@ -62,6 +63,10 @@ def prepare_batch(sample, cfg, device="cuda", src_override=None):
         tm = torch.zeros(B, round_up(Tt, 8), dtype=torch.uint8)
         tm[:, :Tt] = padm.to(torch.uint8)
         tgt_mask = tm.to(dev, non_blocking=True)
+    # fairseq collate_tokens(left_pad=False): padding is a suffix -> it is a key length
+    nonpad = (~padm).sum(1)
+    right_padded = bool(torch.all(padm == (torch.arange(Tt)[None, :] >= nonpad[:, None])))
+    tgt_len32 = nonpad.to(torch.int32).to(dev, non_blocking=True) if right_padded else None
     imgs = img_keymask = None
     imgs_list = ni.get("imgs_list") or []
     if cfg["fusion"] and len(imgs_list) > 0:
@@ -77,7 +82,7 @@ def prepare_batch(sample, cfg, device="cuda", src_override=None):
     return DeviceBatch(
         src=src.contiguous(), src_lengths=torch.as_tensor(lens), Te=Te,
         enc_len32=torch.from_numpy(enc_len).to(dev, non_blocking=True),
-        prev=prev_cpu.to(dev, non_blocking=True).contiguous(), tgt_mask=tgt_mask,
+        prev=prev_cpu.to(dev, non_blocking=True).contiguous(), tgt_mask=tgt_mask, tgt_len32=tgt_len32,
         target=sample["target"].to(dev, non_blocking=True).contiguous(), imgs=imgs,
         img_keymask=img_keymask, ntokens=int(sample["ntokens"]),
         nsentences=int(sample.get("nsentences", B)), n_src_frames=int(lens.sum()))

@@ -182,6 +182,59 @@ def test_attn_softmax_dropout_replay(K):
     assert rel(dS.view(Z, Tq, ldS)[..., :Tk], dS_ref) < 3e-3
 
 
+def _attn_ref(q, k, v, lens, causal, scale, mask=None):
+    s = scale * q @ k.transpose(-1, -2)
+    Tq, Tk = s.shape[-2], s.shape[-1]
+    j = torch.arange(Tk, device=s.device)
+    bad = j[None, None, None, :] >= lens.long()[:, None, None, None]
+    if causal:
+        bad = bad | (j[None, None, None, :] > torch.arange(Tq, device=s.device)[None, None, :, None])
+    p = torch.softmax(s.masked_fill(bad, float("-inf")), -1)
+    if mask is not None:
+        p = p * mask
+    return p @ v
+
+
+@pytest.mark.parametrize("hd", [64, 96])
+@pytest.mark.parametrize("causal,Tq,Tk,lens,p", [
+    (False, 70, 90, [90, 50, 7], 0.0), (True, 70, 70, [70, 41, 3], 0.0),
+    (False, 130, 130, [130, 129, 65], 0.0), (True, 150, 150, [150, 100, 1], 0.25),
+    (False, 33, 200, [200, 64, 63], 0.1)])
+def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p):
+    B, H = 3, 2
+    d = H * hd
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q = torch.randn(B * Tq, d, generator=g, device="cuda").half()
+    kv = torch.randn(B * Tk, 2 * d, generator=g, device="cuda").half()
+    lens_t = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    o = torch.empty(B * Tq, d, dtype=torch.float16, device="cuda")
+    seed, off = 77, 1024
+    lse = K.mha_fwd(q, kv, kv[:, d:], o, d, 2 * d, 2 * d, d, B, H, Tq, Tk, hd, hd ** -0.5, key_len=lens_t,
+                    causal=causal, p=p, drop=(seed, off))
+    qf = q.float().view(B, Tq, H, hd).transpose(1, 2).requires_grad_(True)
+    kf = kv[:, :d].float().view(B, Tk, H, hd).transpose(1, 2).requires_grad_(True)
+    vf = kv[:, d:].float().view(B, Tk, H, hd).transpose(1, 2).requires_grad_(True)
+    mask = None
+    if p > 0:
+        mask = K.dropout_mask(B * H * Tq * Tk, p, seed, off, "cuda").view(B, H, Tq, Tk).float() / (1 - p)
+    ref = _attn_ref(qf, kf, vf, lens_t, causal, hd ** -0.5, mask)
+    got = o.float().view(B, Tq, H, hd).transpose(1, 2)
+    torch.cuda.synchronize()
+    assert rel(got, ref) < 3e-3
+    do = torch.randn(B * Tq, d, generator=g, device="cuda").half()
+    ref.backward(do.float().view(B, Tq, H, hd).transpose(1, 2))
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    K.mha_bwd(q, kv, kv[:, d:], o, d, 2 * d, 2 * d, d, B, H, Tq, Tk, hd, hd ** -0.5, lens_t, causal, p,
+              (seed, off), lse, do, d, dq, d, dkv, 2 * d, dkv[:, d:], 2 * d)
+    torch.cuda.synchronize()
+    t = lambda x, T: x.float().view(B, T, H, hd).transpose(1, 2)
+    assert rel(t(dq, Tq), qf.grad) < 5e-3
+    # keys beyond the length get exactly zero gradient (as the reference's masked softmax)
+    assert rel(t(dkv[:, :d], Tk), kf.grad) < 5e-3
+    assert rel(t(dkv[:, d:], Tk), vf.grad) < 5e-3
+
+
 def test_ls_xent(K):
     rows, V, eps, pad = 333, 1004, 0.2, 1
     Vp = 1008
