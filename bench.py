@@ -33,13 +33,15 @@ runtime = import_module("multimodal-s2ut_amd.runtime")
 kernels = import_module("multimodal-s2ut_amd.kernels")
 parallel = import_module("multimodal-s2ut_amd.parallel")
 trainer_mod = import_module("multimodal-s2ut_amd.trainer")
+model_mod = import_module("multimodal-s2ut_amd.model")
 
 MFMA_PEAK_F16 = 2500.0   # TFLOP/s dense fp16 (MI355X_MICROARCH.md chip parameters)
 HBM_PEAK = 8000.0        # GB/s spec
 
 
-def fwd_flops_per_utt(Ts, Tt, cfg, Ti=577, Di=768, fusion=True):
-    """SURVEY.md §8(d) closed form (true lengths), forward FLOPs of one utterance."""
+def fwd_flops_per_utt(Ts, Tt, cfg, Ti=577, Di=768, fusion=True, split=False):
+    """SURVEY.md §8(d) closed form (true lengths), forward FLOPs of one utterance.
+    split=True -> (total, multi-head attention score/PV FLOPs run by the fused attention kernel)."""
     d, F, C, V = cfg["encoder_embed_dim"], cfg["encoder_ffn_embed_dim"], cfg["conv_channels"], cfg["vocab_size"]
     T1 = (Ts - 1) // 2 + 1
     Te = (T1 - 1) // 2 + 1
@@ -50,7 +52,8 @@ def fwd_flops_per_utt(Ts, Tt, cfg, Ti=577, Di=768, fusion=True):
         f += Te * 8 * d * d + 4 * Ti * Di * d + 4 * Te * (Ti + k) * d
     f += cfg["decoder_layers"] * (Tt * (12 * d * d + 4 * d * F) + 4 * Tt * Tt * d + 4 * Te * d * d + 4 * Tt * Te * d)
     f += 2 * Tt * d * V
-    return f
+    mha = cfg["encoder_layers"] * 4 * Te * Te * d + cfg["decoder_layers"] * (4 * Tt * Tt * d + 4 * Tt * Te * d)
+    return (f, mha) if split else f
 
 
 def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000):
@@ -79,8 +82,13 @@ def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000):
         batch = runtime.prepare_batch(sample, cfg, device, src_override=src_dummy)
         tl = sample["target_lengths"].numpy()
         sl = sample["net_input"]["src_lengths"].numpy()
-        flops = sum(fwd_flops_per_utt(int(s), int(t), cfg, fusion=cfg["fusion"]) for s, t in zip(sl, tl))
-        out.append((wb, batch, sample, 3 * flops))
+        parts = [fwd_flops_per_utt(int(s), int(t), cfg, fusion=cfg["fusion"], split=True) for s, t in zip(sl, tl)]
+        flops = sum(p[0] for p in parts)
+        mha = sum(p[1] for p in parts)
+        # GEMM-kernel share of the algorithmic FLOPs: everything but the multi-head attention
+        # products, which the fused attention kernel executes (the fusion attention stays on GEMMs)
+        gemm_flops = flops - (mha if model_mod.FLASH else 0)
+        out.append((wb, batch, sample, 3 * flops, 3 * gemm_flops))
     return out
 
 
@@ -175,8 +183,10 @@ def main():
     gemm_ms, n_launch, launched_flops = kernels.gemm_profile_end() if not args.no_gemm_timing else (0.0, 0, 0.0)
     elapsed = t1 - t0
     frames = sum(int(batches[(args.warmup + i) % len(batches)][1].n_src_frames) for i in range(args.steps))
-    alg_flops = sum(batches[(args.warmup + i) % len(batches)][3] for i in range(args.steps))
-    stats = torch.tensor([elapsed, frames, alg_flops, gemm_ms, n_launch], dtype=torch.float64, device=device)
+    alg_flops = sum(batches[(args.warmup + i) % len(batches)][4] for i in range(args.steps))
+    total_flops = sum(batches[(args.warmup + i) % len(batches)][3] for i in range(args.steps))
+    stats = torch.tensor([elapsed, frames, alg_flops, gemm_ms, n_launch, total_flops], dtype=torch.float64,
+                         device=device)
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -184,9 +194,10 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed = float(mx[0])
         frames_all = float(sm[1])
-        flops_all, gemm_all, nl_all = float(sm[2]), float(sm[3]), float(sm[4])
+        flops_all, gemm_all, nl_all, total_flops_all = float(sm[2]), float(sm[3]), float(sm[4]), float(sm[5])
     else:
         frames_all, flops_all, gemm_all, nl_all = float(frames), float(alg_flops), gemm_ms, float(n_launch)
+        total_flops_all = float(total_flops)
     ost = tr.opt.stats()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -206,7 +217,8 @@ def main():
                        "model": "mm_s2ut_transformer", "max_tokens": args.max_tokens,
                        "global_batch_frames_per_step": frames_all / args.steps,
                        "parallelism": f"dp{world}", "front_end": "GPU fbank+CMVN in step",
-                       "alg_flops_per_frame": flops_all / max(frames_all, 1)},
+                       "alg_flops_per_frame": total_flops_all / max(frames_all, 1),
+                       "model_tflops_per_s": total_flops_all / elapsed / 1e12},
             "roofline": {"bound": "mfma", "kernel": "mms2ut gemm_kernel (all GEMM launches)",
                          "achieved": achieved, "peak": MFMA_PEAK_F16, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_PEAK_F16) if achieved else None, "traffic": None,

@@ -10,7 +10,16 @@ Plugin names (same as the reference): task ``multimodal_speech_to_speech``, mode
 ``mm_s2ut_transformer``, criterion ``speech_to_unit`` (aliases ``speech_to_speech``,
 ``speech_to_unit_v2``).
 """
-from . import _lib, data, frontend, kernels, model, optim, parallel, runtime, trainer  # noqa: F401
+from . import _lib, data, frontend, kernels, model, optim, parallel, plugins, runtime, trainer  # noqa: F401
 from .model import MMS2UTModel, default_cfg, param_specs  # noqa: F401
+from .plugins import REGISTRY  # noqa: F401
+
+try:  # fairseq --user-dir: register the same names into fairseq's registries
+    import fairseq as _fairseq
+except ImportError:
+    _fairseq = None
+if _fairseq is not None:
+    from . import fairseq_adapter
+    fairseq_adapter.register(_fairseq)
 
 __version__ = "0.1.0"

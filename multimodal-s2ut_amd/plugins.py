@@ -1,0 +1,334 @@
+"""fairseq-compatible plugin surface of the reference, backed by the HIP model.
+
+Names, flags and config keys are the reference's:
+  task       multimodal_speech_to_speech   mm_s2ut/tasks/speech_to_speech.py:45-123
+  model/arch mm_s2ut_transformer           mm_s2ut/models/mm_s2s_transformer.py:625-710
+  criterion  speech_to_unit (+ speech_to_speech [README.md:151], speech_to_unit_v2
+             [criterions/speech_to_speech_criterion.py:33-35])
+  fusion YAML keys                         mm_s2ut/config/multimodal_s2ut_transformer.yaml:1-41
+
+fairseq itself is not importable in this image; the classes register into a local registry with
+the same names (``REGISTRY``).  ``fairseq_adapter.py`` re-registers them into fairseq's own
+registries when fairseq is importable, so ``fairseq-train --user-dir multimodal-s2ut_amd`` resolves
+the same names.
+"""
+import argparse
+import os
+import random
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+
+from . import runtime
+from .model import MMS2UTModel, default_cfg
+
+REGISTRY = {"task": {}, "model": {}, "arch": {}, "criterion": {}}
+
+
+def _register(kind, *names):
+    def deco(obj):
+        for n in names:
+            REGISTRY[kind][n] = obj
+        return obj
+    return deco
+
+
+register_task = lambda *n: _register("task", *n)          # noqa: E731
+register_model = lambda *n: _register("model", *n)        # noqa: E731
+register_criterion = lambda *n: _register("criterion", *n)  # noqa: E731
+register_arch = lambda *n: _register("arch", *n)          # noqa: E731
+
+
+def set_seed(seed=42):
+    """tasks/speech_to_speech.py:33-42 (global seeding at task construction)."""
+    os.environ["PYTHONHASHSEED"] = str(seed)
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+
+
+FUSION_KEYS = ("SA_image_dropout", "SA_text_dropout", "SA_attention_dropout", "image_pre_norm",
+               "is_fusion_top", "image_feat_path", "image_feat_dim", "flickr30k_root",
+               "load_visual_extractor_type", "load_visual_extractor", "modality_dropout",
+               "audio_dropout", "multimodal_attention_type", "use_selective_gate", "is_merge_text_img")
+
+
+def load_fusion_yaml(path):
+    """The fusion YAML (OmegaConf.load in the reference; yaml.safe_load here — same keys)."""
+    import yaml
+    with open(path) as f:
+        y = yaml.safe_load(f) or {}
+    return SimpleNamespace(**{k: y.get(k) for k in set(FUSION_KEYS) | set(y)})
+
+# ------------------------------------------------------------------------------------ arch
+
+
+def s2ut_architecture_base(args):
+    """fairseq s2ut_architecture_base defaults (getattr-with-default; an unset flag is None)."""
+    def g(k, v):
+        if getattr(args, k, None) is None:
+            setattr(args, k, v)
+    g("conv_kernel_sizes", "5,5")
+    g("conv_channels", 1024)
+    g("encoder_embed_dim", 512)
+    g("encoder_ffn_embed_dim", 2048)
+    g("encoder_layers", 12)
+    g("encoder_attention_heads", 8)
+    g("encoder_normalize_before", True)
+    g("decoder_embed_dim", args.encoder_embed_dim)
+    g("decoder_ffn_embed_dim", args.encoder_ffn_embed_dim)
+    g("decoder_layers", 6)
+    g("decoder_attention_heads", 8)
+    g("decoder_normalize_before", True)
+    g("decoder_learned_pos", False)
+    g("dropout", 0.1)
+    g("attention_dropout", args.dropout)
+    g("activation_dropout", args.dropout)
+    g("activation_fn", "relu")
+    g("share_decoder_input_output_embed", False)
+    g("no_scale_embedding", False)
+    g("decoder_layerdrop", 0.0)
+    g("max_source_positions", 6000)
+    g("max_target_positions", 1024)
+    g("n_frames_per_step", 1)
+    g("input_feat_per_channel", 80)
+    g("input_channels", 1)
+
+
+@register_arch("mm_s2ut_transformer")
+def mm_s2ut_architecture_base(args):
+    """mm_s2s_transformer.py:703-707."""
+    s2ut_architecture_base(args)
+
+
+def cfg_from_args(args, fusion_cfg=None, vocab_size=1004):
+    """fairseq args Namespace (+ fusion YAML) -> model config dict."""
+    mm_s2ut_architecture_base(args)
+    unsupported = []
+    if not args.share_decoder_input_output_embed:
+        unsupported.append("--share-decoder-input-output-embed is required (tied output projection)")
+    if args.activation_fn != "relu":
+        unsupported.append("activation_fn must be relu")
+    if not (args.encoder_normalize_before and args.decoder_normalize_before):
+        unsupported.append("pre-LN (normalize_before) only")
+    if args.n_frames_per_step != 1:
+        unsupported.append("n_frames_per_step must be 1 (unit targets)")
+    if getattr(args, "decoder_learned_pos", False):
+        unsupported.append("sinusoidal decoder positions only")
+    if unsupported:
+        raise NotImplementedError("; ".join(unsupported))
+    cfg = default_cfg(
+        input_feat_per_channel=args.input_feat_per_channel, input_channels=args.input_channels,
+        conv_kernel_sizes=tuple(int(k) for k in str(args.conv_kernel_sizes).split(",")),
+        conv_channels=args.conv_channels, encoder_embed_dim=args.encoder_embed_dim,
+        encoder_ffn_embed_dim=args.encoder_ffn_embed_dim, encoder_layers=args.encoder_layers,
+        encoder_attention_heads=args.encoder_attention_heads, decoder_embed_dim=args.decoder_embed_dim,
+        decoder_ffn_embed_dim=args.decoder_ffn_embed_dim, decoder_layers=args.decoder_layers,
+        decoder_attention_heads=args.decoder_attention_heads, dropout=args.dropout,
+        attention_dropout=args.attention_dropout, activation_dropout=args.activation_dropout,
+        vocab_size=vocab_size, max_source_positions=args.max_source_positions,
+        max_target_positions=args.max_target_positions, no_scale_embedding=args.no_scale_embedding,
+        label_smoothing=getattr(args, "label_smoothing", 0.2), fusion=False)
+    if fusion_cfg is not None:
+        dims = fusion_cfg.image_feat_dim
+        dims = list(dims) if isinstance(dims, (list, tuple)) else [dims]
+        if len(dims) != 1:
+            raise NotImplementedError("one image-feature type (SURVEY Q8)")
+        att = fusion_cfg.multimodal_attention_type
+        if att not in ("selective_attention", "multimodal_attention"):
+            raise NotImplementedError(f"multimodal_attention_type={att!r} (out of scope: SURVEY §2)")
+        if getattr(fusion_cfg, "is_merge_text_img", False):
+            raise NotImplementedError("is_merge_text_img=True")
+        cfg.update(fusion=bool(fusion_cfg.is_fusion_top), multimodal_attention_type=att,
+                   use_selective_gate=bool(fusion_cfg.use_selective_gate), image_feat_dim=int(dims[0]),
+                   image_pre_norm=bool(fusion_cfg.image_pre_norm),
+                   SA_image_dropout=float(fusion_cfg.SA_image_dropout),
+                   SA_text_dropout=float(fusion_cfg.SA_text_dropout),
+                   SA_attention_dropout=float(fusion_cfg.SA_attention_dropout),
+                   modality_dropout=float(fusion_cfg.modality_dropout),
+                   audio_dropout=float(fusion_cfg.audio_dropout))
+    return cfg
+
+# ------------------------------------------------------------------------------------ task
+
+
+@register_task("multimodal_speech_to_speech")
+class MultiModalSpeechToSpeechTask:
+    """tasks/speech_to_speech.py:45-123 (flags, seeding, fusion/noise YAML loading)."""
+
+    @staticmethod
+    def add_args(parser):
+        # inherited SpeechToSpeechTask flags used by the canonical command
+        parser.add_argument("data", nargs="?", default=None)
+        parser.add_argument("--config-yaml", default="config.yaml")
+        parser.add_argument("--multitask-config-yaml", default=None)
+        parser.add_argument("--target-is-code", action="store_true")
+        parser.add_argument("--target-code-size", type=int, default=None)
+        parser.add_argument("--n-frames-per-step", type=int, default=1)
+        # the reference's own flags (speech_to_speech.py:47-81)
+        parser.add_argument("--multimodal-translation-config-yaml", type=str, default=None)
+        parser.add_argument("--mhubert-ckpt-path", type=str, default=None)
+        parser.add_argument("--wav2vec2-model-dir", type=str, default=None)
+        parser.add_argument("--freezing-updates", type=int, default=-1)
+        parser.add_argument("--noise-config-yaml", type=str, default=None)
+
+    def __init__(self, args):
+        self.args = args
+        set_seed(getattr(args, "seed", 1))
+        self.multimodal_translation_config = None
+        if getattr(args, "multimodal_translation_config_yaml", None):
+            self.multimodal_translation_config = load_fusion_yaml(args.multimodal_translation_config_yaml)
+        if getattr(args, "mhubert_ckpt_path", None) or getattr(args, "wav2vec2_model_dir", None):
+            raise NotImplementedError("pretrained speech encoders are out of scope (SURVEY §2)")
+        code_size = getattr(args, "target_code_size", None) or 1000
+        self.vocab_size = code_size + 4  # <s> <pad> </s> <unk> + units (fairseq Dictionary)
+        self.padding_idx, self.eos = 1, 2
+
+    @classmethod
+    def setup_task(cls, args, **kw):
+        return cls(args)
+
+    def build_model(self, args, device="cuda"):
+        return MM_S2UTTransformerModel.build_model(args, self, device=device)
+
+    def build_criterion(self, args):
+        return SpeechToUnitCriterion(self, getattr(args, "label_smoothing", 0.2))
+
+# ------------------------------------------------------------------------------------ model
+
+
+@register_model("mm_s2ut_transformer")
+class MM_S2UTTransformerModel:
+    """mm_s2s_transformer.py:625-700 over the HIP model (module tree / state-dict keys kept)."""
+
+    def __init__(self, cfg, device="cuda", seed=1):
+        self.net = MMS2UTModel(cfg, device=device, seed=seed).init_params(seed)
+        self.cfg = self.net.cfg
+
+    @classmethod
+    def build_model(cls, args, task, device="cuda"):
+        cfg = cfg_from_args(args, task.multimodal_translation_config, task.vocab_size)
+        return cls(cfg, device=device, seed=getattr(args, "seed", 1))
+
+    def train(self, mode=True):
+        self.net.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def state_dict(self):
+        return self.net.params.state_dict()
+
+    def load_state_dict(self, sd, strict=True):
+        sd = {k: v for k, v in sd.items() if k != "decoder.output_projection.weight"}
+        return self.net.params.load_state_dict(sd, strict=strict)
+
+    def forward(self, src_tokens, src_lengths, prev_output_tokens, src_audio_path=None, img_path=None,
+                img_tensor=None, imgs_list=(), img_masks_list=(), tgt_speaker=None,
+                return_all_hiddens=False, target=None, **kwargs):
+        """Reference signature (mm_s2s_transformer.py:667-680) -> (logits [B, Tt, V], extra).
+        The logits are autograd-connected to the hand-written backward."""
+        if tgt_speaker is not None:
+            raise NotImplementedError("target speaker embeddings (spk_emb_proj) are out of scope")
+        sample = {"net_input": {"src_tokens": src_tokens, "src_lengths": src_lengths,
+                                "prev_output_tokens": prev_output_tokens, "imgs_list": list(imgs_list),
+                                "img_masks_list": list(img_masks_list)},
+                  "target": target if target is not None else prev_output_tokens,
+                  "ntokens": int(prev_output_tokens.ne(self.cfg["padding_idx"]).sum())}
+        batch = runtime.prepare_batch(sample, self.cfg, self.net.device)
+        logits = runtime.model_logits(self.net, batch)
+        B, Tt = prev_output_tokens.shape
+        V = self.cfg["vocab_size"]
+        out = logits.view(B, Tt, -1)[:, :, :V]
+        extra = {"attn": [None], "inner_states": None, "_batch": batch, "_logits_padded": logits}
+        return out, extra
+
+    __call__ = forward
+
+# ------------------------------------------------------------------------------------ criterion
+
+
+@register_criterion("speech_to_unit", "speech_to_speech", "speech_to_unit_v2")
+class SpeechToUnitCriterion:
+    """fairseq speech_to_unit (ref copy criterions/speech_to_speech_criterion.py:58-102):
+    label-smoothed NLL (eps), reduce=sum, sample_size = ntokens (sentence_avg False)."""
+
+    def __init__(self, task, label_smoothing=0.2, sentence_avg=False):
+        self.eps = label_smoothing
+        self.sentence_avg = sentence_avg
+        self.padding_idx = getattr(task, "padding_idx", 1)
+
+    def __call__(self, model, sample, reduce=True):
+        return self.forward(model, sample, reduce)
+
+    def forward(self, model, sample, reduce=True):
+        ni = dict(sample["net_input"])
+        _, extra = model(**ni, target=sample["target"])
+        batch, logits = extra["_batch"], extra["_logits_padded"]
+        loss, nll = runtime.label_smoothed_ce(logits, batch.target, model.cfg["vocab_size"], self.eps,
+                                              self.padding_idx)
+        sample_size = sample["target"].size(0) if self.sentence_avg else sample["ntokens"]
+        logging_output = {"loss": loss.detach(), "nll_loss": nll.detach(), "ntokens": sample["ntokens"],
+                          "nsentences": sample["target"].size(0), "sample_size": sample_size}
+        return loss, sample_size, logging_output
+
+    @staticmethod
+    def logging_outputs_can_be_summed():
+        # fixed scalars: summed with one all-reduce (parallel.all_reduce_scalars), unlike the
+        # reference's all_gather_list
+        return True
+
+
+def build_parser():
+    """Flag subset of the canonical command (scripts/textless/1_train.sh:105-125)."""
+    p = argparse.ArgumentParser("mms2ut-train")
+    MultiModalSpeechToSpeechTask.add_args(p)
+    p.add_argument("--task", default="multimodal_speech_to_speech")
+    p.add_argument("--arch", default="mm_s2ut_transformer")
+    p.add_argument("--criterion", default="speech_to_unit")
+    p.add_argument("--label-smoothing", type=float, default=0.2)
+    p.add_argument("--share-decoder-input-output-embed", action="store_true")
+    p.add_argument("--dropout", type=float, default=0.1)
+    p.add_argument("--attention-dropout", type=float, default=0.1)
+    p.add_argument("--relu-dropout", dest="activation_dropout", type=float, default=0.1)
+    p.add_argument("--activation-dropout", dest="activation_dropout", type=float)
+    # architecture flags: None = the arch default (s2ut_architecture_base)
+    for f, t in (("--conv-kernel-sizes", str), ("--conv-channels", int), ("--encoder-embed-dim", int),
+                 ("--encoder-ffn-embed-dim", int), ("--encoder-layers", int),
+                 ("--encoder-attention-heads", int), ("--decoder-embed-dim", int),
+                 ("--decoder-ffn-embed-dim", int), ("--decoder-layers", int),
+                 ("--decoder-attention-heads", int)):
+        p.add_argument(f, type=t, default=None)
+    p.add_argument("--lr", type=float, default=5e-4)
+    p.add_argument("--lr-scheduler", default="inverse_sqrt")
+    p.add_argument("--warmup-init-lr", type=float, default=1e-7)
+    p.add_argument("--warmup-updates", type=int, default=10000)
+    p.add_argument("--optimizer", default="adam")
+    p.add_argument("--adam-betas", default="(0.9,0.98)")
+    p.add_argument("--clip-norm", type=float, default=10.0)
+    p.add_argument("--max-update", type=int, default=100)
+    p.add_argument("--max-tokens", type=int, default=40000)
+    p.add_argument("--update-freq", type=int, default=1)
+    p.add_argument("--max-target-positions", type=int, default=None)
+    p.add_argument("--max-source-positions", type=int, default=None)
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--fp16", action="store_true")
+    p.add_argument("--fp16-init-scale", type=int, default=128)
+    p.add_argument("--num-workers", type=int, default=0)
+    p.add_argument("--user-dir", default=None)
+    p.add_argument("--save-dir", default=None)
+    p.add_argument("--log-interval", type=int, default=10)
+    # accepted for command-line compatibility with 1_train.sh (no effect on the training step)
+    p.add_argument("--distributed-world-size", type=int, default=None)
+    p.add_argument("--tensorboard-logdir", default=None)
+    p.add_argument("--vocoder", default=None)
+    p.add_argument("--train-subset", default="train")
+    p.add_argument("--valid-subset", default="valid")
+    p.add_argument("--gen-subset", default="test")
+    p.add_argument("--required-batch-size-multiple", type=int, default=1)
+    p.add_argument("--synthetic", action="store_true", help="synthetic Speech-Multi30K-shaped data")
+    return p

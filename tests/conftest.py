@@ -16,9 +16,9 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
-def pkg():
+def pkg(sub=None):
     """The product package (directory name `multimodal-s2ut_amd`, imported by path)."""
-    return importlib.import_module("multimodal-s2ut_amd")
+    return importlib.import_module("multimodal-s2ut_amd" + (f".{sub}" if sub else ""))
 
 
 def golden_files(prefix):

@@ -1,0 +1,228 @@
+"""Plugin surface (task / arch / criterion names, flags, fusion YAML) and the fairseq adapter.
+
+fairseq is not importable here: the adapter is checked against a stub registry that mimics the
+decorator API of fairseq.tasks / fairseq.models / fairseq.criterions.
+"""
+import sys
+import types
+
+import pytest
+import torch
+
+from conftest import pkg
+
+CANONICAL = (  # scripts/textless/1_train.sh:105-125 (paths replaced)
+    "/data --distributed-world-size 1 --tensorboard-logdir /tmp/tb --config-yaml config.yaml "
+    "--task multimodal_speech_to_speech --target-is-code --target-code-size 1000 --vocoder code_hifigan "
+    "--criterion speech_to_unit --label-smoothing 0.2 --arch mm_s2ut_transformer "
+    "--share-decoder-input-output-embed --dropout 0.1 --attention-dropout 0.1 --relu-dropout 0.1 "
+    "--train-subset train --valid-subset valid --save-dir /tmp/ck --lr 0.0005 --lr-scheduler inverse_sqrt "
+    "--warmup-init-lr 1e-7 --warmup-updates 10000 --optimizer adam --adam-betas (0.9,0.98) "
+    "--clip-norm 10.0 --max-update 100 --max-tokens 40000 --max-target-positions 3000 --update-freq 1 "
+    "--required-batch-size-multiple 1 --multitask-config-yaml config_multitask.yaml "
+    "--multimodal-translation-config-yaml {yaml} --encoder-embed-dim 768 --encoder-ffn-embed-dim 3072 "
+    "--gen-subset test --user-dir mm_s2ut --seed 1 --fp16 --num-workers 8")
+
+# the shipped fusion YAML's effective values (mm_s2ut/config/multimodal_s2ut_transformer.yaml)
+FUSION_YAML = """
+SA_image_dropout: 0.1
+SA_text_dropout: 0.0
+SA_attention_dropout: 0.1
+image_pre_norm: True
+is_fusion_top: True
+image_feat_path: ["/feats/vit_base_patch16_384"]
+image_feat_dim: [768]
+flickr30k_root: /flickr30k
+load_visual_extractor_type: null
+load_visual_extractor: null
+modality_dropout: -0.5
+audio_dropout: -0.5
+multimodal_attention_type: multimodal_attention
+use_selective_gate: True
+is_merge_text_img: False
+"""
+
+
+def _plugins():
+    return pkg("plugins")
+
+
+def _args(tmp_path, extra=""):
+    y = tmp_path / "mm.yaml"
+    y.write_text(FUSION_YAML)
+    return _plugins().build_parser().parse_args((CANONICAL.format(yaml=y) + extra).split())
+
+
+def test_registry_names():
+    R = _plugins().REGISTRY
+    assert "multimodal_speech_to_speech" in R["task"]
+    assert "mm_s2ut_transformer" in R["model"] and "mm_s2ut_transformer" in R["arch"]
+    for c in ("speech_to_unit", "speech_to_speech", "speech_to_unit_v2"):
+        assert c in R["criterion"]
+
+
+def test_canonical_command_gives_base_config(tmp_path):
+    P = _plugins()
+    a = _args(tmp_path)
+    task = P.REGISTRY["task"][a.task].setup_task(a)
+    cfg = P.cfg_from_args(a, task.multimodal_translation_config, task.vocab_size)
+    assert cfg == pkg("model").default_cfg()
+    assert task.vocab_size == 1004 and task.padding_idx == 1 and task.eos == 2
+
+
+def test_arch_defaults_and_overrides(tmp_path):
+    P = _plugins()
+    a = _args(tmp_path, " --encoder-layers 2 --decoder-layers 2 --decoder-embed-dim 768")
+    task = P.MultiModalSpeechToSpeechTask(a)
+    cfg = P.cfg_from_args(a, task.multimodal_translation_config)
+    assert cfg["encoder_layers"] == 2 and cfg["decoder_layers"] == 2
+    assert cfg["decoder_ffn_embed_dim"] == 3072  # follows encoder_ffn_embed_dim (arch default)
+    b = P.build_parser().parse_args(["/d", "--fp16", "--share-decoder-input-output-embed"])
+    cfgb = P.cfg_from_args(b)
+    assert cfgb["encoder_embed_dim"] == 512 and cfgb["max_target_positions"] == 1024
+    assert cfgb["fusion"] is False
+
+
+def test_unsupported_options_fail_loudly(tmp_path):
+    P = _plugins()
+    a = P.build_parser().parse_args(["/d", "--fp16"])  # no --share-decoder-input-output-embed
+    with pytest.raises(NotImplementedError, match="share-decoder"):
+        P.cfg_from_args(a)
+    y = tmp_path / "sel.yaml"
+    y.write_text(FUSION_YAML.replace("multimodal_attention_type: multimodal_attention",
+                                     "multimodal_attention_type: merge_attention"))
+    fus = P.load_fusion_yaml(str(y))
+    a = P.build_parser().parse_args(["/d", "--fp16", "--share-decoder-input-output-embed"])
+    with pytest.raises(NotImplementedError, match="merge_attention"):
+        P.cfg_from_args(a, fus)
+    y.write_text(FUSION_YAML.replace("image_feat_dim: [768]", "image_feat_dim: [256, 768]"))
+    with pytest.raises(NotImplementedError, match="one image-feature type"):
+        P.cfg_from_args(a, P.load_fusion_yaml(str(y)))
+    with pytest.raises(NotImplementedError, match="pretrained"):
+        P.MultiModalSpeechToSpeechTask(P.build_parser().parse_args(
+            ["/d", "--fp16", "--wav2vec2-model-dir", "/w2v"]))
+
+
+def test_selective_attention_yaml(tmp_path):
+    P = _plugins()
+    y = tmp_path / "sel.yaml"
+    y.write_text(FUSION_YAML.replace("multimodal_attention_type: multimodal_attention",
+                                     "multimodal_attention_type: selective_attention")
+                 .replace("use_selective_gate: True", "use_selective_gate: False"))
+    a = P.build_parser().parse_args(["/d", "--fp16", "--share-decoder-input-output-embed"])
+    cfg = P.cfg_from_args(a, P.load_fusion_yaml(str(y)))
+    assert cfg["multimodal_attention_type"] == "selective_attention"
+    assert cfg["use_selective_gate"] is False and cfg["fusion"] is True
+
+
+def test_cli_rejects_non_fp16_and_real_data():
+    cli = pkg("cli")
+    with pytest.raises(SystemExit, match="fp16"):
+        cli.main(["/d", "--share-decoder-input-output-embed"])
+    with pytest.raises(SystemExit, match="synthetic"):
+        cli.main(["/d", "--fp16", "--share-decoder-input-output-embed"])
+    with pytest.raises(SystemExit, match="unknown criterion"):
+        cli.main(["/d", "--fp16", "--criterion", "cross_entropy", "--synthetic"])
+
+
+def _stub_fairseq(monkeypatch, preexisting_criteria=("speech_to_unit",)):
+    regs = {"task": {}, "model": {}, "arch": {}, "criterion": {c: object for c in preexisting_criteria}}
+
+    def deco(kind):
+        def reg(name):
+            def d(cls):
+                assert name not in regs[kind], f"duplicate {kind} {name}"
+                regs[kind][name] = cls
+                return cls
+            return d
+        return reg
+
+    def reg_arch(model_name, arch_name):
+        def d(fn):
+            regs["arch"][arch_name] = (model_name, fn)
+            return fn
+        return d
+
+    class FairseqTask:
+        def __init__(self, args):
+            self.args = args
+
+    class FairseqCriterion(torch.nn.Module):
+        def __init__(self, task):
+            super().__init__()
+            self.task = task
+
+    fs = types.ModuleType("fairseq")
+    tasks = types.ModuleType("fairseq.tasks")
+    tasks.FairseqTask, tasks.register_task = FairseqTask, deco("task")
+    models = types.ModuleType("fairseq.models")
+    models.BaseFairseqModel = torch.nn.Module
+    models.register_model, models.register_model_architecture = deco("model"), reg_arch
+    crit = types.ModuleType("fairseq.criterions")
+    crit.FairseqCriterion, crit.register_criterion = FairseqCriterion, deco("criterion")
+    crit.CRITERION_REGISTRY = regs["criterion"]
+    for name, m in (("fairseq", fs), ("fairseq.tasks", tasks), ("fairseq.models", models),
+                    ("fairseq.criterions", crit)):
+        monkeypatch.setitem(sys.modules, name, m)
+    return fs, regs
+
+
+def test_fairseq_adapter_registers_reference_names(monkeypatch):
+    fs, regs = _stub_fairseq(monkeypatch)
+    task, model, crits = pkg("fairseq_adapter").register(fs)
+    assert regs["task"]["multimodal_speech_to_speech"] is task
+    assert regs["model"]["mm_s2ut_transformer"] is model
+    assert regs["arch"]["mm_s2ut_transformer"][0] == "mm_s2ut_transformer"
+    # fairseq's built-in speech_to_unit keeps its name; the free aliases are ours
+    assert regs["criterion"]["speech_to_unit"] is object
+    assert set(crits) == {"speech_to_speech", "speech_to_unit_v2"}
+    ns = types.SimpleNamespace()
+    regs["arch"]["mm_s2ut_transformer"][1](ns)
+    assert ns.encoder_embed_dim == 512 and ns.decoder_layers == 6 and ns.conv_channels == 1024
+
+
+def _reducer_worker(rank, world, port, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        par = pkg("parallel")
+        r, w, _ = par.init_from_env(backend="gloo")
+        n = 1000
+        g = torch.arange(n, dtype=torch.float32) * (r + 1)
+        red = par.GradAllReducer(g, bucket_mb=256 * 4 / 2 ** 20)  # 256-element buckets
+        assert len(red.bounds) == 4
+        for upto in (100, 300, 600, 1000):  # layer completion offsets
+            red.ready(upto)
+        launched_before_finish = red.next
+        red.finish()
+        s = torch.tensor([1.0 + r, 10.0 * (r + 1)])
+        par.all_reduce_scalars(s)
+        q.put((r, launched_before_finish, torch.equal(g, torch.arange(n, dtype=torch.float32) * 3),
+               s.tolist()))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e), None))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_grad_allreducer_gloo_world2():
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_reducer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for r, launched, ok, scal in res:
+        assert launched == 4, (r, launched, ok)  # every bucket launched during the "backward"
+        assert ok is True
+        assert scal == [3.0, 30.0]
