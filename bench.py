@@ -159,7 +159,7 @@ def main():
     batches = make_batches(cfg, rank, args.nbatches, args.max_tokens, device, fe)
 
     def step(i):
-        wb, batch, _, _ = batches[i % len(batches)]
+        wb, batch = batches[i % len(batches)][:2]
         batch.src = fe(wb)
         tr.train_step(batch)
 

@@ -222,18 +222,20 @@ int mms2ut_ls_xent_bwd(const mms2ut_half* logits, int64_t ld, const int64_t* tar
 enum {
   MMS_OST_MULT = 0, MMS_OST_GNORM = 1, MMS_OST_OVERFLOW = 2, MMS_OST_STEP = 3,
   MMS_OST_STEP_SIZE = 4, MMS_OST_LOSS_SCALE = 5, MMS_OST_ITER = 6, MMS_OST_LAST_OVERFLOW = 7,
-  MMS_OST_LAST_RESCALE = 8, MMS_OST_CLIP_COEF = 9, MMS_OST_FATAL = 10, MMS_OST_SIZE = 16
+  MMS_OST_LAST_RESCALE = 8, MMS_OST_CLIP_COEF = 9, MMS_OST_FATAL = 10, MMS_OST_LR = 11, MMS_OST_SIZE = 16
 };
 int mms2ut_grad_sqnorm(const mms2ut_half* grad, int64_t n, float* part, int nparts,
                        hipStream_t stream);
 int mms2ut_grad_norm_finalize(const float* part, int nparts, float* ost, const float* sample_size,
                               hipStream_t stream);
-int mms2ut_optim_prepare(float* ost, float lr, float beta1, float beta2, float clip_norm,
-                         float scale_window, float min_loss_scale, hipStream_t stream);
+/* lr = fairseq inverse_sqrt(lr, warmup_init_lr, warmup_updates) evaluated on device at the count of
+ * completed (non-overflow) updates, stored in ost[MMS_OST_LR] for adam. */
+int mms2ut_optim_prepare(float* ost, float lr, float warmup_init_lr, float warmup_updates, float beta1,
+                         float beta2, float clip_norm, float scale_window, float min_loss_scale,
+                         hipStream_t stream);
 int mms2ut_adam_fp16_master(mms2ut_half* param, const mms2ut_half* grad, float* master,
                             float* exp_avg, float* exp_avg_sq, int64_t n, const float* ost,
-                            float lr, float beta1, float beta2, float eps, float weight_decay,
-                            hipStream_t stream);
+                            float beta1, float beta2, float eps, float weight_decay, hipStream_t stream);
 
 /* ---------------------------------------------------------------- fbank front end
  * fairseq get_fbank -> torchaudio.compliance.kaldi.fbank (audio_utils.py:326-349), 80 bins,

@@ -89,8 +89,8 @@ SIGNATURES = {
     "mms2ut_ls_xent_bwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp]),
     "mms2ut_grad_sqnorm": (i32, [vp, i64, vp, i32, vp]),
     "mms2ut_grad_norm_finalize": (i32, [vp, i32, vp, vp, vp]),
-    "mms2ut_optim_prepare": (i32, [vp, f32, f32, f32, f32, f32, f32, vp]),
-    "mms2ut_adam_fp16_master": (i32, [vp, vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, f32, vp]),
+    "mms2ut_optim_prepare": (i32, [vp, f32, f32, f32, f32, f32, f32, f32, f32, vp]),
+    "mms2ut_adam_fp16_master": (i32, [vp, vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, vp]),
     "mms2ut_fbank_frames": (i32, [vp, i32, vp, vp]),
     "mms2ut_fbank_f32": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
     "mms2ut_fbank_cmvn_collate": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),

@@ -68,7 +68,7 @@ def main(argv=None):
                     ln2 = math.log(2)
                     rec = {"num_updates": upd, "loss": lg[0] / lg[2] / ln2, "nll_loss": lg[1] / lg[2] / ln2,
                            "ppl": 2 ** (lg[1] / lg[2] / ln2), "wps": ntok / max(el, 1e-9),
-                           "ups": upd / max(el, 1e-9), "lr": tr.opt.get_lr(), "gnorm": st["gnorm"],
+                           "ups": upd / max(el, 1e-9), "lr": st["lr"], "gnorm": st["gnorm"],
                            "loss_scale": st["loss_scale"], "overflow": st["overflow"]}
                     print(json.dumps(rec), flush=True)
             if upd >= args.max_update:

@@ -127,8 +127,8 @@ __global__ void grad_norm_finalize_kernel(const float* __restrict__ part, int np
 }
 
 // one thread: Adam step count / step size / clip coefficient and fairseq DynamicLossScaler
-__global__ void optim_prepare_kernel(float* ost, float lr, float b1, float b2, float clip, float scale_window,
-                                     float min_scale) {
+__global__ void optim_prepare_kernel(float* ost, float lr_peak, float warmup_init_lr, float warmup_updates,
+                                     float b1, float b2, float clip, float scale_window, float min_scale) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const bool overflow = ost[MMS_OST_OVERFLOW] != 0.f;
   float it = ost[MMS_OST_ITER];
@@ -143,11 +143,22 @@ __global__ void optim_prepare_kernel(float* ost, float lr, float b1, float b2, f
     ost[MMS_OST_ITER] = it + 1.f;
     return;
   }
-  const float step = ost[MMS_OST_STEP] + 1.f;
+  // fairseq inverse_sqrt at num_updates = completed (non-skipped) updates: the schedule only
+  // advances on a real step (Trainer.train_step skips set_num_updates on overflow)
+  const float nu = ost[MMS_OST_STEP];
+  float lr;
+  if (warmup_updates > 0.f && nu < warmup_updates)
+    lr = warmup_init_lr + nu * ((lr_peak - warmup_init_lr) / warmup_updates);
+  else
+    lr = lr_peak * sqrtf(fmaxf(warmup_updates, 1.f)) * rsqrtf(fmaxf(nu, 1.f));
+  ost[MMS_OST_LR] = lr;
+  const float step = nu + 1.f;
   ost[MMS_OST_STEP] = step;
   const double bc1 = 1.0 - pow((double)b1, (double)step), bc2 = 1.0 - pow((double)b2, (double)step);
   ost[MMS_OST_STEP_SIZE] = (float)(lr * sqrt(bc2) / bc1);
-  ost[MMS_OST_CLIP_COEF] = clip > 0.f ? fminf(1.f, clip / (ost[MMS_OST_GNORM] + 1e-6f)) : 1.f;
+  // FP16Optimizer.clip_grad_norm with a scaler: multiply_factor *= max_norm / norm when norm > max_norm
+  const float gn = ost[MMS_OST_GNORM];
+  ost[MMS_OST_CLIP_COEF] = (clip > 0.f && gn > clip) ? clip / gn : 1.f;
   // scaler.update(): grow every scale_window clean iterations
   const float since = it - ost[MMS_OST_LAST_OVERFLOW];
   if (fmodf(since, scale_window) == 0.f) {
@@ -159,8 +170,9 @@ __global__ void optim_prepare_kernel(float* ost, float lr, float b1, float b2, f
 
 __global__ void adam_kernel(h16* __restrict__ param, const h16* __restrict__ grad, float* __restrict__ master,
                             float* __restrict__ m, float* __restrict__ v, long n, const float* __restrict__ ost,
-                            float lr, float b1, float b2, float eps, float wd) {
+                            float b1, float b2, float eps, float wd) {
   if (ost[MMS_OST_OVERFLOW] != 0.f) return;  // overflow: skip (FP16Optimizer OverflowError path)
+  const float lr = ost[MMS_OST_LR];
   const float mult = ost[MMS_OST_MULT] * ost[MMS_OST_CLIP_COEF];
   const float step_size = ost[MMS_OST_STEP_SIZE];
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -227,22 +239,23 @@ extern "C" int mms2ut_grad_norm_finalize(const float* part, int nparts, float* o
   return mms::check_launch("grad_norm_finalize");
 }
 
-extern "C" int mms2ut_optim_prepare(float* ost, float lr, float beta1, float beta2, float clip_norm,
-                                    float scale_window, float min_loss_scale, hipStream_t s) {
+extern "C" int mms2ut_optim_prepare(float* ost, float lr, float warmup_init_lr, float warmup_updates,
+                                    float beta1, float beta2, float clip_norm, float scale_window,
+                                    float min_loss_scale, hipStream_t s) {
   MMS_REQUIRE(scale_window >= 1.f, "optim_prepare: scale_window must be >= 1");
-  hipLaunchKernelGGL(optim_prepare_kernel, dim3(1), dim3(64), 0, s, ost, lr, beta1, beta2, clip_norm,
-                     scale_window, min_loss_scale);
+  MMS_REQUIRE(warmup_updates >= 0.f, "optim_prepare: warmup_updates must be >= 0");
+  hipLaunchKernelGGL(optim_prepare_kernel, dim3(1), dim3(64), 0, s, ost, lr, warmup_init_lr, warmup_updates,
+                     beta1, beta2, clip_norm, scale_window, min_loss_scale);
   return mms::check_launch("optim_prepare");
 }
 
 extern "C" int mms2ut_adam_fp16_master(h16* param, const h16* grad, float* master, float* exp_avg,
-                                       float* exp_avg_sq, int64_t n, const float* ost, float lr,
-                                       float beta1, float beta2, float eps, float weight_decay,
-                                       hipStream_t s) {
+                                       float* exp_avg_sq, int64_t n, const float* ost, float beta1,
+                                       float beta2, float eps, float weight_decay, hipStream_t s) {
   if (n == 0) return 0;
   long g = (n + 255) / 256;
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(adam_kernel, dim3((int)g), dim3(256), 0, s, param, grad, master, exp_avg, exp_avg_sq,
-                     (long)n, ost, lr, beta1, beta2, eps, weight_decay);
+                     (long)n, ost, beta1, beta2, eps, weight_decay);
   return mms::check_launch("adam");
 }

@@ -402,7 +402,7 @@ def ls_xent_bwd(logits, ld, target, rows, V, eps, pad, lse, grad, out):
 
 
 OST_MULT, OST_GNORM, OST_OVERFLOW, OST_STEP, OST_STEP_SIZE, OST_LOSS_SCALE, OST_ITER, \
-    OST_LAST_OVERFLOW, OST_LAST_RESCALE, OST_CLIP_COEF, OST_FATAL = range(11)
+    OST_LAST_OVERFLOW, OST_LAST_RESCALE, OST_CLIP_COEF, OST_FATAL, OST_LR = range(12)
 OST_SIZE = 16
 
 
@@ -412,14 +412,14 @@ def grad_norm(grad, ost, sample_size=None, nparts=1024):
     call("mms2ut_grad_norm_finalize", part.data_ptr(), nparts, ost.data_ptr(), _p(sample_size), _s())
 
 
-def optim_prepare(ost, lr, beta1, beta2, clip, scale_window, min_scale):
-    call("mms2ut_optim_prepare", ost.data_ptr(), float(lr), float(beta1), float(beta2), float(clip),
-         float(scale_window), float(min_scale), _s())
+def optim_prepare(ost, lr, warmup_init_lr, warmup_updates, beta1, beta2, clip, scale_window, min_scale):
+    call("mms2ut_optim_prepare", ost.data_ptr(), float(lr), float(warmup_init_lr), float(warmup_updates),
+         float(beta1), float(beta2), float(clip), float(scale_window), float(min_scale), _s())
 
 
-def adam(param, grad, master, m, v, ost, lr, beta1, beta2, eps, wd):
+def adam(param, grad, master, m, v, ost, beta1, beta2, eps, wd):
     call("mms2ut_adam_fp16_master", param.data_ptr(), grad.data_ptr(), master.data_ptr(),
-         m.data_ptr(), v.data_ptr(), param.numel(), ost.data_ptr(), float(lr), float(beta1),
+         m.data_ptr(), v.data_ptr(), param.numel(), ost.data_ptr(), float(beta1),
          float(beta2), float(eps), float(wd), _s())
 
 # ============================================================================ fbank

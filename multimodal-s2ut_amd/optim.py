@@ -29,7 +29,7 @@ class FP16Adam:
         self.scale_window = scale_window or max(1, int(2 ** 14 / world_size / update_freq))
         self.min_loss_scale = min_loss_scale
         self.warmup_updates, self.warmup_init_lr = warmup_updates, warmup_init_lr
-        self.num_updates = 0
+        self.num_updates = 0  # for get_lr() only; the step counts updates on device (ost[OST_STEP])
         ost = torch.zeros(K.OST_SIZE, dtype=torch.float32)
         ost[K.OST_LOSS_SCALE] = init_scale
         ost[K.OST_LAST_OVERFLOW] = -1.0
@@ -45,7 +45,8 @@ class FP16Adam:
         return self.ost[K.OST_LOSS_SCALE]
 
     def get_lr(self):
-        """fairseq inverse_sqrt schedule at the current update count."""
+        """fairseq inverse_sqrt schedule at ``num_updates`` (host restatement; the step itself
+        evaluates the same schedule on device at the count of completed, non-skipped updates)."""
         if self.warmup_updates > 0 and self.num_updates < self.warmup_updates:
             step = (self.lr - self.warmup_init_lr) / self.warmup_updates
             return self.warmup_init_lr + self.num_updates * step
@@ -54,16 +55,15 @@ class FP16Adam:
 
     def step(self, sample_size):
         """sample_size: device fp32 tensor [1] (all-reduced ntokens)."""
-        lr = self.get_lr()
         b1, b2 = self.betas
         K.grad_norm(self.params.grad, self.ost, sample_size)
-        K.optim_prepare(self.ost, lr, b1, b2, self.clip, self.scale_window, self.min_loss_scale)
+        K.optim_prepare(self.ost, self.lr, self.warmup_init_lr, self.warmup_updates, b1, b2, self.clip,
+                        self.scale_window, self.min_loss_scale)
         K.adam(self.params.flat, self.params.grad, self.master, self.exp_avg, self.exp_avg_sq, self.ost,
-               lr, b1, b2, self.eps, self.wd)
-        self.num_updates += 1
+               b1, b2, self.eps, self.wd)
 
     def stats(self):
         o = self.ost.cpu()
         return {"gnorm": float(o[K.OST_GNORM]), "overflow": bool(o[K.OST_OVERFLOW]),
                 "loss_scale": float(o[K.OST_LOSS_SCALE]), "step": int(o[K.OST_STEP]),
-                "fatal": bool(o[K.OST_FATAL])}
+                "fatal": bool(o[K.OST_FATAL]), "lr": float(o[K.OST_LR])}

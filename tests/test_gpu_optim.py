@@ -1,0 +1,62 @@
+"""GPU: device-resident FP16Optimizer/Adam/DynamicLossScaler/inverse_sqrt (optim.py + loss_optim.hip)
+against the oracle restatement of fairseq's (oracle/ref_model.py: fp16_optimizer_step,
+DynamicLossScaler, inverse_sqrt_lr) over several updates: overflow skip, loss-scale halving and
+growth, clipping, warmup->decay.  Master weights: relative error < 1e-5; fp16 params: within 1 ulp."""
+import pytest
+import torch
+
+from conftest import pkg
+from oracle import ref_model as R
+
+pytestmark = pytest.mark.gpu
+
+
+class _Params:
+    def __init__(self, n, dev):
+        g = torch.Generator().manual_seed(0)
+        self.flat = (torch.randn(n, generator=g) * 0.05).half().to(dev)
+        self.grad = torch.zeros(n, dtype=torch.float16, device=dev)
+
+
+@pytest.mark.parametrize("clip", [10.0, 0.05])
+def test_fp16_adam_matches_fairseq_restatement(clip):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mm = pkg()
+    dev = torch.device("cuda")
+    n = 1_000_003
+    P = _Params(n, dev)
+    kw = dict(lr=1e-3, betas=(0.9, 0.98), clip_norm=clip, init_scale=128.0, scale_window=2,
+              warmup_updates=3, warmup_init_lr=1e-7)
+    opt = mm.optim.FP16Adam(P, **kw)
+    master = P.flat.float().cpu()
+    ea, eas = torch.zeros(n), torch.zeros(n)
+    scaler = R.DynamicLossScaler(128.0, scale_window=2)
+    done = 0
+    gen = torch.Generator().manual_seed(1)
+    for it in range(7):
+        ss = 1000.0 + 17 * it
+        g = (torch.randn(n, generator=gen) * 3e-3 * scaler.loss_scale * ss / 1000).half()
+        if it == 2:
+            g[12345] = float("inf")  # fp16 overflow in backward
+        P.grad.copy_(g.to(dev))
+        opt.step(torch.tensor([ss], device=dev))
+        st = opt.stats()
+        lr = R.inverse_sqrt_lr(done, 1e-3, 3, 1e-7)
+        norm, overflow = R.fp16_optimizer_step([master], [g], [(ea, eas)], done + 1, lr,
+                                               1.0 / (scaler.loss_scale * ss), clip_norm=clip)
+        assert st["overflow"] == overflow, it
+        if overflow:
+            scaler.overflow()
+        else:
+            done += 1
+            scaler.update()
+            assert abs(st["gnorm"] - norm) <= 1e-4 * norm, (it, st["gnorm"], norm)
+            assert abs(st["lr"] - lr) <= 1e-6 * lr
+        assert st["loss_scale"] == scaler.loss_scale, (it, st["loss_scale"], scaler.loss_scale)
+        assert st["step"] == done
+        m = opt.master.cpu()
+        err = ((m - master).norm() / master.norm()).item()
+        assert err < 1e-5, (it, err)
+        p16 = P.flat.cpu().float()
+        assert torch.allclose(p16, master.half().float(), rtol=1e-3, atol=1e-7), it
