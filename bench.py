@@ -176,6 +176,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    t_issue = time.perf_counter()  # host finished enqueueing (host-bound if ~ t1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -224,6 +225,8 @@ def main():
                          "frac": (achieved / MFMA_PEAK_F16) if achieved else None, "traffic": None,
                          "gemm_ms_per_step": gemm_all / world / args.steps,
                          "gemm_launches_per_step": nl_all / world / args.steps,
+                         "gemm_launched_tflops": launched_flops / max(gemm_ms, 1e-9) / 1e9,
+                         "host_issue_ms_per_step": 1e3 * (t_issue - t0) / args.steps,
                          "note": "achieved = SURVEY §8d algorithmic FLOPs (true lengths, 3x fwd) / summed "
                                  "HIP-event durations of every GEMM launch in the timed region (weight-grad "
                                  "GEMMs overlap the dgrad chain on a side stream, so contention inflates "

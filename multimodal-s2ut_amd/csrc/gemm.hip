@@ -37,6 +37,7 @@ struct GemmP {
   const h16* aux; long ldaux; long sX1, sX2;
   h16* out2; long ldo2;
   float p; uint32_t thresh; uint64_t seed, offset; long ld_rng;
+  int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity
 };
 
 MMS_DEV int swz_mn(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
@@ -211,6 +212,121 @@ MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, in
   }
 }
 
+// 8 consecutive columns n..n+7 (n % 8 == 0) of row m: 16-B operand loads / stores when aligned,
+// otherwise two 4-wide calls of epilogue_store (which also handles the N tail)
+template <int EPI>
+MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, int n, const float (&v)[8]) {
+  if (m >= P.M || n >= P.N) return;
+  const int N = P.N;
+  if (EPI == MMS_EPI_F32) {
+    float* C = reinterpret_cast<float*>(Cz) + (long)m * P.ldc;
+    if (n + 7 < N) {
+      *reinterpret_cast<f32x4*>(C + n) = f32x4{v[0] * P.alpha, v[1] * P.alpha, v[2] * P.alpha, v[3] * P.alpha};
+      *reinterpret_cast<f32x4*>(C + n + 4) = f32x4{v[4] * P.alpha, v[5] * P.alpha, v[6] * P.alpha, v[7] * P.alpha};
+    } else {
+      for (int r = 0; r < 8; ++r) if (n + r < N) C[n + r] = v[r] * P.alpha;
+    }
+    return;
+  }
+  if (!(P.vec16 && n + 7 < N)) {
+    epilogue_store<EPI>(P, Cz, auxz, m, n, f32x4{v[0], v[1], v[2], v[3]});
+    epilogue_store<EPI>(P, Cz, auxz, m, n + 4, f32x4{v[4], v[5], v[6], v[7]});
+    return;
+  }
+  float x[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) x[r] = v[r] * P.alpha;
+  if (P.bias && EPI != MMS_EPI_RELU_DROP_BWD) {
+    const h16x8 bv = *reinterpret_cast<const h16x8*>(P.bias + n);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] += (float)bv[r];
+  }
+  h16* C = reinterpret_cast<h16*>(Cz) + (long)m * P.ldc;
+  auto ld8 = [&](const h16* src, float (&o)[8]) {
+    const h16x8 t = *reinterpret_cast<const h16x8*>(src);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = (float)t[r];
+  };
+  bool keep[8] = {true, true, true, true, true, true, true, true};
+  if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID) && P.thresh) {
+    const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
+    bool k0[4], k1[4];
+    mms_keep4(P.seed, c0, P.thresh, k0);
+    mms_keep4(P.seed, c0 + 4, P.thresh, k1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { keep[r] = k0[r]; keep[r + 4] = k1[r]; }
+  }
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  float o[8];
+  if (EPI == MMS_EPI_RELU_DROP) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = keep[r] ? fmaxf(x[r], 0.f) * dscale : 0.f;
+  } else if (EPI == MMS_EPI_DROP_RESID) {
+    float a[8];
+    ld8(auxz + (long)m * P.ldaux + n, a);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = a[r] + (keep[r] ? x[r] * dscale : 0.f);
+  } else if (EPI == MMS_EPI_GATE) {
+    float ov[8], tv[8], g[8];
+    ld8(auxz + (long)m * P.ldaux + n, ov);
+    ld8(auxz + (long)m * P.ldaux + N + n, tv);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      g[r] = sigmoidf_(x[r]);
+      o[r] = tv[r] + g[r] * (ov[r] - tv[r]);
+    }
+    h16x8 gv;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) gv[r] = (h16)g[r];
+    *reinterpret_cast<h16x8*>(P.out2 + (long)m * P.ldo2 + n) = gv;
+  } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
+    float h[8];
+    ld8(auxz + (long)m * P.ldaux + n, h);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
+  } else if (EPI == MMS_EPI_F16_ACC) {
+    float c[8];
+    ld8(C + n, c);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = c[r] + x[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = x[r];
+  }
+  h16x8 ov8;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) ov8[r] = (h16)o[r];
+  *reinterpret_cast<h16x8*>(C + n) = ov8;
+}
+
+// Epilogue through LDS: each wave parks its 64x64 fp32 accumulator tile in 16 KiB of the (now idle)
+// operand ring, XOR-swizzled by row, then re-reads it row-major so a lane owns 8 consecutive
+// columns: every global load/store of the epilogue covers whole 128-B row segments instead of
+// 16 rows x 32 B.  Caller guarantees all waves are past their last operand read.
+template <int EPI>
+MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4], int bm, int bn,
+                             int wm, int wn, int wid, int lane, void* Cz, const h16* auxz) {
+  float* stage = reinterpret_cast<float*>(smem) + wid * 64 * 64;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = i * 16 + (lane & 15);
+      const int c = j * 4 + (lane >> 4);
+      *reinterpret_cast<f32x4*>(stage + r * 64 + ((c ^ (r & 15)) << 2)) = acc[i][j];
+    }
+  __syncthreads();
+  const int q = lane & 7;
+#pragma unroll 2
+  for (int pass = 0; pass < 8; ++pass) {
+    const int r = pass * 8 + (lane >> 3);
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + r * 64 + (((2 * q) ^ (r & 15)) << 2));
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + r * 64 + (((2 * q + 1) ^ (r & 15)) << 2));
+    const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    epilogue_store8<EPI>(P, Cz, auxz, bm + wm * 64 + r, bn + wn * 64 + 8 * q, v);
+  }
+}
+
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
@@ -288,14 +404,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int t
   else
     Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
   const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = bm + wm * 64 + i * 16 + (lane & 15);
-      const int n = bn + wn * 64 + j * 16 + 4 * (lane >> 4);
-      epilogue_store<EPI>(P, Cz, auxz, m, n, acc[i][j]);
-    }
+  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -415,14 +524,10 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   else
     Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
   const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = bm + wm * 64 + i * 16 + (lane & 15);
-      const int n = bn + wn * 64 + j * 16 + 4 * (lane >> 4);
-      epilogue_store<EPI>(P, Cz, auxz, m, n, acc[i][j]);
-    }
+  // the ring is idle once every wave is past its last fragment read (no DMA is in flight: the
+  // last k-step waited for vmcnt(0))
+  __syncthreads();
+  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
 }
 
 template <bool A_KC, bool B_KC>
@@ -555,6 +660,15 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
   MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
   MMS_REQUIRE(a->epi != MMS_EPI_GATE || a->out2, "gemm: gate epilogue needs out2");
+  {
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    bool v = al16(a->C) && a->ldc % 8 == 0 && a->sC1 % 8 == 0 && a->sC2 % 8 == 0;
+    if (a->aux) v = v && al16(a->aux) && a->ldaux % 8 == 0 && a->sX1 % 8 == 0 && a->sX2 % 8 == 0 &&
+                    (a->epi != MMS_EPI_GATE || a->N % 8 == 0);
+    if (a->out2) v = v && al16(a->out2) && a->ldo2 % 8 == 0;
+    if (a->bias) v = v && al16(a->bias);
+    P.vec16 = v ? 1 : 0;
+  }
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
   const int nz = a->batch * splitk;
   MMS_REQUIRE(nz <= 65535, "gemm: batch*splitk too large (%d)", nz);

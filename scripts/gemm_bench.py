@@ -21,6 +21,8 @@ SHAPES = [  # name, M, N, K, a_kc, b_kc, splitk
     ("wgrad 3072x768", 3072, 768, M, False, False, 4),
     ("wgrad 768x768", 768, 768, M, False, False, 15),
     ("conv2 fwd", 10000, 1536, 2560, True, True, 1),
+    ("square 4096", 4096, 4096, 4096, True, True, 1),
+    ("square 8192", 8192, 8192, 8192, True, True, 1),
 ]
 
 
@@ -50,8 +52,21 @@ def run(name, m, n, k, a_kc, b_kc, s, reps=20):
             torch.cuda.synchronize()
             t = e0.elapsed_time(e1) / reps
             res[path] = min(res.get(path, 1e9), t)
+    # hipBLASLt through torch on the same operands (C = A·B^T in our convention)
+    At = A if a_kc else A.t()
+    Bt = B.t() if b_kc else B
+    for _ in range(3):
+        torch.matmul(At, Bt)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.matmul(At, Bt)
+    e1.record()
+    torch.cuda.synchronize()
+    res["torch"] = e0.elapsed_time(e1) / reps
     fl = 2.0 * m * n * k
-    print(f"{name:18s} M={m:6d} N={n:5d} K={k:6d}  reg {res['reg']*1e3:7.1f}us {fl/res['reg']/1e9:6.0f} TF"
+    print(f"{name:18s} M={m:6d} N={n:5d} K={k:6d}  torch {res['torch']*1e3:7.1f}us {fl/res['torch']/1e9:6.0f} TF"
+          f"  reg {res['reg']*1e3:7.1f}us {fl/res['reg']/1e9:6.0f} TF"
           f"   dma {res['dma']*1e3:7.1f}us {fl/res['dma']/1e9:6.0f} TF"
           f"   dma2 {res['dma2']*1e3:7.1f}us {fl/res['dma2']/1e9:6.0f} TF", flush=True)
     os.environ.pop("MMS2UT_GEMM_PATH", None)
