@@ -82,6 +82,10 @@ int mms2ut_profile_end(float* total_ms, int* launches, double* flops);
 int mms2ut_splitk_reduce(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
                          void* out, int64_t ldo, int mode, float alpha, hipStream_t stream);
 
+/* `waiter` waits for all work enqueued on `signaler` so far (event record + stream wait).
+ * Forks/joins the weight-gradient side stream (the reference's DDP/autograd stream overlap). */
+int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler);
+
 /* ---------------------------------------------------------------- LayerNorm (eps, affine)
  * Replaces fairseq LayerNorm (self_attn_layer_norm / final_layer_norm / encoder_attn_layer_norm /
  * encoder.layer_norm / decoder.layer_norm) and nn.LayerNorm image_pre_norm_module

@@ -89,6 +89,7 @@ SIGNATURES = {
     "mms2ut_ls_xent_bwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp]),
     "mms2ut_grad_sqnorm": (i32, [vp, i64, vp, i32, vp]),
     "mms2ut_grad_norm_finalize": (i32, [vp, i32, vp, vp, vp]),
+    "mms2ut_stream_wait": (i32, [vp, vp]),
     "mms2ut_optim_prepare": (i32, [vp, f32, f32, f32, f32, f32, f32, f32, f32, vp]),
     "mms2ut_adam_fp16_master": (i32, [vp, vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, vp]),
     "mms2ut_fbank_frames": (i32, [vp, i32, vp, vp]),
@@ -121,7 +122,7 @@ def load():
 
 
 def call(name, *args):
-    rc = getattr(load(), name)(*args)
+    rc = getattr(_lib or load(), name)(*args)
     if rc != 0:
         raise HipError(f"{name} failed ({rc}): {_lib.mms2ut_last_error().decode()}")
     return rc

@@ -65,3 +65,33 @@ extern "C" int mms2ut_splitk_reduce(const float* slabs, int nsplit, int64_t slab
                      rows, cols, out, ldo, out_f16, alpha);
   return mms::check_launch("splitk_reduce");
 }
+
+// ------------------------------------------------------------------------------------------
+// stream fork/join for the weight-gradient side stream: `waiter` waits for everything enqueued
+// on `signaler` so far.  A small ring of timing-disabled events (created once per process) is
+// re-recorded round-robin; a wait binds to the record that precedes it, so reuse is safe.
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int kEvRing = 64;
+hipEvent_t g_ev[kEvRing];
+int g_ev_n = -1, g_ev_i = 0;
+}  // namespace
+
+extern "C" int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler) {
+  if (waiter == signaler) return 0;
+  if (g_ev_n < 0) {
+    for (int i = 0; i < kEvRing; ++i)
+      if (hipEventCreateWithFlags(&g_ev[i], hipEventDisableTiming) != hipSuccess) {
+        mms::set_error("stream_wait: hipEventCreate failed");
+        return 1;
+      }
+    g_ev_n = kEvRing;
+  }
+  hipEvent_t e = g_ev[g_ev_i];
+  g_ev_i = (g_ev_i + 1) % kEvRing;
+  if (hipEventRecord(e, signaler) != hipSuccess || hipStreamWaitEvent(waiter, e, 0) != hipSuccess) {
+    mms::set_error("stream_wait: record/wait failed");
+    return 1;
+  }
+  return 0;
+}

@@ -14,8 +14,19 @@ EPI_F16, EPI_RELU_DROP, EPI_DROP_RESID, EPI_F32, EPI_GATE, EPI_RELU_DROP_BWD, EP
 F16 = torch.float16
 
 
+_DEV = [None]
+
+
+def _dev():
+    if _DEV[0] is None:
+        _DEV[0] = torch.cuda.current_device()
+    return _DEV[0]
+
+
 def _s():
-    return torch.cuda.current_stream().cuda_stream
+    """Raw hipStream_t to enqueue on: the side stream inside a side region, else torch's current
+    stream (read through the C binding: torch.cuda.current_stream() costs ~5 us per call)."""
+    return _Side.override or torch._C._cuda_getCurrentRawStream(_dev())
 
 
 def _p(t):
@@ -130,33 +141,70 @@ def _splitk_for(tiles, kred, slots=512):
 class _Side:
     """Weight-gradient side stream: dW/db GEMMs and reductions do not feed the rest of the
     backward, so they run concurrently with the dgrad chain on a second HIP stream and fill the
-    CUs the (latency-bound, dependent) dgrad kernels leave idle."""
-    stream = None
+    CUs the (latency-bound, dependent) dgrad kernels leave idle.
+
+    The side region does not switch torch's current stream: kernels.py enqueues on
+    ``override``.  Device memory read by side kernels (dy temporaries, saved activations) is kept
+    referenced until ``side_join`` so the caching allocator cannot hand it to main-stream work
+    before the side stream has consumed it; side-only scratch (split-K slabs, column partials)
+    lives in persistent per-stream workspaces (the side stream serialises its own reuse)."""
+    stream = None      # torch.cuda.Stream (RCCL buckets are enqueued on it, parallel.py)
+    ptr = 0
     enabled = True
     used = False
+    override = 0
+    keep = []
+    ws = {}
+
+
+class _SideRegion:
+    __slots__ = ()
+
+    def __enter__(self):
+        _Side.override = _Side.ptr
+        return None
+
+    def __exit__(self, *a):
+        _Side.override = 0
+        return False
+
+
+_SIDE_REGION = _SideRegion()
 
 
 def side_begin(*tensors):
-    """Enter the side stream after everything enqueued so far on the current stream."""
-    if not _Side.enabled or not torch.cuda.is_available():
+    """Fork: the side stream waits for everything enqueued so far on the current stream."""
+    if not _Side.enabled:
         return None
-    main = torch.cuda.current_stream()
-    if _Side.stream is None or _Side.stream.device != main.device:
-        _Side.stream = torch.cuda.Stream(device=main.device)
-    side = _Side.stream
-    side.wait_stream(main)
-    for t in tensors:
-        if t is not None and t.is_cuda:
-            t.record_stream(side)
+    if _Side.stream is None:
+        _Side.stream = torch.cuda.Stream(device=_dev())
+        _Side.ptr = _Side.stream.cuda_stream
+    call("mms2ut_stream_wait", _Side.ptr, torch._C._cuda_getCurrentRawStream(_dev()))
+    _Side.keep.extend(tensors)
     _Side.used = True
-    return torch.cuda.stream(side)
+    return _SIDE_REGION
 
 
 def side_join():
-    """Make the current stream wait for all side-stream work (before consuming gradients)."""
+    """Join: the current stream waits for all side-stream work (before consuming gradients)."""
     if _Side.used and _Side.stream is not None:
-        torch.cuda.current_stream().wait_stream(_Side.stream)
+        call("mms2ut_stream_wait", torch._C._cuda_getCurrentRawStream(_dev()), _Side.ptr)
         _Side.used = False
+        _Side.keep.clear()
+
+
+def _workspace(key, numel, device, dtype=torch.float32):
+    """Scratch owned by the stream it is used on (side-stream serialised reuse; regrowth keeps the
+    old buffer alive until the next join)."""
+    if _Side.override:
+        buf = _Side.ws.get(key)
+        if buf is None or buf.numel() < numel:
+            if buf is not None:
+                _Side.keep.append(buf)
+            buf = torch.empty(max(numel, 1 << 20), dtype=dtype, device=device)
+            _Side.ws[key] = buf
+        return buf[:numel]
+    return torch.empty(numel, dtype=dtype, device=device)
 
 
 class _nullctx:
@@ -167,6 +215,9 @@ class _nullctx:
         return False
 
 
+_NULLCTX = _nullctx()
+
+
 def linear_wgrad(dy, x, dW, *, accumulate_f32=None, side=True):
     """dW[N,K] (fp16 view into the flat grad buffer) = dy[M,N]^T @ x[M,K] (split-K over M).
     With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead."""
@@ -174,10 +225,10 @@ def linear_wgrad(dy, x, dW, *, accumulate_f32=None, side=True):
     K = x.shape[1]
     assert dW is None or tuple(dW.shape) == (N, K)
     ctx = side_begin(dy, x) if side else None
-    with (ctx or _nullctx()):
+    with (ctx or _NULLCTX):
         tiles = -(-N // 128) * -(-K // 128)
         s = _splitk_for(tiles, M)
-        slabs = torch.empty(s, N, K, dtype=torch.float32, device=dy.device)
+        slabs = _workspace("slab", s * N * K, dy.device)
         gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
              epi=EPI_F32, splitk=s, sCsplit=N * K)
         if accumulate_f32 is not None:
@@ -194,9 +245,9 @@ def bias_grad(dy, db, accumulate=False, side=True):
     M, N = dy.shape
     L = _lib.load()
     ctx = side_begin(dy) if side else None
-    with (ctx or _nullctx()):
+    with (ctx or _NULLCTX):
         nparts = L.mms2ut_colsum_nparts(M)
-        part = torch.empty(nparts, N, dtype=torch.float32, device=dy.device)
+        part = _workspace("colsum", nparts * N, dy.device)
         call("mms2ut_colsum_f16", dy.data_ptr(), M, N, dy.stride(0), part.data_ptr(), nparts, _s())
         call("mms2ut_colsum_parts", part.data_ptr(), nparts, N, db.data_ptr(), int(accumulate), _s())
     return db

@@ -62,7 +62,7 @@ class GradAllReducer:
         if side is not None and K._Side.used:
             side.wait_stream(torch.cuda.current_stream())
             ctx = torch.cuda.stream(side)
-        with (ctx or K._nullctx()):
+        with (ctx or K._NULLCTX):
             while self.next < len(self.bounds) and self.bounds[self.next][1] <= upto:
                 a, b = self.bounds[self.next]
                 self.handles.append(dist.all_reduce(self.grad[a:b], op=dist.ReduceOp.SUM,

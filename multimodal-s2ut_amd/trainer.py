@@ -45,8 +45,9 @@ class Trainer:
         # logging / sample-size sync: [loss, nll, ntokens, nsentences] summed over ranks
         self.log[0] = loss.detach()
         self.log[1] = nll.detach()
-        self.log[2] = float(batch.ntokens)
-        self.log[3] = float(batch.nsentences)
+        # fill_ takes the scalar as a kernel argument (item assignment would be a blocking H2D copy)
+        self.log[2].fill_(float(batch.ntokens))
+        self.log[3].fill_(float(batch.nsentences))
         all_reduce_scalars(self.log)
         self.opt.step(self.log[2:3])
         return self.log
