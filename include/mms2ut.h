@@ -93,10 +93,14 @@ int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler);
 int mms2ut_layernorm_fwd(const mms2ut_half* x, const mms2ut_half* gamma, const mms2ut_half* beta,
                          mms2ut_half* y, float* mean, float* rstd, int64_t rows, int D, float eps,
                          hipStream_t stream);
-/* dx = LN'(dy) (+ dres if non-null); partial dgamma/dbeta sums -> part[nblk][2][D] (fp32)  */
+/* dx = LN'(dy) (+ dres if non-null); partial dgamma/dbeta sums -> part[nblk][2][D] (fp32).
+ * dx may be null (parameter grads only).  If dxd is non-null it also receives dropout(dx) with
+ * counters offset + row*D + col: the residual-branch dropout of the sublayer below, whose
+ * output-projection gradient consumes it (saves a separate dropout pass).                  */
 int mms2ut_layernorm_bwd(const mms2ut_half* dy, const mms2ut_half* x, const mms2ut_half* gamma,
                          const float* mean, const float* rstd, const mms2ut_half* dres,
-                         mms2ut_half* dx, float* part, int64_t rows, int D, hipStream_t stream);
+                         mms2ut_half* dx, float* part, int64_t rows, int D, mms2ut_half* dxd,
+                         float p, uint64_t seed, uint64_t offset, hipStream_t stream);
 int mms2ut_layernorm_bwd_parts(int64_t rows);
 /* column sums of fp32 partials [nparts][ncol] -> out (fp16), out += if accumulate */
 int mms2ut_colsum_parts(const float* part, int nparts, int ncol, mms2ut_half* out, int accumulate,

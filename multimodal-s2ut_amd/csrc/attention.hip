@@ -19,7 +19,8 @@
 
 namespace {
 
-constexpr int QB = 64, KB = 64;  // query rows / key rows per workgroup block
+constexpr int QB = 64, KB = 64;  // streamed query / key rows per LDS tile
+constexpr int ATTN_NW = 8;        // waves per block: each owns 16 rows of the block's own dimension
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -46,17 +47,50 @@ struct Tile {
   static constexpr int CH = HD / 8;  // 16-B chunks per row
 };
 
-// cooperative global -> LDS copy of `rows` rows (zero beyond `valid`)
-template <int HD>
-MMS_DEV void load_rows(h16* lds, const h16* g, long ld, int row0, int valid, int rows) {
-  constexpr int CH = Tile<HD>::CH, LD = Tile<HD>::LD;
-  for (int i = threadIdx.x; i < rows * CH; i += blockDim.x) {
-    const int r = i / CH, c = i % CH;
-    s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (row0 + r < valid) v = *reinterpret_cast<const s16x8*>(g + (long)(row0 + r) * ld + c * 8);
-    *reinterpret_cast<s16x8*>(lds + r * LD + c * 8) = v;
+// Register-staged prefetch of a pair of 64-row tiles (K/V or Q/dO): every global load of the
+// pair is issued at once and only stored to LDS at the top of the next iteration, so the load
+// latency hides behind the current tile's MFMAs (load-then-store per chunk serialised ~2 us of
+// latency per chunk round).  Optionally carries two fp32 per row (LSE, D) for the first 64 lanes.
+template <int HD, int NT>
+struct Pair64 {
+  static constexpr int CH = HD / 8, LD = Tile<HD>::LD;
+  static constexpr int N = (64 * CH + NT - 1) / NT;
+  s16x8 a[N], b[N];
+  float fl, fd;
+  MMS_DEV void load(const h16* ga, long lda, const h16* gb, long ldb, int row0, int valid) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const int i = threadIdx.x + n * NT;
+      const int r = i / CH, c = i % CH;
+      const s16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      a[n] = z;
+      b[n] = z;
+      if (i < 64 * CH && row0 + r < valid) {
+        a[n] = *reinterpret_cast<const s16x8*>(ga + (long)(row0 + r) * lda + c * 8);
+        b[n] = *reinterpret_cast<const s16x8*>(gb + (long)(row0 + r) * ldb + c * 8);
+      }
+    }
   }
-}
+  MMS_DEV void load_stats(const float* L, const float* D, long base, int row0, int valid) {
+    const int i = threadIdx.x;
+    fl = fd = 0.f;
+    if (i < 64 && row0 + i < valid) {
+      fl = L[base + row0 + i];
+      fd = D[base + row0 + i];
+    }
+  }
+  MMS_DEV void store(h16* la, h16* lb) const {
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const int i = threadIdx.x + n * NT;
+      const int r = i / CH, c = i % CH;
+      if (i < 64 * CH) {
+        *reinterpret_cast<s16x8*>(la + r * LD + c * 8) = a[n];
+        *reinterpret_cast<s16x8*>(lb + r * LD + c * 8) = b[n];
+      }
+    }
+  }
+};
 
 // A/B fragment with rows along LDS rows: lane l -> X[row0 + (l&15)][k0 + 8(l>>4) .. +7]
 template <int HD>
@@ -94,18 +128,19 @@ MMS_DEV float xsum16_32(float v) {
 }
 
 // ============================================================================ forward
-template <int HD>
-__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP P) {
+template <int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnP P) {
+  constexpr int OWN = 16 * NW;  // query rows owned by the block (16 per wave)
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
   __shared__ __attribute__((aligned(16))) h16 sK[KB * LD];
   __shared__ __attribute__((aligned(16))) h16 sV[KB * LD];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
-  const int qblk = blockIdx.x * QB;
+  const int qblk = blockIdx.x * OWN;
   const int q_own = qblk + w * 16 + (lane & 15);  // this lane's query row
   const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
   int kmax = klen;
-  if (P.causal) kmax = min(kmax, qblk + QB);
+  if (P.causal) kmax = min(kmax, qblk + OWN);
   const h16* Q = P.q + b * P.sqb + h * HD;
   const h16* K = P.k + b * P.skb + h * HD;
   const h16* V = P.v + b * P.svb + h * HD;
@@ -123,11 +158,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnP P) {
   float m = -INFINITY, l = 0.f;
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
+  Pair64<HD, 64 * NW> pf;
+  if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
   for (int kb = 0; kb < kmax; kb += KB) {
     __syncthreads();
-    load_rows<HD>(sK, K, P.ldk, kb, kmax, KB);
-    load_rows<HD>(sV, V, P.ldv, kb, kmax, KB);
+    pf.store(sK, sV);
     __syncthreads();
+    if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
     // S^T for 4 tiles of 16 keys: lane -> S[q_own][kb + 16t + 4g + r]
     f32x4 s[4];
 #pragma unroll
@@ -205,16 +242,41 @@ __global__ void attn_bwd_prep_kernel(AttnP P, int Z) {
   if (lane == 0) const_cast<float*>(P.Dd)[row] = s;
 }
 
-// ============================================================================ backward: dK, dV
+// One wave per token row covering every head: lane = h * (64/H) + j reads chunks j, j + 64/H, ...
+// (4 halfs each) of head h, then a (64/H)-lane segmented reduction.  Needs 64 % H == 0 and
+// (HD/4) % (64/H) == 0 (host check); 8-B loads, whole rows per wave instruction group.
 template <int HD>
-__global__ void __launch_bounds__(256) attn_bwd_kv_kernel(AttnP P) {
+__global__ void __launch_bounds__(256) attn_bwd_prep_rows_kernel(AttnP P, long nrows) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= nrows) return;
+  const int b = (int)(row / P.Tq), t = (int)(row % P.Tq);
+  const int LPH = 64 / P.H;               // lanes per head
+  const int h = lane / LPH, j = lane % LPH;
+  const h16* O = P.o + b * P.sob + (long)t * P.ldo + h * HD;
+  const h16* dO = P.dout + b * P.sdob + (long)t * P.lddo + h * HD;
+  float s = 0.f;
+  for (int c = j; c < HD / 4; c += LPH) {
+    const h16x4 o = *reinterpret_cast<const h16x4*>(O + 4 * c);
+    const h16x4 d = *reinterpret_cast<const h16x4*>(dO + 4 * c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += (float)o[e] * (float)d[e];
+  }
+  for (int off = LPH >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (j == 0) const_cast<float*>(P.Dd)[((long)b * P.H + h) * P.Tq + t] = s;
+}
+
+// ============================================================================ backward: dK, dV
+template <int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_kv_kernel(AttnP P) {
+  constexpr int OWN = 16 * NW;  // keys owned by the block
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
   __shared__ __attribute__((aligned(16))) h16 sQ[QB * LD];
   __shared__ __attribute__((aligned(16))) h16 sDO[QB * LD];
   __shared__ float sL[QB], sD[QB];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
-  const int kblk = blockIdx.x * KB;
+  const int kblk = blockIdx.x * OWN;
   const int key_own = kblk + w * 16 + (lane & 15);
   const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
   const h16* Q = P.q + b * P.sqb + h * HD;
@@ -239,16 +301,23 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(AttnP P) {
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
   const int q_begin = P.causal ? (kblk / QB) * QB : 0;
   if (kblk < klen) {
+    Pair64<HD, 64 * NW> pf;
+    if (q_begin < P.Tq) {
+      pf.load(Q, P.ldq, DO, P.lddo, q_begin, P.Tq);
+      pf.load_stats(P.lse, P.Dd, (long)z * P.Tq, q_begin, P.Tq);
+    }
     for (int qb = q_begin; qb < P.Tq; qb += QB) {
       __syncthreads();
-      load_rows<HD>(sQ, Q, P.ldq, qb, P.Tq, QB);
-      load_rows<HD>(sDO, DO, P.lddo, qb, P.Tq, QB);
-      for (int i = threadIdx.x; i < QB; i += blockDim.x) {
-        const bool ok = qb + i < P.Tq;
-        sL[i] = ok ? P.lse[(long)z * P.Tq + qb + i] : 0.f;
-        sD[i] = ok ? P.Dd[(long)z * P.Tq + qb + i] : 0.f;
+      pf.store(sQ, sDO);
+      if (threadIdx.x < QB) {
+        sL[threadIdx.x] = pf.fl;
+        sD[threadIdx.x] = pf.fd;
       }
       __syncthreads();
+      if (qb + QB < P.Tq) {
+        pf.load(Q, P.ldq, DO, P.lddo, qb + QB, P.Tq);
+        pf.load_stats(P.lse, P.Dd, (long)z * P.Tq, qb + QB, P.Tq);
+      }
       // per 16-query tile: S[q][key], dP'[q][key]; lane -> (q = qb + 16t + 4g + r, key_own)
       f32x4 pt[4], dst[4];
 #pragma unroll
@@ -297,18 +366,19 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(AttnP P) {
 }
 
 // ============================================================================ backward: dQ
-template <int HD>
-__global__ void __launch_bounds__(256) attn_bwd_q_kernel(AttnP P) {
+template <int HD, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd_q_kernel(AttnP P) {
+  constexpr int OWN = 16 * NW;
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
   __shared__ __attribute__((aligned(16))) h16 sK[KB * LD];
   __shared__ __attribute__((aligned(16))) h16 sV[KB * LD];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
-  const int qblk = blockIdx.x * QB;
+  const int qblk = blockIdx.x * OWN;
   const int q_own = qblk + w * 16 + (lane & 15);
   const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
   int kmax = klen;
-  if (P.causal) kmax = min(kmax, qblk + QB);
+  if (P.causal) kmax = min(kmax, qblk + OWN);
   const h16* Q = P.q + b * P.sqb + h * HD;
   const h16* K = P.k + b * P.skb + h * HD;
   const h16* V = P.v + b * P.svb + h * HD;
@@ -332,11 +402,13 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(AttnP P) {
   for (int i = 0; i < NDT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
+  Pair64<HD, 64 * NW> pf;
+  if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
   for (int kb = 0; kb < kmax; kb += KB) {
     __syncthreads();
-    load_rows<HD>(sK, K, P.ldk, kb, kmax, KB);
-    load_rows<HD>(sV, V, P.ldv, kb, kmax, KB);
+    pf.store(sK, sV);
     __syncthreads();
+    if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
     f32x4 ds[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -415,9 +487,10 @@ extern "C" int mms2ut_mha_varlen_fwd(const mms2ut_attn_args* a, hipStream_t s) {
   if (check_common(a)) return 1;
   MMS_REQUIRE(a->lse != nullptr, "attention fwd: lse buffer required");
   AttnP P = make_params(a);
-  dim3 grid((a->Tq + QB - 1) / QB, a->B * a->H);
+  // 8 waves own 128 query rows: for T <= 128 each (b, h) streams its K/V exactly once
+  dim3 grid((a->Tq + 16 * ATTN_NW - 1) / (16 * ATTN_NW), a->B * a->H);
   return pick_hd(a->hd, [&](auto HDc) {
-    hipLaunchKernelGGL((attn_fwd_kernel<decltype(HDc)::value>), grid, dim3(256), 0, s, P);
+    hipLaunchKernelGGL((attn_fwd_kernel<decltype(HDc)::value, ATTN_NW>), grid, dim3(64 * ATTN_NW), 0, s, P);
     return mms::check_launch("mha_varlen_fwd");
   });
 }
@@ -438,11 +511,20 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
   const int Z = a->B * a->H;
   return pick_hd(a->hd, [&](auto HDc) {
     constexpr int HD = decltype(HDc)::value;
-    hipLaunchKernelGGL((attn_bwd_prep_kernel<HD>), dim3(((long)Z * a->Tq + 3) / 4), dim3(256), 0, s, P, Z);
+    const bool rows_ok = a->H <= 64 && 64 % a->H == 0 && (HD / 4) % (64 / a->H) == 0 &&
+                         P.ldo % 4 == 0 && P.lddo % 4 == 0 && P.sob % 4 == 0 && P.sdob % 4 == 0 &&
+                         ((uintptr_t)P.o & 7) == 0 && ((uintptr_t)P.dout & 7) == 0;
+    if (rows_ok) {
+      const long nrows = (long)a->B * a->Tq;
+      hipLaunchKernelGGL((attn_bwd_prep_rows_kernel<HD>), dim3((nrows + 3) / 4), dim3(256), 0, s, P, nrows);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_prep_kernel<HD>), dim3(((long)Z * a->Tq + 3) / 4), dim3(256), 0, s, P, Z);
+    }
     if (int rc = mms::check_launch("mha_varlen_bwd_prep")) return rc;
-    hipLaunchKernelGGL((attn_bwd_kv_kernel<HD>), dim3((a->Tk + KB - 1) / KB, Z), dim3(256), 0, s, P);
+    constexpr int OWN = 16 * ATTN_NW;
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<HD, ATTN_NW>), dim3((a->Tk + OWN - 1) / OWN, Z), dim3(64 * ATTN_NW), 0, s, P);
     if (int rc = mms::check_launch("mha_varlen_bwd_kv")) return rc;
-    hipLaunchKernelGGL((attn_bwd_q_kernel<HD>), dim3((a->Tq + QB - 1) / QB, Z), dim3(256), 0, s, P);
+    hipLaunchKernelGGL((attn_bwd_q_kernel<HD, ATTN_NW>), dim3((a->Tq + OWN - 1) / OWN, Z), dim3(64 * ATTN_NW), 0, s, P);
     return mms::check_launch("mha_varlen_bwd_q");
   });
 }

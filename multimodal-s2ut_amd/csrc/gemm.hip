@@ -303,6 +303,27 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
 // operand ring, XOR-swizzled by row, then re-reads it row-major so a lane owns 8 consecutive
 // columns: every global load/store of the epilogue covers whole 128-B row segments instead of
 // 16 rows x 32 B.  Caller guarantees all waves are past their last operand read.
+// Block -> (z, tm, tn).  The grid is 1-D over tiles_m * tiles_n * nz.  Workgroups are dispatched
+// round-robin over the 8 XCDs, each with a private 4 MiB L2, so the linear id is first remapped
+// (bijectively) to give every XCD one contiguous range of the z-major tile space: a split-K
+// slice, or a batch entry, stays on one XCD.  Inside a z slice tiles go in groups of GROUP_M
+// tile-rows, column by column, so the ~64 blocks an XCD runs at once share 8 A row-panels and 8
+// B column-panels (~3 MiB at K = 768) instead of streaming the whole B operand per row.
+constexpr int GROUP_M = 8;
+MMS_DEV void tile_coords(int bid, int tiles_m, int tiles_n, int total, int& z, int& tm, int& tn) {
+  const int q = total / 8, r = total % 8, x = bid % 8;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  const int ntiles = tiles_m * tiles_n;
+  z = id / ntiles;
+  const int t = id % ntiles;
+  const int per_group = GROUP_M * tiles_n;
+  const int g = t / per_group, first_m = g * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int w = t % per_group;
+  tm = first_m + w % gsize;
+  tn = w / gsize;
+}
+
 template <int EPI>
 MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4], int bm, int bn,
                              int wm, int wn, int wid, int lane, void* Cz, const h16* auxz) {
@@ -328,17 +349,10 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
 }
 
 template <bool A_KC, bool B_KC, int EPI>
-__global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int tiles_n) {
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
-  const int ntiles = tiles_m * tiles_n;
-  // XCD-aware bijective remap of the linear block id (8 XCDs, round-robin dispatch)
-  int bid = blockIdx.x;
-  {
-    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-  }
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int z = blockIdx.y;
+  int z, tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const h16* A = P.A + z1 * P.sA1 + z2 * P.sA2;
@@ -443,16 +457,10 @@ MMS_DEV void wait_vm() {
 }
 
 template <bool A_KC, bool B_KC, int EPI, int STAGES>
-__global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n) {
+__global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
   __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
-  const int ntiles = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-  }
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int z = blockIdx.y;
+  int z, tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const int kbeg = zs * P.kchunk;
@@ -530,14 +538,144 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
 }
 
+// ------------------------------------------------------------------------------------------
+// BK = 32 variant: 16 KiB stages, a 4-deep ring in the same 64 KiB (2 blocks per CU), so two
+// k-tiles stay in flight across every barrier (counted vmcnt, raw s_barrier) instead of one.
+// K-contiguous images are [128 rows][32 k] (64-B rows, chunk ^ f(row), f = bits 1,2 of the
+// row: conflict-free for ds_read_b128's lane groups); MN-contiguous images are the BK = 64
+// layout's first 32 k-rows.
+// ------------------------------------------------------------------------------------------
+constexpr int BK32 = 32, T32_BYTES = 128 * 32 * 2, ST32 = 4;
+MMS_DEV int swz32(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1); }
+
+template <bool KC>
+MMS_DEV void dma_tile32(__amdgpu_buffer_rsrc_t rs, char* lds, long ld, int row0, int k0rel, int wid, int lane) {
+  // 8 wave-instructions per 8 KiB image: wave `wid` issues 2
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ins = wid * 2 + i;
+    int voff;
+    if (KC) {
+      const int row = ins * 16 + (lane >> 2), slot = lane & 3;
+      const int c = slot ^ swz32(row);
+      voff = (int)(((long)(row0 + row) * ld + k0rel + c * 8) * 2);
+    } else {
+      const int kr = ins * 4 + (lane >> 4), slot = lane & 15;
+      const int c = slot ^ swz_mn(kr);
+      voff = (int)(((long)(k0rel + kr) * ld + row0 + c * 8) * 2);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+template <bool KC>
+MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
+  if (KC) {
+    const int r = sub + (lane & 15);
+    const int c = lane >> 4;
+    s16x8 v = *reinterpret_cast<const s16x8*>(lds + r * 64 + ((c ^ swz32(r)) << 4));
+    return __builtin_bit_cast(h16x8, v);
+  }
+  return read_frag<false>(lds, sub, 0, lane);
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ void __launch_bounds__(NT, 2) gemm_dma32_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[ST32 * 2 * T32_BYTES];
+  int z, tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  const int zb = z / P.splitk, zs = z % P.splitk;
+  const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
+  const int kbeg = zs * P.kchunk;
+  const int kend = min(P.K, kbeg + P.kchunk);
+  const int bm = tm * BM, bn = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const h16* Ab = P.A + z1 * P.sA1 + z2 * P.sA2 + (A_KC ? 0 : (long)kbeg * P.lda);
+  const h16* Bb = P.B + z1 * P.sB1 + z2 * P.sB2 + (B_KC ? 0 : (long)kbeg * P.ldb);
+  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.lda + ((P.M + 7) & ~7)) * 2;
+  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.ldb + ((P.N + 7) & ~7)) * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)a_ext, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)b_ext, 0x00020000);
+#define SA32(s) (smem + (2 * (s)) * T32_BYTES)
+#define SB32(s) (smem + (2 * (s) + 1) * T32_BYTES)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + BK32 - 1) / BK32;
+  auto k_rel = [&](int t, bool kc) { return kc ? kbeg + t * BK32 : t * BK32; };
+#pragma unroll
+  for (int t = 0; t < ST32 - 1; ++t) {
+    if (t < nk) {
+      dma_tile32<A_KC>(ra, SA32(t), P.lda, bm, k_rel(t, A_KC), wid, lane);
+      dma_tile32<B_KC>(rb, SB32(t), P.ldb, bn, k_rel(t, B_KC), wid, lane);
+    }
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    // k-tile kt landed once only the younger (issued later) ones are outstanding: 4 per k-tile
+    const int younger = min(ST32 - 2, nk - 1 - kt);
+    if (younger >= 2) wait_vm<8>(); else if (younger == 1) wait_vm<4>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    const int nxt = kt + ST32 - 1;
+    if (nxt < nk) {
+      const int sb = nxt % ST32;
+      dma_tile32<A_KC>(ra, SA32(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
+      dma_tile32<B_KC>(rb, SB32(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
+    }
+    const int cur = kt % ST32;
+    h16x8 fa[4], fb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = read_frag32<A_KC>(SA32(cur), wm * 64 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = read_frag32<B_KC>(SB32(cur), wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+  }
+#undef SA32
+#undef SB32
+  char* Cz;
+  if (EPI == MMS_EPI_F32)
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
+  else
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
+  const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
+  __syncthreads();
+  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+}
+
+template <bool A_KC, bool B_KC>
+int launch_dma32(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
+  const int total = tm * tn * nz;
+  dim3 grid(total), block(NT);
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma32_kernel<A_KC, B_KC, E>), grid, block, 0, s, P, tm, tn, total); break;
+    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+#undef CASE
+    default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
+  }
+  return mms::check_launch("gemm_dma32");
+}
+
 template <bool A_KC, bool B_KC>
 int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
-  dim3 grid(tm * tn, nz), block(NT);
+  const char* bk = getenv("MMS2UT_GEMM_BK");
+  if (bk && bk[0] == '3') return launch_dma32<A_KC, B_KC>(epi, P, tm, tn, nz, s);
+  const int total = tm * tn * nz;
+  dim3 grid(total), block(NT);
   // 2 stages (64 KiB LDS, 2 blocks/CU) measured fastest on this step's shapes; 3 = 1 block/CU
   const char* st = getenv("MMS2UT_DMA_STAGES");
   if (!(st && st[0] == '3')) {
     switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 2>), grid, block, 0, s, P, tm, tn); break;
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 2>), grid, block, 0, s, P, tm, tn, total); break;
       CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
       CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
 #undef CASE
@@ -546,7 +684,7 @@ int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
     return mms::check_launch("gemm_dma2");
   }
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 3>), grid, block, 0, s, P, tm, tn); break;
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 3>), grid, block, 0, s, P, tm, tn, total); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
     CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
 #undef CASE
@@ -557,10 +695,11 @@ int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
 
 template <bool A_KC, bool B_KC>
 int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
-  dim3 grid(tm * tn, nz), block(NT);
+  const int total = tm * tn * nz;
+  dim3 grid(total), block(NT);
   const size_t lds = 0;
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, E>), grid, block, lds, s, P, tm, tn); break;
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, E>), grid, block, lds, s, P, tm, tn, total); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
     CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
 #undef CASE
@@ -671,7 +810,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   }
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
   const int nz = a->batch * splitk;
-  MMS_REQUIRE(nz <= 65535, "gemm: batch*splitk too large (%d)", nz);
+  MMS_REQUIRE((long)tm * tn * nz < (1L << 31), "gemm: too many tiles");
   hipStream_t s = stream;
   // LDS-DMA pipeline when every K-contiguous operand has whole 64-wide k-tiles and the operand
   // extents fit a buffer descriptor; otherwise the register-staged kernel (predicated tails)

@@ -70,17 +70,22 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, 
   }
 }
 
-constexpr int LN_BWD_ROWS = 16;  // rows per block (4 per wave): ~600 blocks for 10k rows
+constexpr int LN_BWD_ROWS = 16;  // rows per block (4 consecutive rows per wave): ~600 blocks for 10k rows
+constexpr int LN_RPW = 4;
 
+// All loads of a wave's 4 rows (x, dy, dres) are issued before any arithmetic, so ~36 8-B loads
+// per lane are in flight at once (the row-at-a-time loop was latency-bound at ~25 % of HBM BW).
 template <int CPL>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy, const h16* __restrict__ x,
                                                      const h16* __restrict__ g, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const h16* __restrict__ dres,
                                                      h16* __restrict__ dx, float* __restrict__ part,
-                                                     long rows, int D) {
+                                                     long rows, int D, h16* __restrict__ dxd, float p,
+                                                     uint32_t thresh, uint64_t seed, uint64_t offset) {
   __shared__ float red[4][2][CPL * 256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = D >> 2;
+  const float dscale = thresh ? 1.f / (1.f - p) : 1.f;
   float dg[CPL][4], db[CPL][4], gam[CPL][4];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
@@ -93,46 +98,72 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy,
       for (int e = 0; e < 4; ++e) gam[c][e] = (float)gg[e];
     }
   }
-  const long r0 = (long)blockIdx.x * LN_BWD_ROWS;
-  for (int rr = w; rr < LN_BWD_ROWS; rr += 4) {
-    const long row = r0 + rr;
-    if (row >= rows) break;
-    const float mu = mean[row], rs = rstd[row];
-    float xh[CPL][4], gd[CPL][4];
-    float s1 = 0.f, s2 = 0.f;
+  const long rb = (long)blockIdx.x * LN_BWD_ROWS + w * LN_RPW;
+  h16x4 xv[LN_RPW][CPL], dv[LN_RPW][CPL], rv[LN_RPW][CPL];
+  float mu[LN_RPW], rs[LN_RPW];
+  const h16x4 z4 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+#pragma unroll
+  for (int rr = 0; rr < LN_RPW; ++rr) {
+    const long row = rb + rr;
+    const bool ok = row < rows;
+    mu[rr] = ok ? mean[row] : 0.f;
+    rs[rr] = ok ? rstd[row] : 0.f;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int ch = lane + c * 64;
-      if (ch < nch) {
-        h16x4 xv = ld4(x + row * D + ch * 4), dv = ld4(dy + row * D + ch * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          xh[c][e] = ((float)xv[e] - mu) * rs;
-          const float d = (float)dv[e];
-          gd[c][e] = d * gam[c][e];
-          s1 += gd[c][e] * xh[c][e];
-          s2 += gd[c][e];
-          dg[c][e] += d * xh[c][e];
-          db[c][e] += d;
-        }
-      }
+      const bool v = ok && ch < nch;
+      xv[rr][c] = v ? ld4(x + row * D + ch * 4) : z4;
+      dv[rr][c] = v ? ld4(dy + row * D + ch * 4) : z4;
+      rv[rr][c] = (v && dres && dx) ? ld4(dres + row * D + ch * 4) : z4;
     }
-    if (!dx) continue;  // parameter grads only (image_pre_norm: image features are leaves)
-    s1 = wave_sum(s1) / D;
-    s2 = wave_sum(s2) / D;
+  }
+  float s1[LN_RPW], s2[LN_RPW];
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const int ch = lane + c * 64;
-      if (ch < nch) {
-        float o[4];
+  for (int rr = 0; rr < LN_RPW; ++rr) {
+    s1[rr] = 0.f;
+    s2[rr] = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = rs * (gd[c][e] - xh[c][e] * s1 - s2);
-        if (dres) {
-          h16x4 rv = ld4(dres + row * D + ch * 4);
+    for (int c = 0; c < CPL; ++c)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] += (float)rv[e];
+      for (int e = 0; e < 4; ++e) {
+        const float xh = ((float)xv[rr][c][e] - mu[rr]) * rs[rr];
+        const float d = (float)dv[rr][c][e];
+        const float gd = d * gam[c][e];
+        s1[rr] += gd * xh;
+        s2[rr] += gd;
+        dg[c][e] += d * xh;
+        db[c][e] += d;
+      }
+  }
+  if (dx) {
+#pragma unroll
+    for (int rr = 0; rr < LN_RPW; ++rr) {
+      s1[rr] = wave_sum(s1[rr]) / D;
+      s2[rr] = wave_sum(s2[rr]) / D;
+    }
+#pragma unroll
+    for (int rr = 0; rr < LN_RPW; ++rr) {
+      const long row = rb + rr;
+      if (row >= rows) break;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nch) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float xh = ((float)xv[rr][c][e] - mu[rr]) * rs[rr];
+            o[e] = rs[rr] * ((float)dv[rr][c][e] * gam[c][e] - xh * s1[rr] - s2[rr]) + (float)rv[rr][c][e];
+          }
+          st4(dx + row * D + ch * 4, o[0], o[1], o[2], o[3]);
+          if (dxd) {
+            // the upstream sublayer's residual-branch dropout, replayed from its counters
+            bool k[4] = {true, true, true, true};
+            if (thresh) mms_keep4(seed, offset + (uint64_t)row * D + ch * 4, thresh, k);
+            st4(dxd + row * D + ch * 4, k[0] ? o[0] * dscale : 0.f, k[1] ? o[1] * dscale : 0.f,
+                k[2] ? o[2] * dscale : 0.f, k[3] ? o[3] * dscale : 0.f);
+          }
         }
-        st4(dx + row * D + ch * 4, o[0], o[1], o[2], o[3]);
       }
     }
   }
@@ -567,7 +598,11 @@ extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
 
 extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamma, const float* mean,
                                     const float* rstd, const h16* dres, h16* dx, float* part,
-                                    int64_t rows, int D, hipStream_t s) {
+                                    int64_t rows, int D, h16* dxd, float p, uint64_t seed,
+                                    uint64_t offset, hipStream_t s) {
+  MMS_REQUIRE(!dxd || dx, "layernorm_bwd: dxd needs dx");
+  MMS_REQUIRE(p < 1.f, "layernorm_bwd: p must be < 1");
+  const uint32_t thresh = mms_drop_thresh(p);
   MMS_REQUIRE(D % 4 == 0 && D <= 1024, "layernorm_bwd: D must be a multiple of 4 and <= 1024");
   if (rows == 0) return 0;
   const int nb = mms2ut_layernorm_bwd_parts(rows);
@@ -575,7 +610,7 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
     constexpr int CPL = decltype(C)::value;
     if constexpr (CPL <= 4) {
       hipLaunchKernelGGL((ln_bwd_kernel<CPL>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, rstd,
-                         dres, dx, part, (long)rows, D);
+                         dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset);
       return mms::check_launch("layernorm_bwd");
     } else {
       mms::set_error("layernorm_bwd: D too large");

@@ -4,6 +4,7 @@ Every function enqueues HIP kernels on PyTorch's current stream through libmms2u
 Tensors are fp16 (``torch.float16``) unless stated; shapes are checked before the call.
 """
 import math
+import os
 
 import torch
 
@@ -126,16 +127,17 @@ def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=Fa
 
 
 def _splitk_for(tiles, kred, slots=512):
-    """split-K count: fill the 512 resident-block slots (2 GEMM blocks per CU) in whole waves."""
-    best, best_eff = 1, 0.0
-    for s in range(1, 33):
-        if s > 1 and kred // s < 256:
-            break
-        blocks = tiles * s
-        eff = blocks / (-(-blocks // slots) * slots)
-        if eff > best_eff + 0.02:
-            best, best_eff = s, eff
-    return best
+    """split-K count for a weight gradient (reduction over kred token rows).  8 slices map one
+    slice to each XCD (tile_coords keeps a z slice on one XCD), so every XCD streams its own rows
+    of dy and x exactly once through its private L2; measured faster than filling the 512 block
+    slots with more, thinner slices (scripts/gemm_bench.py).  Fewer slices when rows are scarce or
+    the tile grid alone fills the chip."""
+    if tiles >= 2 * slots:
+        return 1
+    for s in (8, 4, 2):
+        if kred // s >= 512:
+            return s
+    return 1
 
 
 class _Side:
@@ -150,7 +152,8 @@ class _Side:
     lives in persistent per-stream workspaces (the side stream serialises its own reuse)."""
     stream = None      # torch.cuda.Stream (RCCL buckets are enqueued on it, parallel.py)
     ptr = 0
-    enabled = True
+    enabled = os.environ.get("MMS2UT_SIDE", "1") != "0"
+    wgrad_nosplit = os.environ.get("MMS2UT_WGRAD_SPLIT", "1") == "0"
     used = False
     override = 0
     keep = []
@@ -177,7 +180,7 @@ def side_begin(*tensors):
     if not _Side.enabled:
         return None
     if _Side.stream is None:
-        _Side.stream = torch.cuda.Stream(device=_dev())
+        _Side.stream = torch.cuda.Stream(device=_dev(), priority=100)
         _Side.ptr = _Side.stream.cuda_stream
     call("mms2ut_stream_wait", _Side.ptr, torch._C._cuda_getCurrentRawStream(_dev()))
     _Side.keep.extend(tensors)
@@ -227,6 +230,13 @@ def linear_wgrad(dy, x, dW, *, accumulate_f32=None, side=True):
     ctx = side_begin(dy, x) if side else None
     with (ctx or _NULLCTX):
         tiles = -(-N // 128) * -(-K // 128)
+        if ctx is not None and accumulate_f32 is None and _Side.wgrad_nosplit:
+            # On the side stream the weight gradient only has to finish before the optimizer: one
+            # block per output tile, fp16 straight into the flat gradient (no fp32 slabs, no
+            # reduction pass), leaving most CUs to the dgrad chain on the critical path.
+            gemm(dy, x, dW, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0),
+                 ldc=dW.stride(0), epi=EPI_F16)
+            return dW
         s = _splitk_for(tiles, M)
         slabs = _workspace("slab", s * N * K, dy.device)
         gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
@@ -265,16 +275,23 @@ def layernorm(x, g, b, eps=1e-5):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True):
-    """Returns dx (+dres). dgb: fp16 view of [dgamma | dbeta] (2*D contiguous)."""
+def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None):
+    """Returns dx (+dres). dgb: fp16 view of [dgamma | dbeta] (2*D contiguous).
+    emit=(p, (seed, offset)): also return dropout(dx) for the sublayer below -> (dx, dxd)."""
     R, D = x.shape
     L = _lib.load()
     nparts = L.mms2ut_layernorm_bwd_parts(R)
     part = torch.empty(nparts, 2 * D, dtype=torch.float32, device=x.device)
     dx = torch.empty_like(x) if want_dx else None
+    dxd, p, seed, off = None, 0.0, 0, 0
+    if emit is not None and emit[0] > 0:
+        p, (seed, off) = emit
+        dxd = torch.empty_like(x)
     call("mms2ut_layernorm_bwd", dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr(),
-         rstd.data_ptr(), _p(dres), _p(dx), part.data_ptr(), R, D, _s())
+         rstd.data_ptr(), _p(dres), _p(dx), part.data_ptr(), R, D, _p(dxd), float(p), seed, off, _s())
     call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), 0, _s())
+    if emit is not None:
+        return dx, (dxd if dxd is not None else dx)
     return dx
 
 # ============================================================================ attention

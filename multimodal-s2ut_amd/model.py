@@ -444,7 +444,11 @@ class MMS2UTModel:
         c.update(B=B, T=T, lens32=lens32, pd=pd, pa=pa, pact=pact)
         return x3, c
 
-    def enc_layer_bwd(self, l, c, dx3):
+    def enc_layer_bwd(self, l, c, dx3, dy2=None, emit=None):
+        """dx3: gradient of the layer output; dy2: dropout(dx3) with this layer's fc2-branch mask
+        when the LayerNorm backward above already produced it.  emit=(p, drop) makes this
+        layer's first LayerNorm backward also produce the masked gradient for the layer below.
+        Returns (dx, dx masked by emit or None)."""
         cfg = self.cfg
         p = f"encoder.transformer_layers.{l}"
         d, H = cfg["encoder_embed_dim"], cfg["encoder_attention_heads"]
@@ -452,7 +456,8 @@ class MMS2UTModel:
         B, T = c["B"], c["T"]
         pd, pa, pact = c["pd"], c["pa"], c["pact"]
         # fc2 / fc1
-        dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
+        if dy2 is None:
+            dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
         K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"))
         K.bias_grad(dy2, self.G(p + ".fc2.bias"))
         df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
@@ -460,11 +465,10 @@ class MMS2UTModel:
         K.bias_grad(df1, self.G(p + ".fc1.bias"))
         dh2 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
         del df1
-        dx2 = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".final_layer_norm.weight"), c["m2"], c["r2"],
-                              self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
-                              dres=dx3)
-        # out proj
-        dyo = K.dropout(dx2, pd, c["drop1"], out=torch.empty_like(dx2)) if pd > 0 else dx2
+        dx2, dyo = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".final_layer_norm.weight"), c["m2"], c["r2"],
+                                   self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
+                                   dres=dx3, emit=(pd, c["drop1"]))
+        # out proj (dyo = dropout(dx2) with the attention-branch mask, from the LN backward)
         K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"))
         K.bias_grad(dyo, self.G(p + ".self_attn.out_proj.bias"))
         dO = K.linear_dgrad(dyo, self.P(p + ".self_attn.out_proj.weight"))
@@ -477,10 +481,14 @@ class MMS2UTModel:
         K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
         K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
         dh1 = K.linear_dgrad(dqkv, Wqkv)
-        dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
-                             self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
-                             dres=dx2)
-        return dx
+        if emit is None:
+            dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
+                                 self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
+                                 dres=dx2)
+            return dx, None
+        return K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
+                               self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
+                               dres=dx2, emit=emit)
 
     # -------------------------------------------------------------- fusion (fuse_img_feat)
     def fusion_fwd(self, text, img, img_mask, B, Te):
@@ -690,15 +698,17 @@ class MMS2UTModel:
                       p=pd, drop=c["drop3"])
         return x4, c
 
-    def dec_layer_bwd(self, l, c, dx4, denc, enc):
-        """Returns dx; accumulates the cross-attention K/V dgrad into denc [B*Te, de]."""
+    def dec_layer_bwd(self, l, c, dx4, denc, enc, dy3=None, emit=None):
+        """Returns (dx, masked dx for the layer below or None); accumulates the cross-attention
+        K/V dgrad into denc [B*Te, de].  dy3/emit as enc_layer_bwd's dy2/emit."""
         cfg = self.cfg
         p = f"decoder.layers.{l}"
         d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
         hd = d // H
         B, Tt, Te = c["B"], c["Tt"], c["Te"]
         pd, pa, pact = c["pd"], c["pa"], c["pact"]
-        dy3 = K.dropout(dx4, pd, c["drop3"], out=torch.empty_like(dx4)) if pd > 0 else dx4
+        if dy3 is None:
+            dy3 = K.dropout(dx4, pd, c["drop3"], out=torch.empty_like(dx4)) if pd > 0 else dx4
         K.linear_wgrad(dy3, c["f1"], self.G(p + ".fc2.weight"))
         K.bias_grad(dy3, self.G(p + ".fc2.bias"))
         df1 = K.linear_dgrad(dy3, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
@@ -706,11 +716,10 @@ class MMS2UTModel:
         K.bias_grad(df1, self.G(p + ".fc1.bias"))
         dh3 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
         del df1
-        dx3 = K.layernorm_bwd(dh3, c["x3"], self.P(p + ".final_layer_norm.weight"), c["m3"], c["r3"],
-                              self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
-                              dres=dx4)
+        dx3, dy2 = K.layernorm_bwd(dh3, c["x3"], self.P(p + ".final_layer_norm.weight"), c["m3"], c["r3"],
+                                   self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
+                                   dres=dx4, emit=(pd, c["drop2"]))
         # encoder attention
-        dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
         K.linear_wgrad(dy2, c["cO"], self.G(p + ".encoder_attn.out_proj.weight"))
         K.bias_grad(dy2, self.G(p + ".encoder_attn.out_proj.bias"))
         dO2 = K.linear_dgrad(dy2, self.P(p + ".encoder_attn.out_proj.weight"))
@@ -727,11 +736,10 @@ class MMS2UTModel:
         K.linear_wgrad(dq, c["h2"], self.G(p + ".encoder_attn.q_proj.weight"))
         K.bias_grad(dq, self.G(p + ".encoder_attn.q_proj.bias"))
         dh2 = K.linear_dgrad(dq, self.P(p + ".encoder_attn.q_proj.weight"))
-        dx2 = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".encoder_attn_layer_norm.weight"), c["m2"], c["r2"],
-                              self.params.span(p + ".encoder_attn_layer_norm.weight", p + ".encoder_attn_layer_norm.bias", grad=True),
-                              dres=dx3)
+        dx2, dy1 = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".encoder_attn_layer_norm.weight"), c["m2"], c["r2"],
+                                   self.params.span(p + ".encoder_attn_layer_norm.weight", p + ".encoder_attn_layer_norm.bias", grad=True),
+                                   dres=dx3, emit=(pd, c["drop1"]))
         # self attention
-        dy1 = K.dropout(dx2, pd, c["drop1"], out=torch.empty_like(dx2)) if pd > 0 else dx2
         K.linear_wgrad(dy1, c["sO"], self.G(p + ".self_attn.out_proj.weight"))
         K.bias_grad(dy1, self.G(p + ".self_attn.out_proj.bias"))
         dO = K.linear_dgrad(dy1, self.P(p + ".self_attn.out_proj.weight"))
@@ -744,10 +752,14 @@ class MMS2UTModel:
         K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
         K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
         dh1 = K.linear_dgrad(dqkv, Wqkv)
-        dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
-                             self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
-                             dres=dx2)
-        return dx
+        if emit is None:
+            dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
+                                 self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
+                                 dres=dx2)
+            return dx, None
+        return K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
+                               self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
+                               dres=dx2, emit=emit)
 
     # -------------------------------------------------------------- full model
     def encoder_forward(self, batch):
@@ -801,12 +813,16 @@ class MMS2UTModel:
                                                                          "encoder.selective", "encoder.image"))]
         if last_fusion:
             self._ready(last_fusion[-1])
-        dx = K.layernorm_bwd(denc, ctx["lx"], self.P("encoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
-                             self.params.span("encoder.layer_norm.weight", "encoder.layer_norm.bias", grad=True))
+        layers = ctx["layers"]
+        L = self.cfg["encoder_layers"]
+        emit = lambda l: (layers[l]["pd"], layers[l]["drop2"]) if l >= 0 else None  # noqa: E731
+        dx, dmask = K.layernorm_bwd(denc, ctx["lx"], self.P("encoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
+                                    self.params.span("encoder.layer_norm.weight", "encoder.layer_norm.bias", grad=True),
+                                    emit=emit(L - 1))
         self._ready("encoder.layer_norm.bias")
-        for l in reversed(range(self.cfg["encoder_layers"])):
-            dx = self.enc_layer_bwd(l, ctx["layers"][l], dx)
-            ctx["layers"][l] = None
+        for l in reversed(range(L)):
+            dx, dmask = self.enc_layer_bwd(l, layers[l], dx, dy2=dmask, emit=emit(l - 1))
+            layers[l] = None
             self._ready(f"encoder.transformer_layers.{l}.self_attn_layer_norm.bias")
         scale, pd = ctx["emb"]
         dh = K.scale_dropout_bwd(dx, scale, pd, ctx["drop_emb"])
@@ -851,12 +867,16 @@ class MMS2UTModel:
         K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32, side=False)
         dxl = torch.empty(B * Tt, d, dtype=F16, device=E.device)
         K.gemm(dlogits, E, dxl, B * Tt, d, V, a_kc=True, b_kc=False, lda=ctx["Vp"], ldb=d, ldc=d)
-        dx = K.layernorm_bwd(dxl, ctx["lx"], self.P("decoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
-                             self.params.span("decoder.layer_norm.weight", "decoder.layer_norm.bias", grad=True))
+        layers = ctx["layers"]
+        L = cfg["decoder_layers"]
+        emit = lambda l: (layers[l]["pd"], layers[l]["drop3"]) if l >= 0 else None  # noqa: E731
+        dx, dmask = K.layernorm_bwd(dxl, ctx["lx"], self.P("decoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
+                                    self.params.span("decoder.layer_norm.weight", "decoder.layer_norm.bias", grad=True),
+                                    emit=emit(L - 1))
         self._ready("decoder.layer_norm.bias")
-        for l in reversed(range(cfg["decoder_layers"])):
-            dx = self.dec_layer_bwd(l, ctx["layers"][l], dx, denc, enc)
-            ctx["layers"][l] = None
+        for l in reversed(range(L)):
+            dx, dmask = self.dec_layer_bwd(l, layers[l], dx, denc, enc, dy3=dmask, emit=emit(l - 1))
+            layers[l] = None
             self._ready(f"decoder.layers.{l}.self_attn_layer_norm.bias")
         scale, pd = ctx["emb"]
         K.token_embed_bwd(ctx["tok"], dx, dE32, B, Tt, d, pad, scale, pd, ctx["drop_emb"])

@@ -7,8 +7,11 @@
 fairseq reference: Trainer.train_step (multiply_grads(world/sample_size) after DDP's averaging
 == SUM all-reduce then 1/sample_size), FP16Optimizer.clip_grad_norm(10), DynamicLossScaler.
 """
+import os
+
 import torch
 
+from . import kernels as K
 from . import runtime
 from .optim import FP16Adam
 from .parallel import GradAllReducer, all_reduce_scalars
@@ -25,8 +28,27 @@ class Trainer:
         self.reducer = GradAllReducer(model.params.grad, bucket_mb) if world_size > 1 else None
         self.world = world_size
         self.log = torch.zeros(4, dtype=torch.float32, device=model.params.flat.device)
+        # The step's critical path (forward, dgrad chain, optimizer) runs on a high-priority stream
+        # so the hardware dispatcher prefers its workgroups over the weight-gradient side stream's
+        # (lowest priority), which only fills the CUs the critical path leaves idle.
+        self.stream = None
+        if os.environ.get("MMS2UT_STREAM_PRIO", "1") != "0" and model.params.flat.is_cuda:
+            self.stream = torch.cuda.Stream(device=model.params.flat.device, priority=-100)
+            if K._Side.stream is None:
+                K._Side.stream = torch.cuda.Stream(device=model.params.flat.device, priority=100)
+                K._Side.ptr = K._Side.stream.cuda_stream
 
     def train_step(self, batch):
+        if self.stream is None:
+            return self._train_step(batch)
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            log = self._train_step(batch)
+        cur.wait_stream(self.stream)
+        return log
+
+    def _train_step(self, batch):
         cfg = self.cfg
         m = self.model
         m.train()

@@ -19,7 +19,10 @@ SHAPES = [  # name, M, N, K, a_kc, b_kc, splitk
     ("fc2 dgrad", M, 3072, 768, True, False, 1),
     ("fc1 dgrad", M, 768, 3072, True, False, 1),
     ("wgrad 3072x768", 3072, 768, M, False, False, 4),
+    ("wgrad 3072x768 s8", 3072, 768, M, False, False, 8),
     ("wgrad 768x768", 768, 768, M, False, False, 15),
+    ("wgrad 768x768 s8", 768, 768, M, False, False, 8),
+    ("wgrad 768x768 s16", 768, 768, M, False, False, 16),
     ("conv2 fwd", 10000, 1536, 2560, True, True, 1),
     ("square 4096", 4096, 4096, 4096, True, True, 1),
     ("square 8192", 8192, 8192, 8192, True, True, 1),
@@ -38,8 +41,10 @@ def run(name, m, n, k, a_kc, b_kc, s, reps=20):
     res = {}
     for rnd in range(3):
         for path in ("reg", "dma", "dma2"):
+            # reg: register-staged; dma: 3-stage LDS-DMA; dma2: 2-stage LDS-DMA (default)
             os.environ["MMS2UT_GEMM_PATH"] = path
-            os.environ["MMS2UT_DMA_STAGES"] = "3" if path == "dma" else "2"
+            os.environ["MMS2UT_DMA_STAGES"] = "2"
+            os.environ["MMS2UT_GEMM_BK"] = "32" if path == "dma" else "64"
             for _ in range(2):
                 K.gemm(A, B, C, m, n, k, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=n,
                        epi=epi, splitk=s, sCsplit=m * n)
@@ -67,7 +72,7 @@ def run(name, m, n, k, a_kc, b_kc, s, reps=20):
     fl = 2.0 * m * n * k
     print(f"{name:18s} M={m:6d} N={n:5d} K={k:6d}  torch {res['torch']*1e3:7.1f}us {fl/res['torch']/1e9:6.0f} TF"
           f"  reg {res['reg']*1e3:7.1f}us {fl/res['reg']/1e9:6.0f} TF"
-          f"   dma {res['dma']*1e3:7.1f}us {fl/res['dma']/1e9:6.0f} TF"
+          f"   bk32 {res['dma']*1e3:7.1f}us {fl/res['dma']/1e9:6.0f} TF"
           f"   dma2 {res['dma2']*1e3:7.1f}us {fl/res['dma2']/1e9:6.0f} TF", flush=True)
     os.environ.pop("MMS2UT_GEMM_PATH", None)
 

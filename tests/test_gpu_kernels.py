@@ -132,6 +132,19 @@ def test_layernorm_fwd_bwd(K):
         assert rel(dx, xf.grad + dres.float()) < 3e-3
         assert rel(dgb[:D], gf.grad) < 3e-3
         assert rel(dgb[D:], bf.grad) < 3e-3
+        # fused residual-branch dropout of the gradient: dxd == dropout(dx) with the site's counters
+        dx2, dxd = K.layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=dres, emit=(0.1, (7, 4096)))
+        keep = K.dropout_mask(R * D, 0.1, 7, 4096, x.device).view(R, D).bool()
+        torch.cuda.synchronize()
+        assert torch.equal(dx2, dx)
+        ref = torch.where(keep, dx.float() / 0.9, torch.zeros_like(dx.float()))
+        assert (dxd.float() - ref).abs().max().item() <= 2e-3 * ref.abs().max().item() + 1e-3
+        assert torch.equal(dxd == 0, ~keep | (dx == 0))
+        # parameter-grad-only mode (image LN: no dx)
+        dgb2 = torch.empty_like(dgb)
+        assert K.layernorm_bwd(dy, x, g, mean, rstd, dgb2, want_dx=False) is None
+        torch.cuda.synchronize()
+        assert torch.equal(dgb2, dgb)
 
 
 @pytest.mark.parametrize("causal,extra", [(False, False), (True, False), (False, True)])
