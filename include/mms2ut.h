@@ -67,6 +67,11 @@ typedef struct mms2ut_gemm_args {
   float dropout_p;
   uint64_t seed, offset;
   int64_t ld_rng;
+  /* optional (epi = MMS_EPI_F32, a_kcontig = 0): fp32 A-row sums alpha*sum_k A(m,k) of split s
+   * -> rowsum[s*ld_rowsum + m].  The weight-gradient GEMM's A is dy^T, so these are the split-K
+   * partials of the bias gradient (replaces a separate column-sum pass over dy).             */
+  float* rowsum;
+  int64_t ld_rowsum;
 } mms2ut_gemm_args;
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);

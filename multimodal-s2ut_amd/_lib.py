@@ -32,6 +32,7 @@ class GemmArgs(C.Structure):
         ("dropout_p", f32),
         ("seed", u64), ("offset", u64),
         ("ld_rng", i64),
+        ("rowsum", vp), ("ld_rowsum", i64),
     ]
 
 

@@ -38,6 +38,7 @@ struct GemmP {
   h16* out2; long ldo2;
   float p; uint32_t thresh; uint64_t seed, offset; long ld_rng;
   int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity
+  float* rowsum; long ld_rowsum;  // RS kernels: split-K partial A-row sums (bias gradient)
 };
 
 MMS_DEV int swz_mn(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
@@ -456,7 +457,7 @@ MMS_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool A_KC, bool B_KC, int EPI, int STAGES>
+template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
 __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
   __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
   int z, tm, tn;
@@ -488,6 +489,17 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // RS: the first column of tiles also sums its A rows over k with one extra MFMA per A fragment
+  // (B = ones): lane l ends up with sum_k A(bm + wm*64 + 16i + (l & 15), k) in every element of rs[i]
+  f32x4 rs[4];
+  const bool do_rs = RS && tn == 0 && wn == 0;
+  if (RS) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  h16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (h16)1.f;
   const int nk = (kend - kbeg + BK - 1) / BK;
   // k offset of stage t relative to the descriptor base
   auto k_rel = [&](int t, bool kc) { return kc ? kbeg + t * BK : t * BK; };
@@ -522,10 +534,21 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      if (RS && do_rs) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, fa[i], rs[i], 0, 0, 0);
+      }
     }
   }
 #undef SA
 #undef SB
+  if (RS && do_rs && lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = bm + wm * 64 + i * 16 + lane;
+      if (m < P.M) P.rowsum[(long)zs * P.ld_rowsum + m] = rs[i][0] * P.alpha;
+    }
+  }
   char* Cz;
   if (EPI == MMS_EPI_F32)
     Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
@@ -651,6 +674,132 @@ __global__ void __launch_bounds__(NT, 2) gemm_dma32_kernel(GemmP P, int tiles_m,
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
 }
 
+// ------------------------------------------------------------------------------------------
+// 256x256 tile, 8 waves (2 x 4, each 128 rows x 64 cols = 8x4 MFMA tiles), one block per CU.
+// 32-deep k-slots in a 4-slot LDS-DMA ring (4 x 32 KiB = 128 KiB): slot ks+3 is issued right
+// after the barrier that opens slot ks, so three slots (12 of a wave's DMA instructions) stay in
+// flight across every barrier (counted vmcnt, raw s_barrier).  Per slot a wave reads 8 A + 4 B
+// fragments and issues 32 MFMAs.  Each 256-row operand image is two 128-row halves in the BK=32
+// layouts above.  Epilogue: two 64-row passes through the (idle) ring, 16 KiB per wave.
+// ------------------------------------------------------------------------------------------
+constexpr int BM2 = 256, BN2 = 256, NT2 = 512, SLOT2 = 2 * 2 * T32_BYTES;  // A 16 KiB + B 16 KiB
+constexpr int RING2 = 4;
+
+// one operand's 32-deep slot image: 16 wave-instructions (2 halves x 8); wave w issues w and w+8
+template <bool KC>
+MMS_DEV void dma_slot2(__amdgpu_buffer_rsrc_t rs, char* img, long ld, int row0, int k0rel, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ins = wid + 8 * i;
+    const int half = ins >> 3, hi = ins & 7;
+    const int r0 = row0 + half * 128;
+    int voff;
+    if (KC) {
+      const int row = hi * 16 + (lane >> 2), slot = lane & 3;
+      const int c = slot ^ swz32(row);
+      voff = (int)(((long)(r0 + row) * ld + k0rel + c * 8) * 2);
+    } else {
+      const int kr = hi * 4 + (lane >> 4), slot = lane & 15;
+      const int c = slot ^ swz_mn(kr);
+      voff = (int)(((long)(k0rel + kr) * ld + r0 + c * 8) * 2);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + half * T32_BYTES + hi * 1024), 16, voff, 0, 0, 0);
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[RING2 * SLOT2];
+  int z, tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  const int zb = z / P.splitk, zs = z % P.splitk;
+  const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
+  const int kbeg = zs * P.kchunk;
+  const int kend = min(P.K, kbeg + P.kchunk);
+  const int bm = tm * BM2, bn = tn * BN2;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const h16* Ab = P.A + z1 * P.sA1 + z2 * P.sA2 + (A_KC ? 0 : (long)kbeg * P.lda);
+  const h16* Bb = P.B + z1 * P.sB1 + z2 * P.sB2 + (B_KC ? 0 : (long)kbeg * P.ldb);
+  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.lda + ((P.M + 7) & ~7)) * 2;
+  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.ldb + ((P.N + 7) & ~7)) * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)a_ext, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)b_ext, 0x00020000);
+#define SLA(s) (smem + (s) * SLOT2)
+#define SLB(s) (smem + (s) * SLOT2 + 2 * T32_BYTES)
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + BK32 - 1) / BK32;
+  auto k_rel = [&](int t, bool kc) { return kc ? kbeg + t * BK32 : t * BK32; };
+#pragma unroll
+  for (int t = 0; t < RING2 - 1; ++t) {
+    if (t < nk) {
+      dma_slot2<A_KC>(ra, SLA(t), P.lda, bm, k_rel(t, A_KC), wid, lane);
+      dma_slot2<B_KC>(rb, SLB(t), P.ldb, bn, k_rel(t, B_KC), wid, lane);
+    }
+  }
+  // this wave's A rows live in half wr of the A image, its B columns in half wc>>1 at (wc&1)*64
+  const int a_half = wr * T32_BYTES, b_half = (wc >> 1) * T32_BYTES, b_sub = (wc & 1) * 64;
+  for (int ks = 0; ks < nk; ++ks) {
+    // slot ks landed once only the younger slots' DMAs (4 instructions each) are outstanding
+    const int younger = min(RING2 - 2, nk - 1 - ks);
+    if (younger >= 2) wait_vm<8>(); else if (younger == 1) wait_vm<4>(); else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int nxt = ks + RING2 - 1;
+    if (nxt < nk) {
+      const int sn = nxt % RING2;
+      dma_slot2<A_KC>(ra, SLA(sn), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
+      dma_slot2<B_KC>(rb, SLB(sn), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
+    }
+    const int cur = ks % RING2;
+    h16x8 fa[8], fb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = read_frag32<B_KC>(SLB(cur) + b_half, b_sub + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = read_frag32<A_KC>(SLA(cur) + a_half, i * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+  }
+#undef SLA
+#undef SLB
+  char* Cz;
+  if (EPI == MMS_EPI_F32)
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
+  else
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
+  const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
+  __syncthreads();
+  staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), bm + wr * 128, bn + wc * 64,
+                       0, 0, wid, lane, Cz, auxz);
+  __syncthreads();
+  staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[4]), bm + wr * 128 + 64, bn + wc * 64,
+                       0, 0, wid, lane, Cz, auxz);
+}
+
+template <bool A_KC, bool B_KC>
+int launch_256(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
+  const int total = tm * tn * nz;
+  dim3 grid(total), block(NT2);
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, E>), grid, block, 0, s, P, tm, tn, total); break;
+    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+#undef CASE
+    default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
+  }
+  return mms::check_launch("gemm256");
+}
+
 template <bool A_KC, bool B_KC>
 int launch_dma32(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   const int total = tm * tn * nz;
@@ -770,6 +919,15 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   return rc;
 }
 
+// 256x256-tile kernel or the 128x128 one.  MMS2UT_GEMM_TILE=256 / =128 forces a choice (A/B runs).
+static bool use_256(const mms2ut_gemm_args* a, int nz) {
+  const char* t = getenv("MMS2UT_GEMM_TILE");
+  if (t && t[0] == '2') return true;
+  if (t && t[0] == '1') return false;
+  (void)a; (void)nz;
+  return false;
+}
+
 static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   MMS_REQUIRE(a != nullptr, "gemm: null args");
   MMS_REQUIRE(a->M >= 0 && a->N >= 0 && a->K >= 0, "gemm: negative dims");
@@ -823,7 +981,24 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   const bool k_ok = (!a_kc || a->K % BK == 0) && (!b_kc || a->K % BK == 0);
   const long a_ext = a_kc ? (long)a->M * a->lda : (long)a->K * a->lda;
   const long b_ext = b_kc ? (long)a->N * a->ldb : (long)a->K * a->ldb;
-  if (!force_reg && k_ok && a_ext * 2 < (1L << 31) && b_ext * 2 < (1L << 31)) {
+  const bool dma_ok = k_ok && a_ext * 2 < (1L << 31) && b_ext * 2 < (1L << 31);
+  if (a->rowsum) {
+    MMS_REQUIRE(a->epi == MMS_EPI_F32 && !a_kc && !b_kc && a->batch == 1 && dma_ok,
+                "gemm: rowsum needs the fp32 slab epilogue, M/N-contiguous operands, batch 1");
+    MMS_REQUIRE(a->ld_rowsum >= a->M, "gemm: ld_rowsum < M");
+    P.rowsum = a->rowsum; P.ld_rowsum = a->ld_rowsum;
+    dim3 grid(tm * tn * nz), block(NT);
+    hipLaunchKernelGGL((gemm_dma_kernel<false, false, MMS_EPI_F32, 2, true>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
+    return mms::check_launch("gemm_dma_rs");
+  }
+  if (!force_reg && dma_ok) {
+    if (use_256(a, nz)) {
+      const int tm2 = (a->M + BM2 - 1) / BM2, tn2 = (a->N + BN2 - 1) / BN2;
+      if (a_kc && b_kc) return launch_256<true, true>(a->epi, P, tm2, tn2, nz, s);
+      if (a_kc && !b_kc) return launch_256<true, false>(a->epi, P, tm2, tn2, nz, s);
+      if (!a_kc && b_kc) return launch_256<false, true>(a->epi, P, tm2, tn2, nz, s);
+      return launch_256<false, false>(a->epi, P, tm2, tn2, nz, s);
+    }
     if (a_kc && b_kc) return launch_dma<true, true>(a->epi, P, tm, tn, nz, s);
     if (a_kc && !b_kc) return launch_dma<true, false>(a->epi, P, tm, tn, nz, s);
     if (!a_kc && b_kc) return launch_dma<false, true>(a->epi, P, tm, tn, nz, s);

@@ -61,7 +61,8 @@ class Dropout:
 
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv=1,
          sA=(0, 0), sB=(0, 0), sC=(0, 0), epi=EPI_F16, alpha=1.0, bias=None, aux=None, ldaux=0,
-         sX=(0, 0), out2=None, ldo2=0, p=0.0, seed=0, offset=0, ld_rng=0, splitk=1, sCsplit=0):
+         sX=(0, 0), out2=None, ldo2=0, p=0.0, seed=0, offset=0, ld_rng=0, splitk=1, sCsplit=0,
+         rowsum=None, ld_rowsum=0):
     a = GemmArgs()
     a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
     a.M, a.N, a.K = int(M), int(N), int(K)
@@ -79,6 +80,7 @@ def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv
     a.sX1, a.sX2 = sX
     a.out2, a.ldo2 = _p(out2), int(ldo2)
     a.dropout_p, a.seed, a.offset, a.ld_rng = float(p), int(seed), int(offset), int(ld_rng)
+    a.rowsum, a.ld_rowsum = _p(rowsum), int(ld_rowsum)
     call("mms2ut_gemm_f16", a, _s())
 
 
@@ -221,12 +223,17 @@ class _nullctx:
 _NULLCTX = _nullctx()
 
 
-def linear_wgrad(dy, x, dW, *, accumulate_f32=None, side=True):
+def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
     """dW[N,K] (fp16 view into the flat grad buffer) = dy[M,N]^T @ x[M,K] (split-K over M).
-    With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead."""
+    With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead.
+    With db (fp16 [N]) the bias gradient sum_rows dy comes out of the same GEMM: its first column
+    of tiles sums the dy rows it stages anyway (split-K partials, reduced with the slabs)."""
     M, N = dy.shape
     K = x.shape[1]
     assert dW is None or tuple(dW.shape) == (N, K)
+    if db is not None and (accumulate_f32 is not None or _Side.wgrad_nosplit or K % 64 or N % 4):
+        linear_wgrad(dy, x, dW, accumulate_f32=accumulate_f32, side=side)
+        return bias_grad(dy, db, side=side)
     ctx = side_begin(dy, x) if side else None
     with (ctx or _NULLCTX):
         tiles = -(-N // 128) * -(-K // 128)
@@ -239,8 +246,11 @@ def linear_wgrad(dy, x, dW, *, accumulate_f32=None, side=True):
             return dW
         s = _splitk_for(tiles, M)
         slabs = _workspace("slab", s * N * K, dy.device)
+        rs = _workspace("rowsum", s * N, dy.device) if db is not None else None
         gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
-             epi=EPI_F32, splitk=s, sCsplit=N * K)
+             epi=EPI_F32, splitk=s, sCsplit=N * K, rowsum=rs, ld_rowsum=N)
+        if db is not None:
+            call("mms2ut_splitk_reduce", rs.data_ptr(), s, N, 1, N, db.data_ptr(), N, 1, 1.0, _s())
         if accumulate_f32 is not None:
             call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, accumulate_f32.data_ptr(),
                  accumulate_f32.stride(0), 2, 1.0, _s())

@@ -398,8 +398,8 @@ class MMS2UTModel:
             L = ctx["layers"][i]
             W = self.P(f"encoder.subsample.conv_layers.{i}.weight")
             dy = K.glu_bwd(L["y"], dx, L["Cg"])
-            K.linear_wgrad(dy, L["col"], self.G(f"encoder.subsample.conv_layers.{i}.weight").view(W.shape[0], -1))
-            K.bias_grad(dy, self.G(f"encoder.subsample.conv_layers.{i}.bias"))
+            K.linear_wgrad(dy, L["col"], self.G(f"encoder.subsample.conv_layers.{i}.weight").view(W.shape[0], -1),
+                           db=self.G(f"encoder.subsample.conv_layers.{i}.bias"))
             if i > 0:
                 dcol = K.linear_dgrad(dy, W.view(W.shape[0], -1))
                 dx = K.col2im(dcol, B, L["Tin"], L["Tout"], L["C"], L["k"])
@@ -458,19 +458,19 @@ class MMS2UTModel:
         # fc2 / fc1
         if dy2 is None:
             dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
-        K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"))
-        K.bias_grad(dy2, self.G(p + ".fc2.bias"))
+        K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"),
+                       db=self.G(p + ".fc2.bias"))
         df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
-        K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"))
-        K.bias_grad(df1, self.G(p + ".fc1.bias"))
+        K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"),
+                       db=self.G(p + ".fc1.bias"))
         dh2 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
         del df1
         dx2, dyo = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".final_layer_norm.weight"), c["m2"], c["r2"],
                                    self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
                                    dres=dx3, emit=(pd, c["drop1"]))
         # out proj (dyo = dropout(dx2) with the attention-branch mask, from the LN backward)
-        K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"))
-        K.bias_grad(dyo, self.G(p + ".self_attn.out_proj.bias"))
+        K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"),
+                       db=self.G(p + ".self_attn.out_proj.bias"))
         dO = K.linear_dgrad(dyo, self.P(p + ".self_attn.out_proj.weight"))
         qkv = c["qkv"]
         dqkv = torch.empty_like(qkv)
@@ -478,8 +478,8 @@ class MMS2UTModel:
                       B, H, T, T, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
                       p=pa, drop=c["drop_attn"])
         Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
-        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
-        K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
+                       db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
         dh1 = K.linear_dgrad(dqkv, Wqkv)
         if emit is None:
             dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
@@ -594,16 +594,16 @@ class MMS2UTModel:
             Wo, gWo, gbo = self.P(pre + ".proj.weight"), self.G(pre + ".proj.weight"), self.G(pre + ".proj.bias")
         if cfg["use_selective_gate"]:
             dpre, dmerge = K.gate_bwd(dres, c["merge"], c["g"])
-            K.linear_wgrad(dpre, c["merge"], self.G("encoder.gate_denses.0.weight"))
-            K.bias_grad(dpre, self.G("encoder.gate_denses.0.bias"))
+            K.linear_wgrad(dpre, c["merge"], self.G("encoder.gate_denses.0.weight"),
+                           db=self.G("encoder.gate_denses.0.bias"))
             K.linear_dgrad(dpre, self.P("encoder.gate_denses.0.weight"), out=dmerge, accumulate=True)
             dOp = dmerge[:, :d]
             dtext = dmerge[:, d:]
         else:
             dOp = dres
             dtext = dres
-        K.linear_wgrad(dOp, c["O"], gWo)
-        K.bias_grad(dOp, gbo)
+        K.linear_wgrad(dOp, c["O"], gWo,
+                       db=gbo)
         dO = K.linear_dgrad(dOp, Wo)
         q, kv = c["q"], c["kv"]
         dq = torch.empty_like(q)
@@ -616,8 +616,8 @@ class MMS2UTModel:
             # on the main stream: the rows are zeroed right after (side-stream race otherwise)
             K.bias_grad(rows, self.params.span(pre + ".bias_k", pre + ".bias_v", grad=True), side=False)
             rows.zero_()
-        K.linear_wgrad(dkv, c["imgd"], gWkv)
-        K.bias_grad(dkv, gbkv)
+        K.linear_wgrad(dkv, c["imgd"], gWkv,
+                       db=gbkv)
         if cfg["image_pre_norm"]:
             dimgd = K.linear_dgrad(dkv, Wkv)
             if extra:
@@ -631,8 +631,8 @@ class MMS2UTModel:
                             self.params.span("encoder.image_pre_norm_module.weight",
                                              "encoder.image_pre_norm_module.bias", grad=True),
                             want_dx=False)
-        K.linear_wgrad(dq, c["textd"], gWq)
-        K.bias_grad(dq, gbq)
+        K.linear_wgrad(dq, c["textd"], gWq,
+                       db=gbq)
         dtext_total = torch.empty(B * Te, d, dtype=F16, device=dres.device)
         K.copy2d(dtext, dtext_total, B * Te, d)
         K.linear_dgrad(dq, Wq, out=dtext_total, accumulate=True)
@@ -709,19 +709,19 @@ class MMS2UTModel:
         pd, pa, pact = c["pd"], c["pa"], c["pact"]
         if dy3 is None:
             dy3 = K.dropout(dx4, pd, c["drop3"], out=torch.empty_like(dx4)) if pd > 0 else dx4
-        K.linear_wgrad(dy3, c["f1"], self.G(p + ".fc2.weight"))
-        K.bias_grad(dy3, self.G(p + ".fc2.bias"))
+        K.linear_wgrad(dy3, c["f1"], self.G(p + ".fc2.weight"),
+                       db=self.G(p + ".fc2.bias"))
         df1 = K.linear_dgrad(dy3, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
-        K.linear_wgrad(df1, c["h3"], self.G(p + ".fc1.weight"))
-        K.bias_grad(df1, self.G(p + ".fc1.bias"))
+        K.linear_wgrad(df1, c["h3"], self.G(p + ".fc1.weight"),
+                       db=self.G(p + ".fc1.bias"))
         dh3 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
         del df1
         dx3, dy2 = K.layernorm_bwd(dh3, c["x3"], self.P(p + ".final_layer_norm.weight"), c["m3"], c["r3"],
                                    self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
                                    dres=dx4, emit=(pd, c["drop2"]))
         # encoder attention
-        K.linear_wgrad(dy2, c["cO"], self.G(p + ".encoder_attn.out_proj.weight"))
-        K.bias_grad(dy2, self.G(p + ".encoder_attn.out_proj.bias"))
+        K.linear_wgrad(dy2, c["cO"], self.G(p + ".encoder_attn.out_proj.weight"),
+                       db=self.G(p + ".encoder_attn.out_proj.bias"))
         dO2 = K.linear_dgrad(dy2, self.P(p + ".encoder_attn.out_proj.weight"))
         q, kv = c["q"], c["kv"]
         dq = torch.empty_like(q)
@@ -730,18 +730,18 @@ class MMS2UTModel:
                       hd ** -0.5, dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pa, drop=c["drop_ca"])
         de = cfg["encoder_embed_dim"]
         Wkv = self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight").view(2 * d, de)
-        K.linear_wgrad(dkv, enc, self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight", grad=True).view(2 * d, de))
-        K.bias_grad(dkv, self.params.span(p + ".encoder_attn.k_proj.bias", p + ".encoder_attn.v_proj.bias", grad=True))
+        K.linear_wgrad(dkv, enc, self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight", grad=True).view(2 * d, de),
+                       db=self.params.span(p + ".encoder_attn.k_proj.bias", p + ".encoder_attn.v_proj.bias", grad=True))
         K.linear_dgrad(dkv, Wkv, out=denc, accumulate=True)
-        K.linear_wgrad(dq, c["h2"], self.G(p + ".encoder_attn.q_proj.weight"))
-        K.bias_grad(dq, self.G(p + ".encoder_attn.q_proj.bias"))
+        K.linear_wgrad(dq, c["h2"], self.G(p + ".encoder_attn.q_proj.weight"),
+                       db=self.G(p + ".encoder_attn.q_proj.bias"))
         dh2 = K.linear_dgrad(dq, self.P(p + ".encoder_attn.q_proj.weight"))
         dx2, dy1 = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".encoder_attn_layer_norm.weight"), c["m2"], c["r2"],
                                    self.params.span(p + ".encoder_attn_layer_norm.weight", p + ".encoder_attn_layer_norm.bias", grad=True),
                                    dres=dx3, emit=(pd, c["drop1"]))
         # self attention
-        K.linear_wgrad(dy1, c["sO"], self.G(p + ".self_attn.out_proj.weight"))
-        K.bias_grad(dy1, self.G(p + ".self_attn.out_proj.bias"))
+        K.linear_wgrad(dy1, c["sO"], self.G(p + ".self_attn.out_proj.weight"),
+                       db=self.G(p + ".self_attn.out_proj.bias"))
         dO = K.linear_dgrad(dy1, self.P(p + ".self_attn.out_proj.weight"))
         qkv = c["qkv"]
         dqkv = torch.empty_like(qkv)
@@ -749,8 +749,8 @@ class MMS2UTModel:
                       Tt, Tt, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pa,
                       drop=c["drop_sa"])
         Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
-        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d))
-        K.bias_grad(dqkv, self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
+                       db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
         dh1 = K.linear_dgrad(dqkv, Wqkv)
         if emit is None:
             dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],

@@ -301,3 +301,32 @@ def test_glu_im2col_col2im(K):
     yr.backward(dy.float())
     torch.cuda.synchronize()
     assert rel(dh, hf.grad) < 3e-3
+
+
+@pytest.mark.parametrize("M,N,K_", [(5000, 96, 256), (8704, 768, 768), (1000, 200, 64), (77, 2304, 128)])
+def test_wgrad_fused_bias(K, M, N, K_):
+    """dW and db from one GEMM launch (db = the A-row sums of the first tile column)."""
+    dy = torch.randn(M, N, device="cuda").half()
+    x = torch.randn(M, K_, device="cuda").half()
+    dW = torch.empty(N, K_, dtype=torch.float16, device="cuda")
+    db = torch.full((N,), 7.0, dtype=torch.float16, device="cuda")
+    K.linear_wgrad(dy, x, dW, db=db, side=False)
+    torch.cuda.synchronize()
+    assert rel(dW, dy.float().t() @ x.float()) < 2e-3
+    assert rel(db, dy.float().sum(0)) < 2e-3
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K_", [(300, 520, 192), (513, 96, 768), (64, 1004, 64)])
+def test_gemm_tile256(K, a_kc, b_kc, M, N, K_, monkeypatch):
+    """The 256x256-tile ring kernel on ragged shapes and every operand layout."""
+    monkeypatch.setenv("MMS2UT_GEMM_TILE", "256")
+    A = _mat(M, K_, seed=1) if a_kc else _mat(K_, M, ld=(M + 7) // 8 * 8, seed=1)
+    B = _mat(N, K_, seed=2) if b_kc else _mat(K_, N, ld=(N + 7) // 8 * 8, seed=2)
+    Af = A.float() if a_kc else A.float().t()
+    Bf = B.float() if b_kc else B.float().t()
+    ldc = (N + 7) // 8 * 8
+    C = torch.zeros(M, ldc, dtype=torch.float16, device="cuda")
+    K.gemm(A, B, C, M, N, K_, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=ldc)
+    torch.cuda.synchronize()
+    assert rel(C[:, :N], Af @ Bf.t()) < 2e-3
