@@ -786,10 +786,144 @@ __global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, i
                        0, 0, wid, lane, Cz, auxz);
 }
 
+// Software-pipelined form of the same tile: each 32-deep slot runs in two MFMA phases (rows
+// 0-63, then 64-127 of the wave's 128).  The second half's A fragments are read at the top of the
+// slot (behind phase A), and the NEXT slot's first-half A + B fragments are read right after the
+// slot's barrier (behind phase B), so no ds_read latency sits in front of an MFMA phase.  A
+// RING-slot ring; the barrier of slot s retires slot s+1 (read just after it) and slot s+RING-1
+// is issued behind it, leaving RING-3 slots in flight across the barrier.
+template <bool A_KC, bool B_KC, int EPI, int RING>
+__global__ void __launch_bounds__(NT2, 2) gemm256p_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[RING * SLOT2];
+  int z, tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  const int zb = z / P.splitk, zs = z % P.splitk;
+  const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
+  const int kbeg = zs * P.kchunk;
+  const int kend = min(P.K, kbeg + P.kchunk);
+  const int bm = tm * BM2, bn = tn * BN2;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const h16* Ab = P.A + z1 * P.sA1 + z2 * P.sA2 + (A_KC ? 0 : (long)kbeg * P.lda);
+  const h16* Bb = P.B + z1 * P.sB1 + z2 * P.sB2 + (B_KC ? 0 : (long)kbeg * P.ldb);
+  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.lda + ((P.M + 7) & ~7)) * 2;
+  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2
+                          : ((long)(kend - kbeg - 1) * P.ldb + ((P.N + 7) & ~7)) * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)a_ext, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)b_ext, 0x00020000);
+#define SLA(s) (smem + (s) * SLOT2)
+#define SLB(s) (smem + (s) * SLOT2 + 2 * T32_BYTES)
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (kend - kbeg + BK32 - 1) / BK32;
+  auto k_rel = [&](int t, bool kc) { return kc ? kbeg + t * BK32 : t * BK32; };
+#pragma unroll
+  for (int t = 0; t < RING - 1; ++t) {
+    if (t < nk) {
+      dma_slot2<A_KC>(ra, SLA(t), P.lda, bm, k_rel(t, A_KC), wid, lane);
+      dma_slot2<B_KC>(rb, SLB(t), P.ldb, bn, k_rel(t, B_KC), wid, lane);
+    }
+  }
+  const int a_half = wr * T32_BYTES, b_half = (wc >> 1) * T32_BYTES, b_sub = (wc & 1) * 64;
+  // counted wait for slot `want` given that slots up to `issued` have been issued (4 DMA each)
+  auto wait_slot = [&](int want, int issued) {
+    const int younger = min(issued, nk - 1) - want;  // < 0 past the last slot: drain
+    if (RING >= 5 && younger >= 3) wait_vm<12>();
+    else if (younger >= 2) wait_vm<8>();
+    else if (younger == 1) wait_vm<4>();
+    else wait_vm<0>();
+  };
+  // two register sets for the (first-half A, B) fragments, ping-ponged by a 2-way unrolled loop so
+  // the next slot's fragments are consumed where they land (no copies, no over-wide lgkm waits)
+  h16x8 faA[4], fbA[4], faB[4], fbB[4];
+  if (nk > 0) {
+    wait_slot(0, RING - 2);
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fbA[j] = read_frag32<B_KC>(SLB(0) + b_half, b_sub + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) faA[i] = read_frag32<A_KC>(SLA(0) + a_half, i * 16, lane);
+  }
+  auto slot = [&](int ks, const h16x8 (&fa_lo)[4], const h16x8 (&fb)[4], h16x8 (&fan)[4], h16x8 (&fbn)[4]) {
+    const int cur = ks % RING;
+    h16x8 fa_hi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa_hi[i] = read_frag32<A_KC>(SLA(cur) + a_half, 64 + i * 16, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa_lo[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // slot ks+1 must have landed; slots up to ks+RING-2 are issued at this point.  The wait,
+    // barrier and fragment reads run unconditionally (after the last slot they read a stale but
+    // valid slot): a conditional read would make hipcc merge lgkm counts across both paths and
+    // wait for the next slot's fragments in front of phase B.
+    wait_slot(ks + 1, ks + RING - 2);
+    __builtin_amdgcn_s_barrier();
+    const int nxt = ks + RING - 1;
+    if (nxt < nk) {
+      const int sn = nxt % RING;
+      dma_slot2<A_KC>(ra, SLA(sn), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
+      dma_slot2<B_KC>(rb, SLB(sn), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
+    }
+    const int c1 = (ks + 1) % RING;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fbn[j] = read_frag32<B_KC>(SLB(c1) + b_half, b_sub + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fan[i] = read_frag32<A_KC>(SLA(c1) + a_half, i * 16, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa_hi[i], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  for (int ks = 0; ks < nk; ks += 2) {
+    slot(ks, faA, fbA, faB, fbB);
+    if (ks + 1 < nk) slot(ks + 1, faB, fbB, faA, fbA);
+  }
+#undef SLA
+#undef SLB
+  char* Cz;
+  if (EPI == MMS_EPI_F32)
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
+  else
+    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
+  const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), bm + wr * 128, bn + wc * 64,
+                       0, 0, wid, lane, Cz, auxz);
+  __syncthreads();
+  staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[4]), bm + wr * 128 + 64, bn + wc * 64,
+                       0, 0, wid, lane, Cz, auxz);
+}
+
 template <bool A_KC, bool B_KC>
 int launch_256(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   const int total = tm * tn * nz;
   dim3 grid(total), block(NT2);
+  const char* v = getenv("MMS2UT_GEMM256");
+  const int var = v ? v[0] - '0' : 4;
+  if (var == 4 || var == 5) {
+    switch (epi) {
+#define CASE(E) case E: if (var == 4) hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, E, 4>), grid, block, 0, s, P, tm, tn, total); \
+                        else hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, E, 5>), grid, block, 0, s, P, tm, tn, total); break;
+      CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
+      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+#undef CASE
+      default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
+    }
+    return mms::check_launch("gemm256p");
+  }
   switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, E>), grid, block, 0, s, P, tm, tn, total); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
@@ -924,8 +1058,10 @@ static bool use_256(const mms2ut_gemm_args* a, int nz) {
   const char* t = getenv("MMS2UT_GEMM_TILE");
   if (t && t[0] == '2') return true;
   if (t && t[0] == '1') return false;
-  (void)a; (void)nz;
-  return false;
+  // measured (scripts/gemm_ab.py): the 256 tile wins only with a long K and enough tiles to keep
+  // one block per CU busy (subsampler conv2, large squares); the step's K = 768 projections and
+  // every N = 768 shape run faster on 128x128 tiles at two blocks per CU
+  return nz == 1 && a->K >= 2048 && a->N >= 1536 && a->M >= 4096;
 }
 
 static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
