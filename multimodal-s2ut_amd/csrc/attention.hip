@@ -14,6 +14,8 @@
 //
 // Backward: D = rowsum(dO*O) (prep kernel); dK/dV with keys stationary (kernel A), dQ with queries
 // stationary (kernel B); both recompute P from the saved log-sum-exp — no atomics, deterministic.
+#include <stdlib.h>
+
 #include "common.h"
 #include "../../include/mms2ut.h"
 
@@ -101,6 +103,17 @@ MMS_DEV h16x8 frag_rows(const h16* lds, int row0, int k0, int lane) {
 
 // transposed fragment over a 32-row step with the (4g.., 16+4g..) row permutation:
 // lane l (group g, i = l&15) -> X[row0 + 4g + j][col0 + i] (j<4), X[row0 + 16 + 4g + j-4][col0 + i]
+template <int LDX>
+MMS_DEV h16x8 frag_tr_ld(const h16* lds, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const h16* a1 = lds + (row0 + 4 * g + q) * LDX + col0 + 4 * pp;
+  const h16* a2 = a1 + 16 * LDX;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a2));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(h16x8, v);
+}
+
 template <int HD>
 MMS_DEV h16x8 frag_tr(const h16* lds, int row0, int col0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
@@ -447,6 +460,162 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_q_kernel(AttnP P) {
   }
 }
 
+
+// ============================================================================ backward: fused, short rows
+// One workgroup per (b, h) when Tq, Tk <= 128 (the step's typical encoder / decoder lengths): Q, K,
+// V, dO of the whole head sit in LDS, D = rowsum(dO*O) is formed while loading, and one launch
+// produces dK/dV (keys stationary, phase 2) and dQ (queries stationary, phase 3) from dS kept in
+// LDS as [key][query] — no prep launch, no second pass that re-reads Q/K/V/dO and recomputes P.
+constexpr int FT = 128;  // padded rows per head in the fused kernel
+
+template <int HD>
+__global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P) {
+  constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16, CH = HD / 8, LDS_T = FT + 8;
+  constexpr int NL = (FT * CH + 511) / 512;  // 16-B chunks per thread per operand
+  __shared__ __attribute__((aligned(16))) h16 sQ[FT * LD];
+  __shared__ __attribute__((aligned(16))) h16 sK[FT * LD];
+  __shared__ __attribute__((aligned(16))) h16 sV[FT * LD];
+  __shared__ __attribute__((aligned(16))) h16 sDO[FT * LD];
+  __shared__ __attribute__((aligned(16))) h16 sDS[FT * LDS_T];  // dS^T [key][query]
+  __shared__ float sL[FT], sD[FT];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const int z = blockIdx.x, b = z / P.H, h = z % P.H;
+  const int Tq = P.Tq;
+  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+  const h16* Q = P.q + b * P.sqb + h * HD;
+  const h16* K = P.k + b * P.skb + h * HD;
+  const h16* V = P.v + b * P.svb + h * HD;
+  const h16* O = P.o + b * P.sob + h * HD;
+  const h16* DO = P.dout + b * P.sdob + h * HD;
+  // ---- phase 1: every global load of the head issued at once, then LDS stores
+  if (tid < FT) sD[tid] = 0.f;
+  {
+    s16x8 rq[NL], rk[NL], rv[NL], rd[NL];
+    float dot[NL];
+    const s16x8 zz = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int n = 0; n < NL; ++n) {
+      const int i = tid + n * 512, r = i / CH, c = i % CH;
+      rq[n] = rk[n] = rv[n] = rd[n] = zz;
+      dot[n] = 0.f;
+      if (i < FT * CH) {
+        if (r < Tq) {
+          rq[n] = *reinterpret_cast<const s16x8*>(Q + (long)r * P.ldq + c * 8);
+          rd[n] = *reinterpret_cast<const s16x8*>(DO + (long)r * P.lddo + c * 8);
+          const h16x8 o8 = *reinterpret_cast<const h16x8*>(O + (long)r * P.ldo + c * 8);
+          const h16x8 d8 = __builtin_bit_cast(h16x8, rd[n]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dot[n] += (float)o8[e] * (float)d8[e];
+        }
+        if (r < klen) {
+          rk[n] = *reinterpret_cast<const s16x8*>(K + (long)r * P.ldk + c * 8);
+          rv[n] = *reinterpret_cast<const s16x8*>(V + (long)r * P.ldv + c * 8);
+        }
+      }
+    }
+    // zero dS^T (entries a causal / padded tile never writes are read as 0 by phase 3)
+    for (int i = tid; i < FT * LDS_T / 8; i += 512) reinterpret_cast<s16x8*>(sDS)[i] = zz;
+    __syncthreads();  // sD zeroed
+#pragma unroll
+    for (int n = 0; n < NL; ++n) {
+      const int i = tid + n * 512, r = i / CH, c = i % CH;
+      if (i < FT * CH) {
+        *reinterpret_cast<s16x8*>(sQ + r * LD + c * 8) = rq[n];
+        *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
+        *reinterpret_cast<s16x8*>(sV + r * LD + c * 8) = rv[n];
+        *reinterpret_cast<s16x8*>(sDO + r * LD + c * 8) = rd[n];
+        if (r < Tq) atomicAdd(&sD[r], dot[n]);
+      }
+    }
+    if (tid < FT) sL[tid] = tid < Tq ? P.lse[(long)z * Tq + tid] : 0.f;
+  }
+  __syncthreads();
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  // ---- phase 2: wave w owns keys 16w .. 16w+15: dV, dK and dS^T
+  {
+    const int kw0 = 16 * w, key_own = kw0 + (lane & 15);
+    f32x4 dk[NDT], dv[NDT];
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) { dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[i] = dk[i]; }
+    if (kw0 < klen) {
+      h16x8 kf[NKK], vf[NKK];
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        kf[kk] = frag_rows<HD>(sK, kw0, kk * 32, lane);
+        vf[kk] = frag_rows<HD>(sV, kw0, kk * 32, lane);
+      }
+      const int q_begin = P.causal ? (kw0 / 32) * 32 : 0;
+      for (int qc = q_begin; qc < Tq; qc += 32) {
+        f32x4 pt[2], dst[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int q0 = qc + 16 * tt;
+          f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = sc;
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) {
+            sc = mfma(frag_rows<HD>(sQ, q0, kk * 32, lane), kf[kk], sc);
+            dp = mfma(frag_rows<HD>(sDO, q0, kk * 32, lane), vf[kk], dp);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = q0 + 4 * g + r;
+            const bool ok = q < Tq && key_own < klen && (!P.causal || key_own <= q);
+            const float pr = ok ? __expf(sc[r] * P.scale - sL[q]) : 0.f;
+            float mk = dscale;
+            if (P.thresh && ok)
+              mk = mms_keep(P.seed, P.offset + ((uint64_t)z * Tq + q) * (uint64_t)P.Tk + key_own, P.thresh) ? dscale : 0.f;
+            pt[tt][r] = pr * mk;
+            dst[tt][r] = pr * (dp[r] * mk - sD[q]);
+          }
+          *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + q0 + 4 * g) =
+              h16x4{(h16)dst[tt][0], (h16)dst[tt][1], (h16)dst[tt][2], (h16)dst[tt][3]};
+        }
+        const h16x8 pf = pack8(pt[0], pt[1]);
+        const h16x8 sf = pack8(dst[0], dst[1]);
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) {
+          dv[i] = mfma(frag_tr<HD>(sDO, qc, 16 * i, lane), pf, dv[i]);
+          dk[i] = mfma(frag_tr<HD>(sQ, qc, 16 * i, lane), sf, dk[i]);
+        }
+      }
+    }
+    if (key_own < P.Tk) {
+      h16* DK = P.dk + b * P.sdkb + h * HD + (long)key_own * P.lddk;
+      h16* DV = P.dv + b * P.sdvb + h * HD + (long)key_own * P.lddv;
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) {
+        const f32x4 a = dk[i] * P.scale, c = dv[i];
+        *reinterpret_cast<h16x4*>(DK + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+        *reinterpret_cast<h16x4*>(DV + 16 * i + 4 * g) = h16x4{(h16)c[0], (h16)c[1], (h16)c[2], (h16)c[3]};
+      }
+    }
+  }
+  __syncthreads();
+  // ---- phase 3: wave w owns queries 16w .. 16w+15: dQ^T[d][q] = K^T[d][keys] dS^T[keys][q]
+  {
+    const int q0 = 16 * w, q_own = q0 + (lane & 15);
+    if (q0 < Tq) {
+      const int kend = P.causal ? min(klen, q0 + 16) : klen;
+      f32x4 dq[NDT];
+#pragma unroll
+      for (int i = 0; i < NDT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kc = 0; kc < kend; kc += 32) {
+        const h16x8 sf = frag_tr_ld<LDS_T>(sDS, kc, q0, lane);
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) dq[i] = mfma(frag_tr<HD>(sK, kc, 16 * i, lane), sf, dq[i]);
+      }
+      if (q_own < Tq) {
+        h16* DQ = P.dq + b * P.sdqb + h * HD + (long)q_own * P.lddq;
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) {
+          const f32x4 a = dq[i] * P.scale;
+          *reinterpret_cast<h16x4*>(DQ + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+        }
+      }
+    }
+  }
+}
+
 template <typename F>
 int pick_hd(int hd, F&& f) {
   switch (hd) {
@@ -509,6 +678,22 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
   P.dk = dk; P.lddk = lddk; P.sdkb = sdkb ? sdkb : (long)a->Tk * lddk;
   P.dv = dv; P.lddv = lddv; P.sdvb = sdvb ? sdvb : (long)a->Tk * lddv;
   const int Z = a->B * a->H;
+  const char* fe = getenv("MMS2UT_ATTN_FUSED");
+  const bool fused_ok = !(fe && fe[0] == '0') && a->Tq <= FT && a->Tk <= FT && a->hd <= 96 &&
+                        P.ldo % 8 == 0 && P.sob % 8 == 0 && ((uintptr_t)P.o & 15) == 0 &&
+                        P.lddo % 8 == 0 && P.sdob % 8 == 0 && ((uintptr_t)P.dout & 15) == 0;
+  if (fused_ok) {
+    return pick_hd(a->hd, [&](auto HDc) {
+      constexpr int HD = decltype(HDc)::value;
+      if constexpr (HD <= 96) {
+        hipLaunchKernelGGL((attn_bwd_fused_kernel<HD>), dim3(Z), dim3(512), 0, s, P);
+        return mms::check_launch("mha_varlen_bwd_fused");
+      } else {
+        mms::set_error("unreachable");
+        return 1;
+      }
+    });
+  }
   return pick_hd(a->hd, [&](auto HDc) {
     constexpr int HD = decltype(HDc)::value;
     const bool rows_ok = a->H <= 64 && 64 % a->H == 0 && (HD / 4) % (64 / a->H) == 0 &&

@@ -53,6 +53,10 @@ def case(B, T, H=8, d=768, p=0.1, causal=False):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # one case: B T p [causal]
+        case(int(sys.argv[1]), int(sys.argv[2]), p=float(sys.argv[3]),
+             causal=len(sys.argv) > 4 and sys.argv[4] == "1")
+        sys.exit(0)
     case(95, 106)
     case(95, 106, p=0.0)
     case(95, 128, p=0.0)

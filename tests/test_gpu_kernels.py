@@ -212,8 +212,12 @@ def _attn_ref(q, k, v, lens, causal, scale, mask=None):
 @pytest.mark.parametrize("causal,Tq,Tk,lens,p", [
     (False, 70, 90, [90, 50, 7], 0.0), (True, 70, 70, [70, 41, 3], 0.0),
     (False, 130, 130, [130, 129, 65], 0.0), (True, 150, 150, [150, 100, 1], 0.25),
-    (False, 33, 200, [200, 64, 63], 0.1)])
-def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p):
+    (False, 33, 200, [200, 64, 63], 0.1), (True, 128, 128, [128, 77, 5], 0.1),
+    (False, 100, 128, [128, 100, 1], 0.2), (False, 1, 17, [17, 9, 1], 0.0)])
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p, fused, monkeypatch):
+    """fused=1: Tq, Tk <= 128 take the one-launch backward; fused=0 forces the three-kernel one."""
+    monkeypatch.setenv("MMS2UT_ATTN_FUSED", fused)
     B, H = 3, 2
     d = H * hd
     g = torch.Generator(device="cuda").manual_seed(5)
