@@ -86,6 +86,12 @@ int mms2ut_profile_end(float* total_ms, int* launches, double* flops);
  * mode bit0: fp16 output (else fp32); bit1: accumulate into out (else overwrite)            */
 int mms2ut_splitk_reduce(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
                          void* out, int64_t ldo, int mode, float alpha, hipStream_t stream);
+/* the weight-gradient epilogue in one launch: fp16 dW = sum of `nsplit` fp32 slabs [rows, cols]
+ * (row stride ldo) and fp16 db[rows] = sum of the GEMM's rowsum partials rs_slabs[nsplit][rows].
+ * rows, cols, ldo multiples of 4.  Replaces the bias column-sum of dy (fairseq Linear.bias.grad). */
+int mms2ut_splitk_reduce_bias(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                              mms2ut_half* out, int64_t ldo, const float* rs_slabs,
+                              mms2ut_half* rs_out, hipStream_t stream);
 
 /* `waiter` waits for all work enqueued on `signaler` so far (event record + stream wait).
  * Forks/joins the weight-gradient side stream (the reference's DDP/autograd stream overlap). */

@@ -31,7 +31,7 @@ extern "C" int mms2ut_version(void) { return 1; }
 namespace {
 __global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int nsplit, long slab,
                                      int rows, int cols, void* out, long ldo, int out_f16,
-                                     float alpha) {
+                                     float alpha, const float* __restrict__ rs_slabs, h16* __restrict__ rs_out) {
   const long n4 = (long)rows * (cols / 4);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const long r = i / (cols / 4), c = (i % (cols / 4)) * 4;
@@ -50,6 +50,16 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int nsplit
       *o = s;
     }
   }
+  // optional tail: the bias-gradient partials [nsplit][rows] -> rs_out fp16 (overwrite)
+  if (rs_slabs) {
+    const long m4 = rows / 4;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < m4; i += (long)gridDim.x * blockDim.x) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < nsplit; ++k) s += *reinterpret_cast<const f32x4*>(rs_slabs + (long)k * rows + 4 * i);
+      s *= alpha;
+      *reinterpret_cast<h16x4*>(rs_out + 4 * i) = h16x4{(h16)s[0], (h16)s[1], (h16)s[2], (h16)s[3]};
+    }
+  }
 }
 }  // namespace
 
@@ -62,8 +72,23 @@ extern "C" int mms2ut_splitk_reduce(const float* slabs, int nsplit, int64_t slab
   int grid = (int)((n4 + 255) / 256);
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, stream, slabs, nsplit, slab,
-                     rows, cols, out, ldo, out_f16, alpha);
+                     rows, cols, out, ldo, out_f16, alpha, (const float*)nullptr, (h16*)nullptr);
   return mms::check_launch("splitk_reduce");
+}
+
+extern "C" int mms2ut_splitk_reduce_bias(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                                         mms2ut_half* out, int64_t ldo, const float* rs_slabs,
+                                         mms2ut_half* rs_out, hipStream_t stream) {
+  MMS_REQUIRE(cols % 4 == 0 && ldo % 4 == 0 && rows % 4 == 0,
+              "splitk_reduce_bias: rows/cols/ldo must be multiples of 4");
+  MMS_REQUIRE(rs_slabs && rs_out && ((uintptr_t)rs_out & 7) == 0, "splitk_reduce_bias: bad bias buffers");
+  const long n4 = (long)rows * (cols / 4);
+  if (n4 == 0) return 0;
+  int grid = (int)((n4 + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, stream, slabs, nsplit, slab,
+                     rows, cols, (void*)out, ldo, 1, 1.f, rs_slabs, rs_out);
+  return mms::check_launch("splitk_reduce_bias");
 }
 
 // ------------------------------------------------------------------------------------------

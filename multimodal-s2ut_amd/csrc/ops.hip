@@ -2,6 +2,8 @@
 // LayerNorm parameter grads), masked attention softmax fwd/bwd with counter-RNG dropout,
 // embeddings, GLU, im2col/col2im, the fusion-gate backward and small elementwise helpers.
 // All HBM-bound: one wave per row for row ops, 8-byte (4 x fp16) vector accesses, fp32 math.
+#include <stdlib.h>
+
 #include "common.h"
 #include "../../include/mms2ut.h"
 
@@ -182,6 +184,129 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy,
     const int c = ch / 64, ln = ch % 64;
     const int idx = (c * 64 + ln) * 4 + e;
     out[i] = red[0][which][idx] + red[1][which][idx] + red[2][which][idx] + red[3][which][idx];
+  }
+}
+
+// LayerNorm backward for D % 256 == 0 (the step's D = 768): a half-wave per row so every global
+// access is a 16-B lane access (whole 512-B row segments per half-wave instruction).  Same row
+// blocking as ln_bwd_kernel (16 rows per block, part[block][2][D]); wave w takes row pairs w and
+// w + 4, all their loads (x, dy, dres) in flight at once.  dgamma / dbeta column partials are
+// folded across the two half-waves by a lane-32 shuffle and across the 4 waves through LDS.
+template <int C8>  // 16-B chunks per lane per row = D / 256
+__global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ dy, const h16* __restrict__ x,
+                                                       const h16* __restrict__ g, const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd, const h16* __restrict__ dres,
+                                                       h16* __restrict__ dx, float* __restrict__ part,
+                                                       long rows, int D, h16* __restrict__ dxd, float p,
+                                                       uint32_t thresh, uint64_t seed, uint64_t offset) {
+  __shared__ __attribute__((aligned(16))) float red[4][2][C8 * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
+  const float dscale = thresh ? 1.f / (1.f - p) : 1.f;
+  const float invD = 1.f / D;
+  float gam[C8][8], dg[C8][8], db[C8][8];
+#pragma unroll
+  for (int c = 0; c < C8; ++c) {
+    const h16x8 gg = *reinterpret_cast<const h16x8*>(g + (hl + 32 * c) * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { gam[c][e] = (float)gg[e]; dg[c][e] = 0.f; db[c][e] = 0.f; }
+  }
+  const long rb = (long)blockIdx.x * LN_BWD_ROWS;
+  const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+  h16x8 xv[2][C8], dv[2][C8], rv[2][C8];
+  float mu[2], rs[2];
+  long row[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    row[k] = rb + 2 * (w + 4 * k) + half;
+    const bool ok = row[k] < rows;
+    mu[k] = ok ? mean[row[k]] : 0.f;
+    rs[k] = ok ? rstd[row[k]] : 0.f;
+#pragma unroll
+    for (int c = 0; c < C8; ++c) {
+      const long off = row[k] * D + (hl + 32 * c) * 8;
+      xv[k][c] = ok ? *reinterpret_cast<const h16x8*>(x + off) : z8;
+      dv[k][c] = ok ? *reinterpret_cast<const h16x8*>(dy + off) : z8;
+      rv[k][c] = (ok && dres && dx) ? *reinterpret_cast<const h16x8*>(dres + off) : z8;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < C8; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
+        const float d = (float)dv[k][c][e];
+        const float gd = d * gam[c][e];
+        s1 += gd * xh;
+        s2 += gd;
+        dg[c][e] += d * xh;
+        db[c][e] += d;
+      }
+    if (!dx) continue;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    s1 *= invD;
+    s2 *= invD;
+    if (row[k] >= rows) continue;
+#pragma unroll
+    for (int c = 0; c < C8; ++c) {
+      const long off = row[k] * D + (hl + 32 * c) * 8;
+      float o8[8];
+      h16x8 ov;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
+        o8[e] = rs[k] * ((float)dv[k][c][e] * gam[c][e] - xh * s1 - s2) + (float)rv[k][c][e];
+        ov[e] = (h16)o8[e];
+      }
+      *reinterpret_cast<h16x8*>(dx + off) = ov;
+      if (dxd) {
+        bool k0[4] = {true, true, true, true}, k1[4] = {true, true, true, true};
+        if (thresh) {
+          mms_keep4(seed, offset + (uint64_t)off, thresh, k0);
+          mms_keep4(seed, offset + (uint64_t)off + 4, thresh, k1);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ov[e] = (h16)(k0[e] ? o8[e] * dscale : 0.f);
+          ov[e + 4] = (h16)(k1[e] ? o8[e + 4] * dscale : 0.f);
+        }
+        *reinterpret_cast<h16x8*>(dxd + off) = ov;
+      }
+    }
+  }
+  // fold the two half-waves (same columns), then the 4 waves through LDS
+#pragma unroll
+  for (int c = 0; c < C8; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dg[c][e] += __shfl_xor(dg[c][e], 32, 64);
+      db[c][e] += __shfl_xor(db[c][e], 32, 64);
+    }
+  if (half == 0) {
+#pragma unroll
+    for (int c = 0; c < C8; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        *reinterpret_cast<f32x4*>(&red[w][0][(hl + 32 * c) * 8 + 4 * h]) =
+            f32x4{dg[c][4 * h], dg[c][4 * h + 1], dg[c][4 * h + 2], dg[c][4 * h + 3]};
+        *reinterpret_cast<f32x4*>(&red[w][1][(hl + 32 * c) * 8 + 4 * h]) =
+            f32x4{db[c][4 * h], db[c][4 * h + 1], db[c][4 * h + 2], db[c][4 * h + 3]};
+      }
+  }
+  __syncthreads();
+  float* out = part + (long)blockIdx.x * 2 * D;
+  for (int i = threadIdx.x; i < 2 * D / 4; i += 256) {
+    const int which = (4 * i) / D, j = 4 * i - which * D;
+    f32x4 t = *reinterpret_cast<const f32x4*>(&red[0][which][j]);
+#pragma unroll
+    for (int v = 1; v < 4; ++v) t += *reinterpret_cast<const f32x4*>(&red[v][which][j]);
+    *reinterpret_cast<f32x4*>(out + 4 * i) = t;
   }
 }
 
@@ -606,6 +731,16 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
   MMS_REQUIRE(D % 4 == 0 && D <= 1024, "layernorm_bwd: D must be a multiple of 4 and <= 1024");
   if (rows == 0) return 0;
   const int nb = mms2ut_layernorm_bwd_parts(rows);
+  const char* e16 = getenv("MMS2UT_LN16");
+  if (D % 256 == 0 && D <= 1024 && !(e16 && e16[0] == '0')) {
+    switch (D / 256) {
+#define CASE(C) case C: hipLaunchKernelGGL((ln_bwd16_kernel<C>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, rstd, \
+                                          dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset); break;
+      CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+    }
+    return mms::check_launch("layernorm_bwd16");
+  }
   return pick_cpl(D / 4, [&](auto C) {
     constexpr int CPL = decltype(C)::value;
     if constexpr (CPL <= 4) {

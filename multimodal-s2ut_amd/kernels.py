@@ -249,6 +249,10 @@ def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
         rs = _workspace("rowsum", s * N, dy.device) if db is not None else None
         gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
              epi=EPI_F32, splitk=s, sCsplit=N * K, rowsum=rs, ld_rowsum=N)
+        if db is not None and accumulate_f32 is None and N % 4 == 0:
+            call("mms2ut_splitk_reduce_bias", slabs.data_ptr(), s, N * K, N, K, dW.data_ptr(), dW.stride(0),
+                 rs.data_ptr(), db.data_ptr(), _s())
+            return dW
         if db is not None:
             call("mms2ut_splitk_reduce", rs.data_ptr(), s, N, 1, N, db.data_ptr(), N, 1, 1.0, _s())
         if accumulate_f32 is not None:

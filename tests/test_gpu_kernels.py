@@ -113,8 +113,11 @@ def test_wgrad_splitk(K):
     assert rel(dW, dy.float().t() @ x.float()) < 2e-3
 
 
-def test_layernorm_fwd_bwd(K):
-    for R, D in ((1000, 768), (37, 256), (5, 96)):
+@pytest.mark.parametrize("ln16", ["1", "0"])
+def test_layernorm_fwd_bwd(K, ln16, monkeypatch):
+    """ln16=1: D % 256 == 0 takes the 16-B half-wave-per-row backward; 0 forces the 8-B one."""
+    monkeypatch.setenv("MMS2UT_LN16", ln16)
+    for R, D in ((1000, 768), (37, 256), (5, 96), (3, 1024)):
         x = (3 * torch.randn(R, D, device="cuda") + 1).half()
         g = (1 + 0.1 * torch.randn(D, device="cuda")).half()
         b = (0.1 * torch.randn(D, device="cuda")).half()
