@@ -57,12 +57,16 @@ def param_specs(cfg):
     ks = cfg["conv_kernel_sizes"]
     S = []
 
-    def mha(p, dm, kd):
-        # q, k, v adjacent (fused QKV / KV GEMMs), then biases q, k, v adjacent
-        S.extend([(f"{p}.q_proj.weight", (dm, dm)), (f"{p}.k_proj.weight", (dm, kd)),
-                  (f"{p}.v_proj.weight", (dm, kd)), (f"{p}.q_proj.bias", (dm,)),
-                  (f"{p}.k_proj.bias", (dm,)), (f"{p}.v_proj.bias", (dm,)),
-                  (f"{p}.out_proj.weight", (dm, dm)), (f"{p}.out_proj.bias", (dm,))])
+    def mha(p, dm, kd, kv=True):
+        # q, k, v adjacent (fused QKV / KV GEMMs), then biases q, k, v adjacent; kv=False leaves
+        # k/v to the decoder's cross-attention block below
+        S.append((f"{p}.q_proj.weight", (dm, dm)))
+        if kv:
+            S.extend([(f"{p}.k_proj.weight", (dm, kd)), (f"{p}.v_proj.weight", (dm, kd))])
+        S.append((f"{p}.q_proj.bias", (dm,)))
+        if kv:
+            S.extend([(f"{p}.k_proj.bias", (dm,)), (f"{p}.v_proj.bias", (dm,))])
+        S.extend([(f"{p}.out_proj.weight", (dm, dm)), (f"{p}.out_proj.bias", (dm,))])
 
     def ln(p, n):
         S.extend([(f"{p}.weight", (n,)), (f"{p}.bias", (n,))])
@@ -73,10 +77,20 @@ def param_specs(cfg):
         S.extend([(f"{p}.fc2.weight", (dd, Fd)), (f"{p}.fc2.bias", (dd,)),
                   (f"{p}.fc1.weight", (Fd, dd)), (f"{p}.fc1.bias", (Fd,))])
         ln(p + ".final_layer_norm", dd)
-        mha(p + ".encoder_attn", dd, d)
+        mha(p + ".encoder_attn", dd, d, kv=False)
         ln(p + ".encoder_attn_layer_norm", dd)
         mha(p + ".self_attn", dd, dd)
         ln(p + ".self_attn_layer_norm", dd)
+    # Every decoder layer's cross-attention K/V projection reads the same encoder output, so their
+    # weights sit layer-major in one [L_d*2*dd, d] slab (and biases in one [L_d*2*dd] vector): one
+    # forward GEMM, one dgrad and one wgrad for all layers.  Their gradients complete after the whole
+    # decoder backward, hence the block's place after the decoder layers.
+    for l in range(cfg["decoder_layers"]):
+        p = f"decoder.layers.{l}.encoder_attn"
+        S.extend([(f"{p}.k_proj.weight", (dd, d)), (f"{p}.v_proj.weight", (dd, d))])
+    for l in range(cfg["decoder_layers"]):
+        p = f"decoder.layers.{l}.encoder_attn"
+        S.extend([(f"{p}.k_proj.bias", (dd,)), (f"{p}.v_proj.bias", (dd,))])
     S.append(("decoder.embed_tokens.weight", (V, dd)))
     if cfg["fusion"]:
         Di = cfg["image_feat_dim"]
@@ -348,6 +362,14 @@ class MMS2UTModel:
         else:
             off, _, n = self.params.offsets[last_param]
             self.grad_ready_hook(off + n)
+
+    def cross_kv(self, grad=False):
+        """(W [L_d*2d, de], b [L_d*2d]) of all decoder layers' cross-attention K/V projections."""
+        L = self.cfg["decoder_layers"]
+        f, t = "decoder.layers.0.encoder_attn", f"decoder.layers.{L - 1}.encoder_attn"
+        W = self.params.span(f + ".k_proj.weight", t + ".v_proj.weight", grad=grad)
+        b = self.params.span(f + ".k_proj.bias", t + ".v_proj.bias", grad=grad)
+        return W.view(b.numel(), -1), b
 
     def P(self, n):
         return self.params.p[n]
@@ -641,7 +663,7 @@ class MMS2UTModel:
         return dtext_total
 
     # -------------------------------------------------------------- decoder layer
-    def dec_layer_fwd(self, l, x, enc, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None):
+    def dec_layer_fwd(self, l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None):
         cfg = self.cfg
         p = f"decoder.layers.{l}"
         d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
@@ -672,14 +694,12 @@ class MMS2UTModel:
         h2, c["m2"], c["r2"] = K.layernorm(x2, self.P(p + ".encoder_attn_layer_norm.weight"), self.P(p + ".encoder_attn_layer_norm.bias"))
         c["h2"] = h2
         q = K.linear(h2, self.P(p + ".encoder_attn.q_proj.weight"), self.P(p + ".encoder_attn.q_proj.bias"))
-        de = cfg["encoder_embed_dim"]
-        Wkv = self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight").view(2 * d, de)
-        bkv = self.params.span(p + ".encoder_attn.k_proj.bias", p + ".encoder_attn.v_proj.bias")
-        kv = K.linear(enc, Wkv, bkv)
+        ldkv = kv_all.stride(0)
+        kv = kv_all[:, 2 * d * l:2 * d * (l + 1)]   # this layer's K | V columns of the batched projection
         c["q"], c["kv"] = q, kv
         O2 = torch.empty(R, d, dtype=F16, device=x.device)
         c["drop_ca"] = self._drop(pa, B * H * Tt * Te)
-        c["cattn"] = attn_forward(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tt, Te, hd, hd ** -0.5, O2, d,
+        c["cattn"] = attn_forward(q, kv, kv[:, d:], d, ldkv, ldkv, B, H, Tt, Te, hd, hd ** -0.5, O2, d,
                                   key_len=enc_len32, p=pa, drop=c["drop_ca"])
         c["cO"] = O2
         c["drop2"] = self._drop(pd, R * d)
@@ -698,9 +718,10 @@ class MMS2UTModel:
                       p=pd, drop=c["drop3"])
         return x4, c
 
-    def dec_layer_bwd(self, l, c, dx4, denc, enc, dy3=None, emit=None):
-        """Returns (dx, masked dx for the layer below or None); accumulates the cross-attention
-        K/V dgrad into denc [B*Te, de].  dy3/emit as enc_layer_bwd's dy2/emit."""
+    def dec_layer_bwd(self, l, c, dx4, dkv_all, dy3=None, emit=None):
+        """Returns (dx, masked dx for the layer below or None); writes this layer's cross-attention
+        K/V gradient into its columns of dkv_all [B*Te, L_d*2d] (the K/V projection's dgrad and
+        wgrad run once for all layers, decoder_backward).  dy3/emit as enc_layer_bwd's dy2/emit."""
         cfg = self.cfg
         p = f"decoder.layers.{l}"
         d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
@@ -725,14 +746,10 @@ class MMS2UTModel:
         dO2 = K.linear_dgrad(dy2, self.P(p + ".encoder_attn.out_proj.weight"))
         q, kv = c["q"], c["kv"]
         dq = torch.empty_like(q)
-        dkv = torch.empty_like(kv)
-        attn_backward(c["cattn"], dO2, d, c["cO"], q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tt, Te, hd,
-                      hd ** -0.5, dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pa, drop=c["drop_ca"])
-        de = cfg["encoder_embed_dim"]
-        Wkv = self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight").view(2 * d, de)
-        K.linear_wgrad(dkv, enc, self.params.span(p + ".encoder_attn.k_proj.weight", p + ".encoder_attn.v_proj.weight", grad=True).view(2 * d, de),
-                       db=self.params.span(p + ".encoder_attn.k_proj.bias", p + ".encoder_attn.v_proj.bias", grad=True))
-        K.linear_dgrad(dkv, Wkv, out=denc, accumulate=True)
+        dkv = dkv_all[:, 2 * d * l:2 * d * (l + 1)]
+        ldkv, lddkv = kv.stride(0), dkv.stride(0)
+        attn_backward(c["cattn"], dO2, d, c["cO"], q, kv, kv[:, d:], d, ldkv, ldkv, B, H, Tt, Te, hd,
+                      hd ** -0.5, dq, dkv, dkv[:, d:], d, lddkv, lddkv, p=pa, drop=c["drop_ca"])
         K.linear_wgrad(dq, c["h2"], self.G(p + ".encoder_attn.q_proj.weight"),
                        db=self.G(p + ".encoder_attn.q_proj.bias"))
         dh2 = K.linear_dgrad(dq, self.P(p + ".encoder_attn.q_proj.weight"))
@@ -844,8 +861,11 @@ class MMS2UTModel:
         ctx["emb"] = (scale, pd)
         tgt_mask = batch.tgt_mask  # uint8 [B, round8(Tt)] or None (no target padding in the batch)
         ctx["layers"] = []
+        Wkv, bkv = self.cross_kv()
+        kv_all = K.linear(enc, Wkv, bkv)   # [B*Te, L_d*2d]: every layer's cross-attention K | V
+        ctx["kv_all"] = kv_all
         for l in range(cfg["decoder_layers"]):
-            x, c = self.dec_layer_fwd(l, x, enc, B, Tt, Te, tgt_mask, enc_len32, batch.tgt_len32)
+            x, c = self.dec_layer_fwd(l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, batch.tgt_len32)
             ctx["layers"].append(c)
         xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("decoder.layer_norm.weight"), self.P("decoder.layer_norm.bias"))
         ctx["lx"], ctx["xl"] = x, xl
@@ -874,10 +894,18 @@ class MMS2UTModel:
                                     self.params.span("decoder.layer_norm.weight", "decoder.layer_norm.bias", grad=True),
                                     emit=emit(L - 1))
         self._ready("decoder.layer_norm.bias")
+        dkv_all = torch.empty_like(ctx["kv_all"])
         for l in reversed(range(L)):
-            dx, dmask = self.dec_layer_bwd(l, layers[l], dx, denc, enc, dy3=dmask, emit=emit(l - 1))
+            dx, dmask = self.dec_layer_bwd(l, layers[l], dx, dkv_all, dy3=dmask, emit=emit(l - 1))
             layers[l] = None
             self._ready(f"decoder.layers.{l}.self_attn_layer_norm.bias")
+        # cross-attention K/V projections of all layers: one wgrad (+ bias) and one dgrad (K = L_d*2d)
+        Wkv, _ = self.cross_kv()
+        gWkv, gbkv = self.cross_kv(grad=True)
+        K.linear_wgrad(dkv_all, enc, gWkv, db=gbkv)
+        K.linear_dgrad(dkv_all, Wkv, out=denc)   # the encoder output's only gradient source
+        del dkv_all
+        self._ready(f"decoder.layers.{L - 1}.encoder_attn.v_proj.bias")
         scale, pd = ctx["emb"]
         K.token_embed_bwd(ctx["tok"], dx, dE32, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
         gE = self.G("decoder.embed_tokens.weight")

@@ -103,7 +103,7 @@ class _ModelFn(torch.autograd.Function):
         ectx, dctx, enc, batch = fctx.saved
         fctx.saved = None
         d = model.cfg["encoder_embed_dim"]
-        denc = torch.zeros(enc.shape[0], d, dtype=F16, device=enc.device)
+        denc = torch.empty(enc.shape[0], d, dtype=F16, device=enc.device)  # written by decoder_backward
         model.decoder_backward(dctx, dlogits.contiguous(), enc, denc)
         del dctx
         model.encoder_backward(ectx, denc)

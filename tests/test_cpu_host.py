@@ -68,6 +68,13 @@ def test_flat_layout_spans_contiguous():
     assert ps.span(p + ".q_proj.bias", p + ".v_proj.bias").numel() == 3 * 768
     for name, (off, shape, n) in ps.offsets.items():
         assert off % 8 == 0
+    # all decoder layers' cross-attention K/V projections form one [L_d*2d, d] slab (one GEMM)
+    L = mm.default_cfg()["decoder_layers"]
+    f, t = "decoder.layers.0.encoder_attn", f"decoder.layers.{L - 1}.encoder_attn"
+    assert ps.span(f + ".k_proj.weight", t + ".v_proj.weight").numel() == L * 2 * 768 * 768
+    assert ps.span(f + ".k_proj.bias", t + ".v_proj.bias").numel() == L * 2 * 768
+    l1 = "decoder.layers.1.encoder_attn"
+    assert ps.offsets[l1 + ".k_proj.weight"][0] == ps.offsets[f + ".v_proj.weight"][0] + 768 * 768
 
 
 def test_collater_contract():
