@@ -96,6 +96,9 @@ int mms2ut_splitk_reduce_bias(const float* slabs, int nsplit, int64_t slab, int 
 /* `waiter` waits for all work enqueued on `signaler` so far (event record + stream wait).
  * Forks/joins the weight-gradient side stream (the reference's DDP/autograd stream overlap). */
 int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler);
+/* new stream whose kernels may only run on the CUs whose bit is set in mask[nwords]
+ * (hipExtStreamCreateWithCUMask); used for the weight-gradient side stream.                    */
+int mms2ut_stream_create_cumask(const uint32_t* mask, int nwords, hipStream_t* out);
 
 /* ---------------------------------------------------------------- LayerNorm (eps, affine)
  * Replaces fairseq LayerNorm (self_attn_layer_norm / final_layer_norm / encoder_attn_layer_norm /

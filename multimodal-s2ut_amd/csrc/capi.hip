@@ -120,3 +120,16 @@ extern "C" int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler) {
   }
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------
+// A stream restricted to a subset of CUs (bit i of mask = logical CU i), for the weight-gradient
+// side stream: the dgrad chain on the main stream then keeps the remaining CUs to itself.
+// ------------------------------------------------------------------------------------------
+extern "C" int mms2ut_stream_create_cumask(const uint32_t* mask, int nwords, hipStream_t* out) {
+  MMS_REQUIRE(mask && nwords > 0 && out, "stream_create_cumask: bad arguments");
+  if (hipExtStreamCreateWithCUMask(out, (uint32_t)nwords, mask) != hipSuccess) {
+    mms::set_error("stream_create_cumask: hipExtStreamCreateWithCUMask failed");
+    return 1;
+  }
+  return 0;
+}

@@ -339,13 +339,94 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
     }
   __syncthreads();
   const int q = lane & 7;
-#pragma unroll 2
-  for (int pass = 0; pass < 8; ++pass) {
-    const int r = pass * 8 + (lane >> 3);
+  const int n = bn + wn * 64 + 8 * q;
+  auto stage8 = [&](int r, float (&v)[8]) {
     const f32x4 lo = *reinterpret_cast<const f32x4*>(stage + r * 64 + (((2 * q) ^ (r & 15)) << 2));
     const f32x4 hi = *reinterpret_cast<const f32x4*>(stage + r * 64 + (((2 * q + 1) ^ (r & 15)) << 2));
-    const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    epilogue_store8<EPI>(P, Cz, auxz, bm + wm * 64 + r, bn + wn * 64 + 8 * q, v);
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  };
+  constexpr bool LOADS = EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GATE || EPI == MMS_EPI_RELU_DROP_BWD ||
+                         EPI == MMS_EPI_F16_ACC;
+  if (EPI == MMS_EPI_F32 || !(P.vec16 && n + 7 < P.N)) {
+#pragma unroll 2
+    for (int pass = 0; pass < 8; ++pass) {
+      const int r = pass * 8 + (lane >> 3);
+      float v[8];
+      stage8(r, v);
+      epilogue_store8<EPI>(P, Cz, auxz, bm + wm * 64 + r, n, v);
+    }
+    return;
+  }
+  // Fast path (every fp16 row operand 16-B aligned, 8 whole columns): the global operand loads of
+  // all 8 rows (aux / existing C, bias) are issued before the first store.  Interleaved per row,
+  // hipcc must keep each row's loads behind the previous row's stores (they may alias), which
+  // serialised the epilogue into 8 dependent global round trips.
+  const int m0 = bm + wm * 64 + (lane >> 3);
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (EPI != MMS_EPI_RELU_DROP_BWD && P.bias) {
+    const h16x8 b8 = *reinterpret_cast<const h16x8*>(P.bias + n);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = (float)b8[e];
+  }
+  h16* C = reinterpret_cast<h16*>(Cz);
+  h16x8 ax[8], ax2[8];
+  const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+#pragma unroll
+  for (int pass = 0; pass < 8; ++pass) {
+    const int m = m0 + 8 * pass;
+    ax[pass] = z8;
+    ax2[pass] = z8;
+    if (LOADS && m < P.M) {
+      if (EPI == MMS_EPI_F16_ACC) {
+        ax[pass] = *reinterpret_cast<const h16x8*>(C + (long)m * P.ldc + n);
+      } else {
+        ax[pass] = *reinterpret_cast<const h16x8*>(auxz + (long)m * P.ldaux + n);
+        if (EPI == MMS_EPI_GATE) ax2[pass] = *reinterpret_cast<const h16x8*>(auxz + (long)m * P.ldaux + P.N + n);
+      }
+    }
+  }
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+#pragma unroll
+  for (int pass = 0; pass < 8; ++pass) {
+    const int m = m0 + 8 * pass;
+    if (m >= P.M) continue;
+    float x[8];
+    stage8(pass * 8 + (lane >> 3), x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = x[e] * P.alpha + bv[e];
+    bool keep[8] = {true, true, true, true, true, true, true, true};
+    if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID) && P.thresh) {
+      const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
+      bool k0[4], k1[4];
+      mms_keep4(P.seed, c0, P.thresh, k0);
+      mms_keep4(P.seed, c0 + 4, P.thresh, k1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { keep[e] = k0[e]; keep[e + 4] = k1[e]; }
+    }
+    h16x8 o8;
+    if (EPI == MMS_EPI_GATE) {
+      h16x8 g8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = sigmoidf_(x[e]), ov = (float)ax[pass][e], tv = (float)ax2[pass][e];
+        g8[e] = (h16)g;
+        o8[e] = (h16)(tv + g * (ov - tv));
+      }
+      *reinterpret_cast<h16x8*>(P.out2 + (long)m * P.ldo2 + n) = g8;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float o;
+        if (EPI == MMS_EPI_RELU_DROP) o = keep[e] ? fmaxf(x[e], 0.f) * dscale : 0.f;
+        else if (EPI == MMS_EPI_DROP_RESID) o = (float)ax[pass][e] + (keep[e] ? x[e] * dscale : 0.f);
+        else if (EPI == MMS_EPI_RELU_DROP_BWD) o = (float)ax[pass][e] > 0.f ? x[e] * dscale : 0.f;
+        else if (EPI == MMS_EPI_F16_ACC) o = (float)ax[pass][e] + x[e];
+        else o = x[e];
+        o8[e] = (h16)o;
+      }
+    }
+    *reinterpret_cast<h16x8*>(C + (long)m * P.ldc + n) = o8;
   }
 }
 

@@ -136,7 +136,10 @@ def _splitk_for(tiles, kred, slots=512):
     the tile grid alone fills the chip."""
     if tiles >= 2 * slots:
         return 1
+    cap = int(os.environ.get("MMS2UT_WGRAD_SPLITK", "8"))
     for s in (8, 4, 2):
+        if s > cap:
+            continue
         if kred // s >= 512:
             return s
     return 1
@@ -177,12 +180,32 @@ class _SideRegion:
 _SIDE_REGION = _SideRegion()
 
 
+def make_side_stream(device):
+    """The weight-gradient side stream: lowest priority; with MMS2UT_SIDE_CUS=stride:K (every K-th
+    CU) or block:K (the first 1/K of the CUs) it is also confined to that CU subset."""
+    spec = os.environ.get("MMS2UT_SIDE_CUS", "")
+    if not spec:
+        return torch.cuda.Stream(device=device, priority=100)
+    import ctypes
+    kind, k = spec.split(":")
+    k = int(k)
+    n = torch.cuda.get_device_properties(device).multi_processor_count
+    on = [(i % k == 0) if kind == "stride" else (i < n // k) for i in range(n)]
+    words = (ctypes.c_uint32 * ((n + 31) // 32))()
+    for i, b in enumerate(on):
+        if b:
+            words[i // 32] |= 1 << (i % 32)
+    h = ctypes.c_void_p()
+    call("mms2ut_stream_create_cumask", ctypes.addressof(words), len(words), ctypes.addressof(h))
+    return torch.cuda.ExternalStream(h.value, device=device)
+
+
 def side_begin(*tensors):
     """Fork: the side stream waits for everything enqueued so far on the current stream."""
     if not _Side.enabled:
         return None
     if _Side.stream is None:
-        _Side.stream = torch.cuda.Stream(device=_dev(), priority=100)
+        _Side.stream = make_side_stream(_dev())
         _Side.ptr = _Side.stream.cuda_stream
     call("mms2ut_stream_wait", _Side.ptr, torch._C._cuda_getCurrentRawStream(_dev()))
     _Side.keep.extend(tensors)

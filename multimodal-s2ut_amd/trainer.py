@@ -35,7 +35,7 @@ class Trainer:
         if os.environ.get("MMS2UT_STREAM_PRIO", "1") != "0" and model.params.flat.is_cuda:
             self.stream = torch.cuda.Stream(device=model.params.flat.device, priority=-100)
             if K._Side.stream is None:
-                K._Side.stream = torch.cuda.Stream(device=model.params.flat.device, priority=100)
+                K._Side.stream = K.make_side_stream(model.params.flat.device)
                 K._Side.ptr = K._Side.stream.cuda_stream
 
     def train_step(self, batch):

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--step", type=int, default=-2)
     ap.add_argument("--list", action="store_true")
+    ap.add_argument("--per-queue", action="store_true")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -55,6 +56,18 @@ def main():
     print(f"  GPU busy (union) {cov / 1e3:.1f} us, idle {(t1 - t0 - cov) / 1e3:.1f} us")
     for k, (n, d) in sorted(agg.items(), key=lambda x: -x[1][1]):
         print(f"  {d:9.1f} us {n:5d}x {d / n:8.1f} us  {k}")
+    if a.per_queue:
+        for q in busy:
+            qa = defaultdict(lambda: [0, 0.0])
+            for r in step:
+                if r["Queue_Id"] != q:
+                    continue
+                d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                qa[short(r["Kernel_Name"])][0] += 1
+                qa[short(r["Kernel_Name"])][1] += d
+            print(f"== queue {q}")
+            for k, (n, d) in sorted(qa.items(), key=lambda x: -x[1][1])[:25]:
+                print(f"  {d:9.1f} us {n:5d}x {d / n:8.1f} us  {k}")
     if a.list:
         for r in step:
             st = (int(r["Start_Timestamp"]) - t0) / 1e3
