@@ -326,7 +326,11 @@ def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None)
         dxd = torch.empty_like(x)
     call("mms2ut_layernorm_bwd", dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr(),
          rstd.data_ptr(), _p(dres), _p(dx), part.data_ptr(), R, D, _p(dxd), float(p), seed, off, _s())
-    call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), 0, _s())
+    # gamma/beta gradients feed only the optimizer: their partial-sum reduction leaves the
+    # critical path for the weight-gradient side stream
+    ctx = side_begin(part)
+    with (ctx or _NULLCTX):
+        call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), 0, _s())
     if emit is not None:
         return dx, (dxd if dxd is not None else dx)
     return dx
