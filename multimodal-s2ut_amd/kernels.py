@@ -200,6 +200,14 @@ def make_side_stream(device):
     return torch.cuda.ExternalStream(h.value, device=device)
 
 
+def side_stream(device):
+    """The (lazily created) weight-gradient side stream."""
+    if _Side.stream is None:
+        _Side.stream = make_side_stream(device)
+        _Side.ptr = _Side.stream.cuda_stream
+    return _Side.stream
+
+
 def side_begin(*tensors):
     """Fork: the side stream waits for everything enqueued so far on the current stream."""
     if not _Side.enabled:

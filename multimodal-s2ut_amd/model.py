@@ -18,6 +18,7 @@ Reference path restated here:
   fairseq TransformerUnitDecoder             (6 pre-LN layers, tied output projection)
 """
 import math
+import re
 from collections import OrderedDict
 
 import numpy as np
@@ -158,6 +159,52 @@ class ParamStore:
         self.unused = OrderedDict((n, torch.zeros(s, dtype=F16, device=device)) for n, s in unused)
         self.p = {k: self.view(k) for k in self.offsets}
         self.g = {k: self.view(k, grad=True) for k in self.offsets}
+        self.groups = self._forward_groups()
+        self.pending = {}   # group -> event of its (deferred) optimizer update, see await_group
+
+    @staticmethod
+    def group_of(name):
+        """Forward-consumption group of a parameter (one flat contiguous range per group)."""
+        m = re.match(r"encoder\.transformer_layers\.(\d+)\.", name)
+        if m:
+            return f"enc{m.group(1)}"
+        if name.startswith("encoder.subsample."):
+            return "sub"
+        if name.startswith("encoder."):
+            return "enc_tail"        # final encoder LN + fusion
+        if re.match(r"decoder\.layers\.\d+\.encoder_attn\.[kv]_proj\.", name):
+            return "cross_kv"
+        m = re.match(r"decoder\.layers\.(\d+)\.", name)
+        if m:
+            return f"dec{m.group(1)}"
+        if name.startswith("decoder.embed_tokens"):
+            return "dec_emb"
+        return "dec_ln"
+
+    def _forward_groups(self):
+        """[(group, start, end)] flat element ranges in the order the forward consumes them (the
+        reverse of the backward-completion layout)."""
+        runs = []
+        for name, _ in self.specs:
+            off, _, n = self.offsets[name]
+            grp = self.group_of(name)
+            if runs and runs[-1][0] == grp:
+                runs[-1][2] = round_up(off + n, self.ALIGN)
+            else:
+                assert all(r[0] != grp for r in runs), f"group {grp} not contiguous"
+                runs.append([grp, off, round_up(off + n, self.ALIGN)])
+        runs[-1][2] = self.numel
+        return [tuple(r) for r in reversed(runs)]
+
+    def await_group(self, grp):
+        """Make the current stream wait for a deferred optimizer update of `grp` (no-op if none)."""
+        ev = self.pending.pop(grp, None)
+        if ev is not None:
+            torch.cuda.current_stream(self.flat.device).wait_event(ev)
+
+    def await_all(self):
+        for grp in list(self.pending):
+            self.await_group(grp)
 
     def view(self, name, grad=False):
         off, shape, n = self.offsets[name]
@@ -172,6 +219,7 @@ class ParamStore:
         return buf[a:b]
 
     def load_state_dict(self, sd, strict=True):
+        self.await_all()
         seen = set()
         for k, v in sd.items():
             if k in self.offsets:
@@ -186,6 +234,7 @@ class ParamStore:
         return missing
 
     def state_dict(self):
+        self.await_all()
         sd = OrderedDict((k, v.detach().clone()) for k, v in self.p.items())
         for k, v in self.unused.items():
             sd[k] = v.detach().clone()
@@ -787,6 +836,7 @@ class MMS2UTModel:
         imgs, img_mask = batch.imgs, batch.img_keymask
         B = src_tokens.shape[0]
         ctx = {}
+        self.params.await_group("sub")
         h, Te, ctx["sub"] = self.subsample_fwd(src_tokens, None)
         assert Te == batch.Te, (Te, batch.Te)
         lens32 = batch.enc_len32
@@ -799,8 +849,10 @@ class MMS2UTModel:
         ctx["emb"] = (scale, pd)
         ctx["layers"] = []
         for l in range(cfg["encoder_layers"]):
+            self.params.await_group(f"enc{l}")
             x, c = self.enc_layer_fwd(l, x, B, Te, lens32)
             ctx["layers"].append(c)
+        self.params.await_group("enc_tail")
         xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("encoder.layer_norm.weight"), self.P("encoder.layer_norm.bias"))
         ctx["lx"] = x
         ctx["fusion"] = None
@@ -857,16 +909,20 @@ class MMS2UTModel:
         pd = self._p("dropout")
         ctx["drop_emb"] = self._drop(pd, B * Tt * d)
         ctx["tok"] = tok
+        self.params.await_group("dec_emb")
         x = K.token_embed(tok, self.P("decoder.embed_tokens.weight"), pos, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
         ctx["emb"] = (scale, pd)
         tgt_mask = batch.tgt_mask  # uint8 [B, round8(Tt)] or None (no target padding in the batch)
         ctx["layers"] = []
+        self.params.await_group("cross_kv")
         Wkv, bkv = self.cross_kv()
         kv_all = K.linear(enc, Wkv, bkv)   # [B*Te, L_d*2d]: every layer's cross-attention K | V
         ctx["kv_all"] = kv_all
         for l in range(cfg["decoder_layers"]):
+            self.params.await_group(f"dec{l}")
             x, c = self.dec_layer_fwd(l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, batch.tgt_len32)
             ctx["layers"].append(c)
+        self.params.await_all()   # "dec_ln" and anything not consumed above
         xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("decoder.layer_norm.weight"), self.P("decoder.layer_norm.bias"))
         ctx["lx"], ctx["xl"] = x, xl
         Vp = round_up(V, 8)
@@ -882,9 +938,10 @@ class MMS2UTModel:
         B, Tt = ctx["B"], ctx["Tt"]
         E = self.P("decoder.embed_tokens.weight")
         dE32 = torch.zeros(V, d, dtype=torch.float32, device=E.device)
-        # tied output projection: dE += dlogits^T xl ; dxl = dlogits E
-        # main stream: the embedding scatter (token_embed_bwd) accumulates into the same dE32
-        K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32, side=False)
+        # tied output projection: dE += dlogits^T xl ; dxl = dlogits E.  Both halves of the tied
+        # embedding gradient (this wgrad and the token scatter below) run on the side stream, in
+        # order, accumulating into dE32 (zeroed here on the main stream before the fork).
+        K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32)
         dxl = torch.empty(B * Tt, d, dtype=F16, device=E.device)
         K.gemm(dlogits, E, dxl, B * Tt, d, V, a_kc=True, b_kc=False, lda=ctx["Vp"], ldb=d, ldc=d)
         layers = ctx["layers"]
@@ -907,8 +964,9 @@ class MMS2UTModel:
         del dkv_all
         self._ready(f"decoder.layers.{L - 1}.encoder_attn.v_proj.bias")
         scale, pd = ctx["emb"]
-        K.token_embed_bwd(ctx["tok"], dx, dE32, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
         gE = self.G("decoder.embed_tokens.weight")
-        K.call("mms2ut_splitk_reduce", dE32.data_ptr(), 1, dE32.numel(), V, d, gE.data_ptr(), d, 1, 1.0,
-               K._s())
+        with (K.side_begin(dx, ctx["tok"], dE32) or K._NULLCTX):
+            K.token_embed_bwd(ctx["tok"], dx, dE32, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
+            K.call("mms2ut_splitk_reduce", dE32.data_ptr(), 1, dE32.numel(), V, d, gE.data_ptr(), d, 1, 1.0,
+                   K._s())
         self._ready("decoder.embed_tokens.weight")

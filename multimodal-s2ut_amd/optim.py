@@ -10,6 +10,7 @@ Reference semantics (fairseq, invoked by textless/1_train.sh:105-125):
   --warmup-init-lr 1e-7 --warmup-updates 10000 --fp16 (init scale 128, scale window 2^14/world).
 """
 import math
+import os
 
 import torch
 
@@ -35,6 +36,7 @@ class FP16Adam:
         ost[K.OST_LAST_OVERFLOW] = -1.0
         ost[K.OST_CLIP_COEF] = 1.0
         self.ost = ost.to(params.flat.device)
+        self.defer = os.environ.get("MMS2UT_DEFER_ADAM", "0") == "1"
 
     def resync_master(self):
         """After loading fp16 weights: master := fp32 copy of the fp16 params."""
@@ -54,15 +56,38 @@ class FP16Adam:
         return self.lr * math.sqrt(wu) * max(self.num_updates, 1) ** -0.5
 
     def step(self, sample_size):
-        """sample_size: device fp32 tensor [1] (all-reduced ntokens)."""
+        """sample_size: device fp32 tensor [1] (all-reduced ntokens).
+
+        The global part (grad norm, clip factor, overflow / loss-scale logic) runs on the current
+        stream.  The Adam update itself is deferred: it is enqueued on the side stream in chunks,
+        one per forward-consumption group of the parameter layout (subsampler, encoder layer 0, ...),
+        each recording an event that the next forward waits on right before it reads that group
+        (ParamStore.await_group), so the HBM-bound update can overlap the next step's first
+        layers.  MMS2UT_DEFER_ADAM=1 enables it; otherwise one
+        launch in stream order (the default: measured no faster)."""
         b1, b2 = self.betas
         K.grad_norm(self.params.grad, self.ost, sample_size)
         K.optim_prepare(self.ost, self.lr, self.warmup_init_lr, self.warmup_updates, b1, b2, self.clip,
                         self.scale_window, self.min_loss_scale)
-        K.adam(self.params.flat, self.params.grad, self.master, self.exp_avg, self.exp_avg_sq, self.ost,
-               b1, b2, self.eps, self.wd)
+        ps = self.params
+        if not (self.defer and ps.flat.is_cuda and hasattr(ps, "groups")):
+            K.adam(ps.flat, ps.grad, self.master, self.exp_avg, self.exp_avg_sq, self.ost, b1, b2, self.eps,
+                   self.wd)
+            return
+        ps.await_all()  # the previous step's chunks (normally already awaited by the forward)
+        side = K.side_stream(ps.flat.device)
+        side.wait_stream(torch.cuda.current_stream(ps.flat.device))
+        with torch.cuda.stream(side):
+            for grp, a, b in ps.groups:
+                K.adam(ps.flat[a:b], ps.grad[a:b], self.master[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
+                       self.ost, b1, b2, self.eps, self.wd)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                ps.pending[grp] = ev
 
     def stats(self):
+        if hasattr(self.params, "await_all"):
+            self.params.await_all()
         o = self.ost.cpu()
         return {"gnorm": float(o[K.OST_GNORM]), "overflow": bool(o[K.OST_OVERFLOW]),
                 "loss_scale": float(o[K.OST_LOSS_SCALE]), "step": int(o[K.OST_STEP]),

@@ -52,11 +52,14 @@ class Trainer:
         cfg = self.cfg
         m = self.model
         m.train()
-        m.params.grad.zero_()
         if self.reducer is not None:
             self.reducer.reset()
             m.grad_ready_hook = self.reducer.ready
         logits = runtime.model_logits(m, batch)
+        # zeroed after the forward: by then every deferred optimizer chunk of the previous step
+        # (which reads the gradients) has been waited for (ParamStore.await_group)
+        m.params.await_all()
+        m.params.grad.zero_()
         loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
                                               cfg["label_smoothing"], cfg["padding_idx"])
         del logits

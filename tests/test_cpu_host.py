@@ -177,3 +177,19 @@ def test_lr_schedule_inverse_sqrt():
     opt.num_updates = 40000
     assert abs(opt.get_lr() - 5e-4 * (10000 / 40000) ** 0.5) < 1e-12
     assert opt.scale_window == 16384
+
+
+def test_param_groups_tile_flat_buffer():
+    """The deferred optimizer's forward-consumption groups tile the flat buffer."""
+    mm = pkg()
+    ps = mm.model.ParamStore(mm.param_specs(mm.default_cfg())[0], "cpu")
+    g = ps.groups
+    assert g[0][0] == "sub" and g[1][0] == "enc0" and g[-1][0] == "dec_ln"
+    spans = sorted((a, b) for _, a, b in g)
+    assert spans[0][0] == 0 and spans[-1][1] == ps.numel
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(len(spans) - 1))
+    for name in ps.offsets:
+        grp = ps.group_of(name)
+        a, b = [(x, y) for n, x, y in g if n == grp][0]
+        off, _, n = ps.offsets[name]
+        assert a <= off and off + n <= b, name
