@@ -92,6 +92,19 @@ def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000):
     return out
 
 
+def gemm_pmc_traffic():
+    """Measured HBM bytes per GEMM launch: the newest profiles/*_gemm_traffic.json, written by
+    scripts/pmc_traffic.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this bench
+    (gfx950 FETCH x2 correction).  A PMC pass cannot run inside the timed bench itself."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("gemm_hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cfg, model, sample, budget_s=20.0):
     """The oracle (fp32 PyTorch-CPU restatement) timed on the host cores on a bounded sample of the
     same workload: a few utterances of one batch, full training step (fwd + bwd + Adam)."""
@@ -181,7 +194,8 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    gemm_ms, n_launch, launched_flops = kernels.gemm_profile_end() if not args.no_gemm_timing else (0.0, 0, 0.0)
+    gemm_ms, n_launch, launched_flops, gemm_bytes = (kernels.gemm_profile_end() if not args.no_gemm_timing
+                                                     else (0.0, 0, 0.0, 0.0))
     elapsed = t1 - t0
     frames = sum(int(batches[(args.warmup + i) % len(batches)][1].n_src_frames) for i in range(args.steps))
     alg_flops = sum(batches[(args.warmup + i) % len(batches)][4] for i in range(args.steps))
@@ -200,6 +214,7 @@ def main():
         frames_all, flops_all, gemm_all, nl_all = float(frames), float(alg_flops), gemm_ms, float(n_launch)
         total_flops_all = float(total_flops)
     ost = tr.opt.stats()
+    traffic, traffic_src = gemm_pmc_traffic()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, model, batches[0][2], args.cpu_budget)
@@ -222,7 +237,9 @@ def main():
                        "model_tflops_per_s": total_flops_all / elapsed / 1e12},
             "roofline": {"bound": "mfma", "kernel": "mms2ut gemm_kernel (all GEMM launches)",
                          "achieved": achieved, "peak": MFMA_PEAK_F16, "unit": "TFLOP/s",
-                         "frac": (achieved / MFMA_PEAK_F16) if achieved else None, "traffic": None,
+                         "frac": (achieved / MFMA_PEAK_F16) if achieved else None, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": gemm_bytes / max(n_launch, 1),
                          "gemm_ms_per_step": gemm_all / world / args.steps,
                          "gemm_launches_per_step": nl_all / world / args.steps,
                          "gemm_launched_tflops": launched_flops / max(gemm_ms, 1e-9) / 1e9,

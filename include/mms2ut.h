@@ -81,6 +81,9 @@ int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
  * kernel time, the launch count and the launched (padded) FLOPs.  Not thread-safe.          */
 int mms2ut_profile_begin(int max_launches);
 int mms2ut_profile_end(float* total_ms, int* launches, double* flops);
+/* algorithmic HBM bytes of the GEMM launches of the last begin/end window (A and B read once, C
+ * written once; fp32 split-K slabs, residual / accumulate / gate operands included)            */
+int mms2ut_profile_bytes(double* bytes);
 
 /* sum `nsplit` fp32 slabs [rows, cols] (slab stride `slab`) * alpha -> out, row stride ldo.
  * mode bit0: fp16 output (else fp32); bit1: accumulate into out (else overwrite)            */

@@ -1083,6 +1083,7 @@ struct GemmProfile {
   int cap = 0, n = 0;
   hipEvent_t* ev = nullptr;
   double flops = 0.0;
+  double bytes = 0.0;  // algorithmic HBM bytes: A, B (and aux / accumulated C) read once, C written once
 } g_prof;
 }  // namespace
 
@@ -1096,6 +1097,7 @@ extern "C" int mms2ut_profile_begin(int max_launches) {
   g_prof.cap = max_launches;
   g_prof.n = 0;
   g_prof.flops = 0.0;
+  g_prof.bytes = 0.0;
   g_prof.on = true;
   return 0;
 }
@@ -1130,8 +1132,22 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   hipEventRecord(g_prof.ev[2 * i], stream);
   const int rc = gemm_dispatch(a, stream);
   hipEventRecord(g_prof.ev[2 * i + 1], stream);
-  if (a) g_prof.flops += 2.0 * a->M * a->N * a->K * (a->batch > 0 ? a->batch : 1);
+  if (a) {
+    const double nb = a->batch > 0 ? a->batch : 1;
+    g_prof.flops += 2.0 * a->M * a->N * a->K * nb;
+    const double c_bytes = (double)a->M * a->N * (a->epi == MMS_EPI_F32 ? 4.0 * (a->splitk > 0 ? a->splitk : 1) : 2.0);
+    double extra = 0.0;
+    if (a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_RELU_DROP_BWD || a->epi == MMS_EPI_F16_ACC) extra = 2.0 * a->M * a->N;
+    if (a->epi == MMS_EPI_GATE) extra = 6.0 * a->M * a->N;  // o, t read; g written
+    g_prof.bytes += nb * (2.0 * ((double)a->M * a->K + (double)a->N * a->K) + c_bytes + extra);
+  }
   return rc;
+}
+
+extern "C" int mms2ut_profile_bytes(double* bytes) {
+  MMS_REQUIRE(bytes != nullptr, "profile_bytes: null");
+  *bytes = g_prof.bytes;
+  return 0;
 }
 
 // 256x256-tile kernel or the 128x128 one.  MMS2UT_GEMM_TILE=256 / =128 forces a choice (A/B runs).

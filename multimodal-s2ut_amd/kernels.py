@@ -90,11 +90,12 @@ def gemm_profile_begin(max_launches=100000):
 
 
 def gemm_profile_end():
-    """-> (summed GEMM kernel ms, launches, launched FLOPs)."""
+    """-> (summed GEMM kernel ms, launches, launched FLOPs, algorithmic HBM bytes)."""
     import ctypes
-    ms, n, fl = ctypes.c_float(), ctypes.c_int(), ctypes.c_double()
+    ms, n, fl, by = ctypes.c_float(), ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
     call("mms2ut_profile_end", ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl))
-    return ms.value, n.value, fl.value
+    call("mms2ut_profile_bytes", ctypes.byref(by))
+    return ms.value, n.value, fl.value, by.value
 
 
 def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
