@@ -96,6 +96,17 @@ int mms2ut_splitk_reduce_bias(const float* slabs, int nsplit, int64_t slab, int 
                               mms2ut_half* out, int64_t ldo, const float* rs_slabs,
                               mms2ut_half* rs_out, hipStream_t stream);
 
+/* batched transpose of row-major fp16 matrices: dst[d.dst + c*rows + r] = src[d.src + r*cols + c]
+ * (element offsets).  descs (DEVICE memory) sorted by tile0, the first 64x64 tile of each matrix;
+ * rows, cols multiples of 8.  Keeps the W^T images that make every dgrad GEMM NT (K-contiguous
+ * operands) — the reference's cuBLAS dgrad reads W in place.                                    */
+typedef struct mms2ut_transpose_desc {
+  int64_t src, dst;
+  int32_t rows, cols, tile0, pad;
+} mms2ut_transpose_desc;
+int mms2ut_transpose_batch(const mms2ut_half* src, mms2ut_half* dst, const mms2ut_transpose_desc* descs,
+                           int n, int total_tiles, hipStream_t stream);
+
 /* `waiter` waits for all work enqueued on `signaler` so far (event record + stream wait).
  * Forks/joins the weight-gradient side stream (the reference's DDP/autograd stream overlap). */
 int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler);

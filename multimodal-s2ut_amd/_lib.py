@@ -62,6 +62,7 @@ SIGNATURES = {
     "mms2ut_splitk_reduce": (i32, [vp, i32, i64, i32, i32, vp, i64, i32, f32, vp]),
     "mms2ut_splitk_reduce_bias": (i32, [vp, i32, i64, i32, i32, vp, i64, vp, vp, vp]),
     "mms2ut_stream_create_cumask": (i32, [vp, i32, vp]),
+    "mms2ut_transpose_batch": (i32, [vp, vp, vp, i32, i32, vp]),
     "mms2ut_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
     "mms2ut_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp, f32, u64, u64, vp]),
     "mms2ut_layernorm_bwd_parts": (i32, [i64]),

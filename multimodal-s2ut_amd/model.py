@@ -18,6 +18,7 @@ Reference path restated here:
   fairseq TransformerUnitDecoder             (6 pre-LN layers, tied output projection)
 """
 import math
+import os
 import re
 from collections import OrderedDict
 
@@ -359,6 +360,56 @@ class MMS2UTModel:
         self.np_rng = np.random  # modality-dropout draws use the global numpy stream (reference)
         # autograd anchor: the model's output is connected to the graph through this leaf
         self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
+        self.wt = None  # K.TransposedWeights of the dgrad weights (built at the first training forward)
+
+    def dgrad_weights(self):
+        """Every weight matrix the hand-written backward multiplies a gradient by (dx = dy @ W),
+        exactly as the backward passes it to K.linear_dgrad."""
+        cfg, P, span = self.cfg, self.P, self.params.span
+        d, dd = cfg["encoder_embed_dim"], cfg["decoder_embed_dim"]
+        mats = []
+
+        def layer(p, dm):
+            mats.extend([P(p + ".fc2.weight"), P(p + ".fc1.weight"), P(p + ".self_attn.out_proj.weight"),
+                         span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * dm, dm)])
+
+        for l in range(cfg["encoder_layers"]):
+            layer(f"encoder.transformer_layers.{l}", d)
+        for l in range(cfg["decoder_layers"]):
+            p = f"decoder.layers.{l}"
+            layer(p, dd)
+            mats.extend([P(p + ".encoder_attn.out_proj.weight"), P(p + ".encoder_attn.q_proj.weight")])
+        mats.append(self.cross_kv()[0])
+        for i in range(1, len(cfg["conv_kernel_sizes"])):
+            W = P(f"encoder.subsample.conv_layers.{i}.weight")
+            mats.append(W.view(W.shape[0], -1))
+        if cfg["fusion"]:
+            Di = cfg["image_feat_dim"]
+            mats.append(P("encoder.gate_denses.0.weight"))
+            if cfg["multimodal_attention_type"] == "multimodal_attention":
+                pre = "encoder.multimodal_attns.0"
+                mats.append(P(pre + ".out_proj.weight"))
+                if Di == d:
+                    W = P(pre + ".in_proj_weight")
+                    mats.extend([W[:d], W[d:]])
+                else:
+                    mats.extend([P(pre + ".q_proj_weight"),
+                                 span(pre + ".k_proj_weight", pre + ".v_proj_weight").view(2 * d, Di)])
+            else:
+                pre = "encoder.selective_attns.0"
+                mats.extend([P(pre + ".proj.weight"), P(pre + ".q_proj.weight"),
+                             span(pre + ".k_proj.weight", pre + ".v_proj.weight").view(2 * d, Di)])
+        return [W for W in mats if W.shape[0] % 8 == 0 and W.shape[1] % 8 == 0]
+
+    def refresh_transposed_weights(self):
+        """Re-transpose the dgrad weights (side stream) for this step's backward."""
+        if not (self.training and self.params.flat.is_cuda) or os.environ.get("MMS2UT_WT", "1") == "0":
+            K.TransposedWeights.active = None
+            return
+        if self.wt is None:
+            self.wt = K.TransposedWeights(self.params.flat, self.dgrad_weights())
+        self.wt.refresh()
+        K.TransposedWeights.active = self.wt
 
     def init_params(self, seed=1):
         """Random init with fairseq's schemes (random-init weights of the architecture; no
@@ -837,6 +888,7 @@ class MMS2UTModel:
         B = src_tokens.shape[0]
         ctx = {}
         self.params.await_group("sub")
+        self.refresh_transposed_weights()
         h, Te, ctx["sub"] = self.subsample_fwd(src_tokens, None)
         assert Te == batch.Te, (Te, batch.Te)
         lens32 = batch.enc_len32

@@ -337,3 +337,26 @@ def test_gemm_tile256(K, a_kc, b_kc, M, N, K_, monkeypatch):
     K.gemm(A, B, C, M, N, K_, a_kc=a_kc, b_kc=b_kc, lda=A.stride(0), ldb=B.stride(0), ldc=ldc)
     torch.cuda.synchronize()
     assert rel(C[:, :N], Af @ Bf.t()) < 2e-3
+
+
+def test_transposed_weight_images(K):
+    """One transpose_batch launch writes W^T for every registered matrix (ragged tile edges); the
+    dgrad through the image equals the dgrad through W."""
+    flat = torch.randn(200_000, device="cuda").half()
+    mats = [flat[:72 * 136].view(72, 136), flat[10_000:10_000 + 256 * 64].view(256, 64),
+            flat[40_000:40_000 + 200 * 96].view(200, 96)]
+    wt = K.TransposedWeights(flat, mats)
+    wt.refresh()
+    for W in mats:
+        T = wt.get(W)
+        torch.cuda.synchronize()
+        assert T is not None and torch.equal(T, W.t())
+    dy = torch.randn(333, 200, device="cuda").half()
+    ref = K.linear_dgrad(dy, mats[2])
+    K.TransposedWeights.active = wt
+    try:
+        got = K.linear_dgrad(dy, mats[2])
+    finally:
+        K.TransposedWeights.active = None
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
