@@ -23,37 +23,15 @@ static bool g_fb_init = false;
 
 MMS_DEV int bitrev9(int x) { return (int)(__builtin_bitreverse32((unsigned)x) >> 23); }
 
-constexpr int MEL_W_MAX = 4096;  // packed nonzero filter weights staged in LDS (80 Kaldi bins: ~514)
-
-// Persistent blocks: the sparse triangle weights (mel_range[m] = [k0, k1) support of bank m) are
-// packed into LDS once per block; each wave then walks frames f = blockIdx.x*4 + w, += gridDim.x*4.
 __global__ void __launch_bounds__(256) fbank_kernel(const float* __restrict__ wave, const int64_t* __restrict__ wave_off,
                                                     const int* __restrict__ frame_off, int B, int total,
                                                     const float* __restrict__ banks,
                                                     const int* __restrict__ mel_range, int nbins,
                                                     float* __restrict__ feats) {
   __shared__ float s_re[4][NFFT], s_im[4][NFFT], s_x[4][WIN + 4];
-  __shared__ float s_w[MEL_W_MAX];
-  __shared__ int s_k0[256], s_cnt[256], s_off[257];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int m = threadIdx.x; m < nbins; m += 256) {
-    s_k0[m] = mel_range[2 * m];
-    s_cnt[m] = mel_range[2 * m + 1] - mel_range[2 * m];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int o = 0;
-    for (int m = 0; m < nbins; ++m) { s_off[m] = o; o += s_cnt[m]; }
-    s_off[nbins] = o;
-  }
-  __syncthreads();
-  for (int m = 0; m < nbins; ++m)
-    for (int i = threadIdx.x; i < s_cnt[m]; i += 256) s_w[s_off[m] + i] = banks[(long)m * NBIN + s_k0[m] + i];
-  __syncthreads();
-  float* X = s_x[w];
-  float* re = s_re[w];
-  float* im = s_im[w];
-  for (int f = blockIdx.x * 4 + w; f < total; f += gridDim.x * 4) {
+  const int f = blockIdx.x * 4 + w;
+  if (f >= total) return;
   // utterance of this frame (binary search over frame_off)
   int lo = 0, hi = B;
   while (hi - lo > 1) {
@@ -63,9 +41,10 @@ __global__ void __launch_bounds__(256) fbank_kernel(const float* __restrict__ wa
   const int b = lo;
   const int t = f - frame_off[b];
   const float* src = wave + wave_off[b] + (long)t * SHIFT;
+  float* X = s_x[w];
+  float* re = s_re[w];
+  float* im = s_im[w];
   float sum = 0.f;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   for (int j = lane; j < WIN; j += 64) { const float v = src[j]; X[j] = v; sum += v; }
   const float mean = wave_sum(sum) / WIN;
   __builtin_amdgcn_wave_barrier();
@@ -118,12 +97,11 @@ __global__ void __launch_bounds__(256) fbank_kernel(const float* __restrict__ wa
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   const float flt_eps = 1.1920928955078125e-07f;
   for (int m = lane; m < nbins; m += 64) {
-    const float* wk = s_w + s_off[m];
-    const float* xk = X + s_k0[m];
+    const float* bk = banks + (long)m * NBIN;
     float acc = 0.f;
-    for (int k = 0; k < s_cnt[m]; ++k) acc += wk[k] * xk[k];   // triangle support only, same order
+    const int k0 = mel_range[2 * m], k1 = mel_range[2 * m + 1];  // triangle support only
+    for (int k = k0; k < k1; ++k) acc += bk[k] * X[k];
     feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
-  }
   }
 }
 
@@ -172,12 +150,17 @@ __global__ void __launch_bounds__(256) cmvn_collate_kernel(const float* __restri
     s_std[c] = cmvn ? __fsqrt_rn(fmaxf(var, 1e-10f)) : 1.f;
   }
   __syncthreads();
+  // normalise + collate, 4 consecutive bins per thread (16-B loads, 8-B stores)
   const long n = (long)Tmax * nbins;
-  for (long i = threadIdx.x; i < n; i += blockDim.x) {
+  for (long i = 4 * threadIdx.x; i < n; i += 4 * blockDim.x) {
     const int t = (int)(i / nbins), c = (int)(i % nbins);
-    float v = 0.f;
-    if (t < T) v = __fdiv_rn(__fsub_rn(feats[(long)(f0 + t) * nbins + c], s_mean[c]), s_std[c]);
-    out[(long)b * n + i] = (h16)v;
+    h16x4 o = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+    if (t < T) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(feats + (long)(f0 + t) * nbins + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (h16)__fdiv_rn(__fsub_rn(v[e], s_mean[c + e]), s_std[c + e]);
+    }
+    *reinterpret_cast<h16x4*>(out + (long)b * n + i) = o;
   }
 }
 
@@ -219,22 +202,7 @@ extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, cons
   MMS_REQUIRE(mel_range != nullptr, "fbank: mel_range required");
   if (init_consts(s)) return 1;
   if (total_frames == 0) return 0;
-  // the packed filter weights must fit the LDS table: checked once per mel_range buffer (a
-  // frontend uploads it once), so steady-state calls never synchronise the host
-  static const int32_t* g_checked = nullptr;
-  if (mel_range != g_checked) {
-    int32_t rng[512];
-    if (hipMemcpy(rng, mel_range, sizeof(int32_t) * 2 * nbins, hipMemcpyDeviceToHost) != hipSuccess) {
-      mms::set_error("fbank: mel_range read failed");
-      return 1;
-    }
-    long nz = 0;
-    for (int m = 0; m < nbins; ++m) nz += rng[2 * m + 1] - rng[2 * m];
-    MMS_REQUIRE(nz <= MEL_W_MAX, "fbank: %ld nonzero filter weights exceed the LDS table (%d)", nz, MEL_W_MAX);
-    g_checked = mel_range;
-  }
-  const int blocks = (int)std::min<long>((total_frames + 3) / 4, 2048);
-  hipLaunchKernelGGL(fbank_kernel, dim3(blocks), dim3(256), 0, s, wave, wave_off, frame_off, B,
+  hipLaunchKernelGGL(fbank_kernel, dim3((total_frames + 3) / 4), dim3(256), 0, s, wave, wave_off, frame_off, B,
                      total_frames, mel_banks, mel_range, nbins, feats);
   return mms::check_launch("fbank");
 }
@@ -242,7 +210,7 @@ extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, cons
 extern "C" int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
                                          int nbins, int cmvn, h16* out, hipStream_t s) {
   MMS_REQUIRE(nbins <= 256 && nbins % 4 == 0, "cmvn: nbins must be a multiple of 4, <= 256");
-  MMS_REQUIRE(((uintptr_t)feats & 15) == 0, "cmvn: feats must be 16-B aligned");
+  MMS_REQUIRE(((uintptr_t)feats & 15) == 0 && ((uintptr_t)out & 7) == 0, "cmvn: feats / out misaligned");
   if (B == 0) return 0;
   hipLaunchKernelGGL(cmvn_collate_kernel, dim3(B), dim3(256), 0, s, feats, frame_off, B, Tmax, nbins, cmvn, out);
   return mms::check_launch("fbank_cmvn_collate");
