@@ -142,7 +142,7 @@ MMS_DEV float xsum16_32(float v) {
 
 // ============================================================================ forward
 template <int HD, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnP P) {
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) attn_fwd_kernel(AttnP P) {
   constexpr int OWN = 16 * NW;  // query rows owned by the block (16 per wave)
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
   __shared__ __attribute__((aligned(16))) h16 sK[KB * LD];
@@ -150,7 +150,7 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnP P) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
   const int qblk = blockIdx.x * OWN;
-  const int q_own = qblk + w * 16 + (lane & 15);  // this lane's query row
+  const int w_row0 = qblk + w * 16, q_own = w_row0 + (lane & 15);  // this lane's query row
   const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
   int kmax = klen;
   if (P.causal) kmax = min(kmax, qblk + OWN);
@@ -178,6 +178,9 @@ __global__ void __launch_bounds__(64 * NW) attn_fwd_kernel(AttnP P) {
     pf.store(sK, sV);
     __syncthreads();
     if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
+    // a wave past the last query row, or whose rows all precede this key tile (causal), only
+    // helps stage K/V
+    if (w_row0 >= P.Tq || (P.causal && kb > w_row0 + 15)) continue;
     // S^T for 4 tiles of 16 keys: lane -> S[q_own][kb + 16t + 4g + r]
     f32x4 s[4];
 #pragma unroll
@@ -461,23 +464,34 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_q_kernel(AttnP P) {
 }
 
 
-// ============================================================================ backward: fused, short rows
-// One workgroup per (b, h) when Tq, Tk <= 128 (the step's typical encoder / decoder lengths): Q, K,
-// V, dO of the whole head sit in LDS, D = rowsum(dO*O) is formed while loading, and one launch
-// produces dK/dV (keys stationary, phase 2) and dQ (queries stationary, phase 3) from dS kept in
-// LDS as [key][query] — no prep launch, no second pass that re-reads Q/K/V/dO and recomputes P.
-constexpr int FT = 128;  // padded rows per head in the fused kernel
+// ============================================================================ backward: fused, Tk <= 256
+// One workgroup per (b, h) when Tk <= 256 (every length of the step's encoder / decoder / cross
+// attention): the head's K stays in LDS, each wave keeps V fragments of its own keys in registers,
+// and the queries stream through in chunks of QC rows.  Per chunk: phase 2 (keys stationary)
+// accumulates dK/dV in registers across all chunks and writes dS^T [key][query] to LDS; phase 3
+// (queries stationary) forms dQ = dS K for the chunk from LDS.  D = rowsum(dO*O) is formed while
+// the chunk is stored; the next chunk's Q/dO/O rows are loaded into registers during the current
+// chunk's MFMA phases.  No prep launch, no second pass that re-reads Q/K/V/dO and recomputes P.
+//   NKC = key chunks of 128 (1 or 2): wave w owns keys 16w + 128j (j < NKC); QC = 128 / NKC.
+template <int HD, int NKC>
+struct FusedCfg {
+  static constexpr int QC = 128 / NKC, TKP = 128 * NKC, LDS_T = QC + 8;
+  static constexpr int NQT = QC / 16, DSPLIT = 8 / NQT;
+  static constexpr int CH = HD / 8, NLQ = (QC * CH + 511) / 512, NLK = (TKP * CH + 511) / 512;
+};
 
-template <int HD>
+template <int HD, int NKC>
 __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P) {
-  constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16, CH = HD / 8, LDS_T = FT + 8;
-  constexpr int NL = (FT * CH + 511) / 512;  // 16-B chunks per thread per operand
-  __shared__ __attribute__((aligned(16))) h16 sQ[FT * LD];
-  __shared__ __attribute__((aligned(16))) h16 sK[FT * LD];
-  __shared__ __attribute__((aligned(16))) h16 sV[FT * LD];
-  __shared__ __attribute__((aligned(16))) h16 sDO[FT * LD];
-  __shared__ __attribute__((aligned(16))) h16 sDS[FT * LDS_T];  // dS^T [key][query]
-  __shared__ float sL[FT], sD[FT];
+  using F = FusedCfg<HD, NKC>;
+  constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16, CH = F::CH;
+  constexpr int QC = F::QC, TKP = F::TKP, LDS_T = F::LDS_T, NQT = F::NQT, NDW = NDT / F::DSPLIT;
+  constexpr int NLQ = F::NLQ, NLK = F::NLK;
+  static_assert(NDT % F::DSPLIT == 0, "d tiles must split evenly over the phase-3 wave pairs");
+  __shared__ __attribute__((aligned(16))) h16 sK[TKP * LD];
+  __shared__ __attribute__((aligned(16))) h16 sQ[QC * LD];
+  __shared__ __attribute__((aligned(16))) h16 sDO[QC * LD];
+  __shared__ __attribute__((aligned(16))) h16 sDS[TKP * LDS_T];  // dS^T [key][query of the chunk]
+  __shared__ float sL[2][QC], sD[2][QC];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const int z = blockIdx.x, b = z / P.H, h = z % P.H;
   const int Tq = P.Tq;
@@ -487,85 +501,112 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P) {
   const h16* V = P.v + b * P.svb + h * HD;
   const h16* O = P.o + b * P.sob + h * HD;
   const h16* DO = P.dout + b * P.sdob + h * HD;
-  // ---- phase 1: every global load of the head issued at once, then LDS stores
-  if (tid < FT) sD[tid] = 0.f;
+  const s16x8 zz = {0, 0, 0, 0, 0, 0, 0, 0};
+  // register-staged rows of one query chunk
+  s16x8 rq[NLQ], rd[NLQ], ro[NLQ];
+  float rl = 0.f;
+  auto load_chunk = [&](int qbase) {
+#pragma unroll
+    for (int n = 0; n < NLQ; ++n) {
+      const int i = tid + n * 512, r = i / CH, c = i % CH, q = qbase + r;
+      rq[n] = rd[n] = ro[n] = zz;
+      if (i < QC * CH && q < Tq) {
+        rq[n] = *reinterpret_cast<const s16x8*>(Q + (long)q * P.ldq + c * 8);
+        rd[n] = *reinterpret_cast<const s16x8*>(DO + (long)q * P.lddo + c * 8);
+        ro[n] = *reinterpret_cast<const s16x8*>(O + (long)q * P.ldo + c * 8);
+      }
+    }
+    rl = (tid < QC && qbase + tid < Tq) ? P.lse[(long)z * Tq + qbase + tid] : 0.f;
+  };
+  load_chunk(0);
+  // K of the whole head -> LDS; V fragments of the wave's own keys -> registers
   {
-    s16x8 rq[NL], rk[NL], rv[NL], rd[NL];
-    float dot[NL];
-    const s16x8 zz = {0, 0, 0, 0, 0, 0, 0, 0};
+    s16x8 rk[NLK];
 #pragma unroll
-    for (int n = 0; n < NL; ++n) {
+    for (int n = 0; n < NLK; ++n) {
       const int i = tid + n * 512, r = i / CH, c = i % CH;
-      rq[n] = rk[n] = rv[n] = rd[n] = zz;
-      dot[n] = 0.f;
-      if (i < FT * CH) {
-        if (r < Tq) {
-          rq[n] = *reinterpret_cast<const s16x8*>(Q + (long)r * P.ldq + c * 8);
-          rd[n] = *reinterpret_cast<const s16x8*>(DO + (long)r * P.lddo + c * 8);
-          const h16x8 o8 = *reinterpret_cast<const h16x8*>(O + (long)r * P.ldo + c * 8);
-          const h16x8 d8 = __builtin_bit_cast(h16x8, rd[n]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) dot[n] += (float)o8[e] * (float)d8[e];
-        }
-        if (r < klen) {
-          rk[n] = *reinterpret_cast<const s16x8*>(K + (long)r * P.ldk + c * 8);
-          rv[n] = *reinterpret_cast<const s16x8*>(V + (long)r * P.ldv + c * 8);
-        }
-      }
+      rk[n] = zz;
+      if (i < TKP * CH && r < klen) rk[n] = *reinterpret_cast<const s16x8*>(K + (long)r * P.ldk + c * 8);
     }
-    // zero dS^T (entries a causal / padded tile never writes are read as 0 by phase 3)
-    for (int i = tid; i < FT * LDS_T / 8; i += 512) reinterpret_cast<s16x8*>(sDS)[i] = zz;
-    __syncthreads();  // sD zeroed
 #pragma unroll
-    for (int n = 0; n < NL; ++n) {
+    for (int n = 0; n < NLK; ++n) {
       const int i = tid + n * 512, r = i / CH, c = i % CH;
-      if (i < FT * CH) {
-        *reinterpret_cast<s16x8*>(sQ + r * LD + c * 8) = rq[n];
-        *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
-        *reinterpret_cast<s16x8*>(sV + r * LD + c * 8) = rv[n];
-        *reinterpret_cast<s16x8*>(sDO + r * LD + c * 8) = rd[n];
-        if (r < Tq) atomicAdd(&sD[r], dot[n]);
-      }
+      if (i < TKP * CH) *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
     }
-    if (tid < FT) sL[tid] = tid < Tq ? P.lse[(long)z * Tq + tid] : 0.f;
   }
+  h16x8 vf[NKC][NKK];
+#pragma unroll
+  for (int j = 0; j < NKC; ++j) {
+    const int key = 16 * w + 128 * j + (lane & 15);
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      s16x8 t = zz;
+      if (key < klen) t = *reinterpret_cast<const s16x8*>(V + (long)key * P.ldv + kk * 32 + 8 * g);
+      vf[j][kk] = __builtin_bit_cast(h16x8, t);
+    }
+  }
+  if (tid < QC) sD[0][tid] = 0.f;
   __syncthreads();
+  f32x4 dk[NKC][NDT], dv[NKC][NDT];
+#pragma unroll
+  for (int j = 0; j < NKC; ++j)
+#pragma unroll
+    for (int i = 0; i < NDT; ++i) { dk[j][i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[j][i] = dk[j][i]; }
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
-  // ---- phase 2: wave w owns keys 16w .. 16w+15: dV, dK and dS^T
-  {
-    const int kw0 = 16 * w, key_own = kw0 + (lane & 15);
-    f32x4 dk[NDT], dv[NDT];
+  const int nch = (Tq + QC - 1) / QC;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int qbase = ch * QC, buf = ch & 1;
+    float* L = sL[buf];
+    float* Dr = sD[buf];
+    // ---- phase 1: staged rows -> LDS, D = rowsum(dO*O); prefetch the next chunk
+    __syncthreads();  // previous chunk's phase 3 is done with sDS, its phase 2 with sQ / sDO
 #pragma unroll
-    for (int i = 0; i < NDT; ++i) { dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[i] = dk[i]; }
-    if (kw0 < klen) {
-      h16x8 kf[NKK], vf[NKK];
+    for (int n = 0; n < NLQ; ++n) {
+      const int i = tid + n * 512, r = i / CH, c = i % CH;
+      if (i < QC * CH) {
+        *reinterpret_cast<s16x8*>(sQ + r * LD + c * 8) = rq[n];
+        *reinterpret_cast<s16x8*>(sDO + r * LD + c * 8) = rd[n];
+        const h16x8 o8 = __builtin_bit_cast(h16x8, ro[n]), d8 = __builtin_bit_cast(h16x8, rd[n]);
+        float dot = 0.f;
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        kf[kk] = frag_rows<HD>(sK, kw0, kk * 32, lane);
-        vf[kk] = frag_rows<HD>(sV, kw0, kk * 32, lane);
+        for (int e = 0; e < 8; ++e) dot += (float)o8[e] * (float)d8[e];
+        if (qbase + r < Tq) atomicAdd(&Dr[r], dot);
       }
-      const int q_begin = P.causal ? (kw0 / 32) * 32 : 0;
-      for (int qc = q_begin; qc < Tq; qc += 32) {
+    }
+    if (tid < QC) { L[tid] = rl; sD[buf ^ 1][tid] = 0.f; }
+    if (ch + 1 < nch) load_chunk(qbase + QC);
+    __syncthreads();
+    // ---- phase 2: wave w owns keys 16w + 128j: dV, dK accumulate, dS^T -> LDS
+#pragma unroll
+    for (int j = 0; j < NKC; ++j) {
+      const int kw0 = 16 * w + 128 * j, key_own = kw0 + (lane & 15);
+      for (int qs = 0; qs < QC; qs += 32) {
+        const int qa = qbase + qs;
+        if (kw0 >= klen || qa >= Tq || (P.causal && qa + 31 < kw0)) {
+          *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 4 * g) = h16x4{};
+          *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 16 + 4 * g) = h16x4{};
+          continue;
+        }
         f32x4 pt[2], dst[2];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
-          const int q0 = qc + 16 * tt;
+          const int q0 = qs + 16 * tt;
           f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = sc;
 #pragma unroll
           for (int kk = 0; kk < NKK; ++kk) {
-            sc = mfma(frag_rows<HD>(sQ, q0, kk * 32, lane), kf[kk], sc);
-            dp = mfma(frag_rows<HD>(sDO, q0, kk * 32, lane), vf[kk], dp);
+            sc = mfma(frag_rows<HD>(sQ, q0, kk * 32, lane), frag_rows<HD>(sK, kw0, kk * 32, lane), sc);
+            dp = mfma(frag_rows<HD>(sDO, q0, kk * 32, lane), vf[j][kk], dp);
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int q = q0 + 4 * g + r;
+            const int ql = q0 + 4 * g + r, q = qbase + ql;
             const bool ok = q < Tq && key_own < klen && (!P.causal || key_own <= q);
-            const float pr = ok ? __expf(sc[r] * P.scale - sL[q]) : 0.f;
+            const float pr = ok ? __expf(sc[r] * P.scale - L[ql]) : 0.f;
             float mk = dscale;
             if (P.thresh && ok)
               mk = mms_keep(P.seed, P.offset + ((uint64_t)z * Tq + q) * (uint64_t)P.Tk + key_own, P.thresh) ? dscale : 0.f;
             pt[tt][r] = pr * mk;
-            dst[tt][r] = pr * (dp[r] * mk - sD[q]);
+            dst[tt][r] = pr * (dp[r] * mk - Dr[ql]);
           }
           *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + q0 + 4 * g) =
               h16x4{(h16)dst[tt][0], (h16)dst[tt][1], (h16)dst[tt][2], (h16)dst[tt][3]};
@@ -574,43 +615,48 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P) {
         const h16x8 sf = pack8(dst[0], dst[1]);
 #pragma unroll
         for (int i = 0; i < NDT; ++i) {
-          dv[i] = mfma(frag_tr<HD>(sDO, qc, 16 * i, lane), pf, dv[i]);
-          dk[i] = mfma(frag_tr<HD>(sQ, qc, 16 * i, lane), sf, dk[i]);
+          dv[j][i] = mfma(frag_tr<HD>(sDO, qs, 16 * i, lane), pf, dv[j][i]);
+          dk[j][i] = mfma(frag_tr<HD>(sQ, qs, 16 * i, lane), sf, dk[j][i]);
         }
       }
     }
+    __syncthreads();
+    // ---- phase 3: query tile w % NQT, d tiles (w / NQT)*NDW ..: dQ^T[d][q] = K^T[d][keys] dS^T[keys][q]
+    {
+      const int q0 = 16 * (w % NQT), qa0 = qbase + q0, d0 = (w / NQT) * NDW, q_own = qa0 + (lane & 15);
+      if (qa0 < Tq) {
+        const int kend = P.causal ? min(klen, qa0 + 16) : klen;
+        f32x4 dq[NDW];
+#pragma unroll
+        for (int i = 0; i < NDW; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int kc = 0; kc < kend; kc += 32) {
+          const h16x8 sf = frag_tr_ld<LDS_T>(sDS, kc, q0, lane);
+#pragma unroll
+          for (int i = 0; i < NDW; ++i) dq[i] = mfma(frag_tr<HD>(sK, kc, 16 * (d0 + i), lane), sf, dq[i]);
+        }
+        if (q_own < Tq) {
+          h16* DQ = P.dq + b * P.sdqb + h * HD + (long)q_own * P.lddq;
+#pragma unroll
+          for (int i = 0; i < NDW; ++i) {
+            const f32x4 a = dq[i] * P.scale;
+            *reinterpret_cast<h16x4*>(DQ + 16 * (d0 + i) + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+          }
+        }
+      }
+    }
+  }
+  // dK, dV of the wave's own keys (keys in [klen, Tk) are written as zeros)
+#pragma unroll
+  for (int j = 0; j < NKC; ++j) {
+    const int key_own = 16 * w + 128 * j + (lane & 15);
     if (key_own < P.Tk) {
       h16* DK = P.dk + b * P.sdkb + h * HD + (long)key_own * P.lddk;
       h16* DV = P.dv + b * P.sdvb + h * HD + (long)key_own * P.lddv;
 #pragma unroll
       for (int i = 0; i < NDT; ++i) {
-        const f32x4 a = dk[i] * P.scale, c = dv[i];
+        const f32x4 a = dk[j][i] * P.scale, c = dv[j][i];
         *reinterpret_cast<h16x4*>(DK + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
         *reinterpret_cast<h16x4*>(DV + 16 * i + 4 * g) = h16x4{(h16)c[0], (h16)c[1], (h16)c[2], (h16)c[3]};
-      }
-    }
-  }
-  __syncthreads();
-  // ---- phase 3: wave w owns queries 16w .. 16w+15: dQ^T[d][q] = K^T[d][keys] dS^T[keys][q]
-  {
-    const int q0 = 16 * w, q_own = q0 + (lane & 15);
-    if (q0 < Tq) {
-      const int kend = P.causal ? min(klen, q0 + 16) : klen;
-      f32x4 dq[NDT];
-#pragma unroll
-      for (int i = 0; i < NDT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int kc = 0; kc < kend; kc += 32) {
-        const h16x8 sf = frag_tr_ld<LDS_T>(sDS, kc, q0, lane);
-#pragma unroll
-        for (int i = 0; i < NDT; ++i) dq[i] = mfma(frag_tr<HD>(sK, kc, 16 * i, lane), sf, dq[i]);
-      }
-      if (q_own < Tq) {
-        h16* DQ = P.dq + b * P.sdqb + h * HD + (long)q_own * P.lddq;
-#pragma unroll
-        for (int i = 0; i < NDT; ++i) {
-          const f32x4 a = dq[i] * P.scale;
-          *reinterpret_cast<h16x4*>(DQ + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
-        }
       }
     }
   }
@@ -656,10 +702,16 @@ extern "C" int mms2ut_mha_varlen_fwd(const mms2ut_attn_args* a, hipStream_t s) {
   if (check_common(a)) return 1;
   MMS_REQUIRE(a->lse != nullptr, "attention fwd: lse buffer required");
   AttnP P = make_params(a);
-  // 8 waves own 128 query rows: for T <= 128 each (b, h) streams its K/V exactly once
-  dim3 grid((a->Tq + 16 * ATTN_NW - 1) / (16 * ATTN_NW), a->B * a->H);
+  // each wave owns 16 query rows: 8 waves (128 rows) for Tq <= 128, else 16 waves (256 rows), so
+  // that for every length up to 256 each (b, h) streams its K/V exactly once
+  const int nw = a->Tq > 16 * ATTN_NW ? 2 * ATTN_NW : ATTN_NW;
+  dim3 grid((a->Tq + 16 * nw - 1) / (16 * nw), a->B * a->H);
   return pick_hd(a->hd, [&](auto HDc) {
-    hipLaunchKernelGGL((attn_fwd_kernel<decltype(HDc)::value, ATTN_NW>), grid, dim3(64 * ATTN_NW), 0, s, P);
+    constexpr int HD = decltype(HDc)::value;
+    if (nw == ATTN_NW)
+      hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW>), grid, dim3(64 * ATTN_NW), 0, s, P);
+    else
+      hipLaunchKernelGGL((attn_fwd_kernel<HD, 2 * ATTN_NW>), grid, dim3(128 * ATTN_NW), 0, s, P);
     return mms::check_launch("mha_varlen_fwd");
   });
 }
@@ -679,14 +731,17 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
   P.dv = dv; P.lddv = lddv; P.sdvb = sdvb ? sdvb : (long)a->Tk * lddv;
   const int Z = a->B * a->H;
   const char* fe = getenv("MMS2UT_ATTN_FUSED");
-  const bool fused_ok = !(fe && fe[0] == '0') && a->Tq <= FT && a->Tk <= FT && a->hd <= 96 &&
+  const bool fused_ok = !(fe && fe[0] == '0') && a->Tk <= 256 && a->hd <= 96 &&
                         P.ldo % 8 == 0 && P.sob % 8 == 0 && ((uintptr_t)P.o & 15) == 0 &&
                         P.lddo % 8 == 0 && P.sdob % 8 == 0 && ((uintptr_t)P.dout & 15) == 0;
   if (fused_ok) {
     return pick_hd(a->hd, [&](auto HDc) {
       constexpr int HD = decltype(HDc)::value;
       if constexpr (HD <= 96) {
-        hipLaunchKernelGGL((attn_bwd_fused_kernel<HD>), dim3(Z), dim3(512), 0, s, P);
+        if (a->Tk <= 128)
+          hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 1>), dim3(Z), dim3(512), 0, s, P);
+        else
+          hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 2>), dim3(Z), dim3(512), 0, s, P);
         return mms::check_launch("mha_varlen_bwd_fused");
       } else {
         mms::set_error("unreachable");

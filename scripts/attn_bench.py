@@ -63,3 +63,6 @@ if __name__ == "__main__":
     case(40, 250)
     case(95, 128, causal=True)
     case(32, 301, causal=True)
+    case(85, 142, causal=True)
+    case(68, 177, causal=True)
+    case(68, 250, causal=True)

@@ -216,10 +216,13 @@ def _attn_ref(q, k, v, lens, causal, scale, mask=None):
     (False, 70, 90, [90, 50, 7], 0.0), (True, 70, 70, [70, 41, 3], 0.0),
     (False, 130, 130, [130, 129, 65], 0.0), (True, 150, 150, [150, 100, 1], 0.25),
     (False, 33, 200, [200, 64, 63], 0.1), (True, 128, 128, [128, 77, 5], 0.1),
-    (False, 100, 128, [128, 100, 1], 0.2), (False, 1, 17, [17, 9, 1], 0.0)])
+    (False, 100, 128, [128, 100, 1], 0.2), (False, 1, 17, [17, 9, 1], 0.0),
+    (False, 300, 100, [100, 57, 2], 0.1), (True, 256, 256, [256, 200, 9], 0.1),
+    (False, 301, 213, [213, 129, 1], 0.1), (True, 257, 257, [257, 130, 4], 0.0)])
 @pytest.mark.parametrize("fused", ["1", "0"])
 def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p, fused, monkeypatch):
-    """fused=1: Tq, Tk <= 128 take the one-launch backward; fused=0 forces the three-kernel one."""
+    """fused=1: Tk <= 256 takes the one-launch chunked backward (any Tq); fused=0 forces the
+    three-kernel one.  Tk = 257 exercises the fallback to the three-kernel path."""
     monkeypatch.setenv("MMS2UT_ATTN_FUSED", fused)
     B, H = 3, 2
     d = H * hd
