@@ -16,6 +16,8 @@
 // stationary (kernel B); both recompute P from the saved log-sum-exp — no atomics, deterministic.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "../../include/mms2ut.h"
 
@@ -123,6 +125,17 @@ MMS_DEV h16x8 frag_tr(const h16* lds, int row0, int col0, int lane) {
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a2));
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(h16x8, v);
+}
+
+// buffer resource over `rows` rows of stride ld (elements) from base: loads of rows >= rows (or
+// rows <= 0) are out of range and return zero
+MMS_DEV __amdgpu_buffer_rsrc_t rsrc_rows(const h16* base, int rows, long ld) {
+  const int bytes = rows > 0 ? (int)(rows * ld * 2) : 0;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+MMS_DEV s16x8 ld16b(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }
 
 MMS_DEV f32x4 mfma(h16x8 a, h16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -481,7 +494,7 @@ struct FusedCfg {
 };
 
 template <int HD, int NKC>
-__global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P) {
+__global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
   using F = FusedCfg<HD, NKC>;
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16, CH = F::CH;
   constexpr int QC = F::QC, TKP = F::TKP, LDS_T = F::LDS_T, NQT = F::NQT, NDW = NDT / F::DSPLIT;
@@ -491,175 +504,234 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P) {
   __shared__ __attribute__((aligned(16))) h16 sQ[QC * LD];
   __shared__ __attribute__((aligned(16))) h16 sDO[QC * LD];
   __shared__ __attribute__((aligned(16))) h16 sDS[TKP * LDS_T];  // dS^T [key][query of the chunk]
-  __shared__ float sL[2][QC], sD[2][QC];
+  __shared__ __attribute__((aligned(16))) float sL[2][QC];
+  __shared__ __attribute__((aligned(16))) float sD[2][QC];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
-  const int z = blockIdx.x, b = z / P.H, h = z % P.H;
-  const int Tq = P.Tq;
-  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
-  const h16* Q = P.q + b * P.sqb + h * HD;
-  const h16* K = P.k + b * P.skb + h * HD;
-  const h16* V = P.v + b * P.svb + h * HD;
-  const h16* O = P.o + b * P.sob + h * HD;
-  const h16* DO = P.dout + b * P.sdob + h * HD;
+  const int Tq = P.Tq, nch = (Tq + QC - 1) / QC;
   const s16x8 zz = {0, 0, 0, 0, 0, 0, 0, 0};
-  // register-staged rows of one query chunk
-  s16x8 rq[NLQ], rd[NLQ], ro[NLQ];
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  // register staging: the rows of one query chunk, K of one head, V fragments of the wave's keys
+  s16x8 rq[NLQ], rd[NLQ], ro[NLQ], rk[NLK];
   float rl = 0.f;
-  auto load_chunk = [&](int qbase) {
+  h16x8 vf[NKC][NKK];
+  // Loads go through buffer resources built per head / chunk (SGPRs): rows past the valid range
+  // fall outside num_records and read as zero, and the per-thread offsets stay 32-bit.
+  auto load_chunk = [&](int zc, int qbase) {
+    int tid_ = tid;
+    asm volatile("" : "+v"(tid_));
+    const int tid = tid_;
+    const int bc = zc / P.H, hc = zc % P.H, rows = Tq - qbase;
+    const auto rQ = rsrc_rows(P.q + bc * P.sqb + hc * HD + (long)qbase * P.ldq, rows, P.ldq);
+    const auto rD = rsrc_rows(P.dout + bc * P.sdob + hc * HD + (long)qbase * P.lddo, rows, P.lddo);
+    const auto rO = rsrc_rows(P.o + bc * P.sob + hc * HD + (long)qbase * P.ldo, rows, P.ldo);
 #pragma unroll
     for (int n = 0; n < NLQ; ++n) {
-      const int i = tid + n * 512, r = i / CH, c = i % CH, q = qbase + r;
-      rq[n] = rd[n] = ro[n] = zz;
-      if (i < QC * CH && q < Tq) {
-        rq[n] = *reinterpret_cast<const s16x8*>(Q + (long)q * P.ldq + c * 8);
-        rd[n] = *reinterpret_cast<const s16x8*>(DO + (long)q * P.lddo + c * 8);
-        ro[n] = *reinterpret_cast<const s16x8*>(O + (long)q * P.ldo + c * 8);
+      const int i = tid + n * 512, r = i / CH, c = i % CH;
+      if (QC * CH % 512 == 0 || i < QC * CH) {  // straight-line when every thread loads
+        rq[n] = ld16b(rQ, (r * (int)P.ldq + c * 8) * 2);
+        rd[n] = ld16b(rD, (r * (int)P.lddo + c * 8) * 2);
+        ro[n] = ld16b(rO, (r * (int)P.ldo + c * 8) * 2);
       }
     }
-    rl = (tid < QC && qbase + tid < Tq) ? P.lse[(long)z * Tq + qbase + tid] : 0.f;
+    // LSE of the chunk's rows (threads >= QC load a value nobody reads; rows >= Tq read 0)
+    const __amdgpu_buffer_rsrc_t rL = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(P.lse + (long)zc * Tq + qbase), (short)0, rows > 0 ? rows * 4 : 0, 0x00020000);
+    rl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rL, tid * 4, 0, 0));
   };
-  load_chunk(0);
-  // K of the whole head -> LDS; V fragments of the wave's own keys -> registers
-  {
-    s16x8 rk[NLK];
+  auto load_kv = [&](int zc) {
+    int tid_ = tid;
+    asm volatile("" : "+v"(tid_));
+    const int tid = tid_, lane = tid & 63, g = lane >> 4, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int bc = zc / P.H, hc = zc % P.H;
+    const int kl = P.key_len ? min(P.key_len[bc], P.Tk) : P.Tk;
+    const auto rK = rsrc_rows(P.k + bc * P.skb + hc * HD, kl, P.ldk);
+    const auto rV = rsrc_rows(P.v + bc * P.svb + hc * HD, kl, P.ldv);
 #pragma unroll
     for (int n = 0; n < NLK; ++n) {
       const int i = tid + n * 512, r = i / CH, c = i % CH;
-      rk[n] = zz;
-      if (i < TKP * CH && r < klen) rk[n] = *reinterpret_cast<const s16x8*>(K + (long)r * P.ldk + c * 8);
+      if (TKP * CH % 512 == 0 || i < TKP * CH) rk[n] = ld16b(rK, (r * (int)P.ldk + c * 8) * 2);
     }
+#pragma unroll
+    for (int j = 0; j < NKC; ++j) {
+      const int key = 16 * w + 128 * j + (lane & 15);
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk)
+        vf[j][kk] = __builtin_bit_cast(h16x8, ld16b(rV, (key * (int)P.ldv + kk * 32 + 8 * g) * 2));
+    }
+  };
+  // persistent: block handles heads blockIdx.x, + gridDim.x, ...; the next head's rows, K and V
+  // are loaded into registers while the current head's MFMA phases run
+  int z = blockIdx.x;
+  if (z >= Z) return;
+  load_chunk(z, 0);
+  load_kv(z);
+  if (tid < QC) sD[0][tid] = 0.f;
+  int gc = 0;  // running chunk counter: parity selects the sL / sD buffer
+  for (; z < Z; z += gridDim.x) {
+    const int b = z / P.H, h = z % P.H, znext = z + gridDim.x;
+    const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+    __syncthreads();  // the previous head's phase 3 is done with sK
 #pragma unroll
     for (int n = 0; n < NLK; ++n) {
       const int i = tid + n * 512, r = i / CH, c = i % CH;
       if (i < TKP * CH) *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
     }
-  }
-  h16x8 vf[NKC][NKK];
+    f32x4 dk[NKC][NDT], dv[NKC][NDT];
 #pragma unroll
-  for (int j = 0; j < NKC; ++j) {
-    const int key = 16 * w + 128 * j + (lane & 15);
+    for (int j = 0; j < NKC; ++j)
 #pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {
-      s16x8 t = zz;
-      if (key < klen) t = *reinterpret_cast<const s16x8*>(V + (long)key * P.ldv + kk * 32 + 8 * g);
-      vf[j][kk] = __builtin_bit_cast(h16x8, t);
-    }
-  }
-  if (tid < QC) sD[0][tid] = 0.f;
-  __syncthreads();
-  f32x4 dk[NKC][NDT], dv[NKC][NDT];
+      for (int i = 0; i < NDT; ++i) { dk[j][i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[j][i] = dk[j][i]; }
+    // one query chunk; the last chunk of the head also writes dK / dV and prefetches the next head
+    // (peeled, so that the next head's K stays out of the register live range of phase 2)
+    auto chunk = [&](const int ch, auto last_c) {
+      constexpr bool LAST = decltype(last_c)::value;
+      // per-thread indices re-derived from an opaque copy of tid: keeps the compiler from hoisting
+      // dozens of per-lane offsets / counters out of the head loop (they would spill)
+      int tl = tid;
+      asm volatile("" : "+v"(tl));
+      const int lane = tl & 63, g = lane >> 4, w = __builtin_amdgcn_readfirstlane(tl >> 6);
+      const int qbase = ch * QC, buf = gc & 1;
+      float* L = sL[buf];
+      float* Dr = sD[buf];
+      const uint64_t zctr = P.offset + (uint64_t)z * Tq * (uint64_t)P.Tk;  // RNG counter of (z, 0, 0)
+      const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)Tq * P.Tk - 1);  // uniform
+      const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
+      // ---- phase 1: staged rows -> LDS, D = rowsum(dO*O); prefetch the next chunk / head
+      __syncthreads();  // previous chunk's phase 3 is done with sDS, its phase 2 with sQ / sDO
 #pragma unroll
-  for (int j = 0; j < NKC; ++j)
+      for (int n = 0; n < NLQ; ++n) {
+        const int i = tid + n * 512, r = i / CH, c = i % CH;
+        if (i < QC * CH) {
+          *reinterpret_cast<s16x8*>(sQ + r * LD + c * 8) = rq[n];
+          *reinterpret_cast<s16x8*>(sDO + r * LD + c * 8) = rd[n];
+          const h16x8 o8 = __builtin_bit_cast(h16x8, ro[n]), d8 = __builtin_bit_cast(h16x8, rd[n]);
+          float dot = 0.f;
 #pragma unroll
-    for (int i = 0; i < NDT; ++i) { dk[j][i] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[j][i] = dk[j][i]; }
-  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
-  const int nch = (Tq + QC - 1) / QC;
-  for (int ch = 0; ch < nch; ++ch) {
-    const int qbase = ch * QC, buf = ch & 1;
-    float* L = sL[buf];
-    float* Dr = sD[buf];
-    // ---- phase 1: staged rows -> LDS, D = rowsum(dO*O); prefetch the next chunk
-    __syncthreads();  // previous chunk's phase 3 is done with sDS, its phase 2 with sQ / sDO
-#pragma unroll
-    for (int n = 0; n < NLQ; ++n) {
-      const int i = tid + n * 512, r = i / CH, c = i % CH;
-      if (i < QC * CH) {
-        *reinterpret_cast<s16x8*>(sQ + r * LD + c * 8) = rq[n];
-        *reinterpret_cast<s16x8*>(sDO + r * LD + c * 8) = rd[n];
-        const h16x8 o8 = __builtin_bit_cast(h16x8, ro[n]), d8 = __builtin_bit_cast(h16x8, rd[n]);
-        float dot = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dot += (float)o8[e] * (float)d8[e];
-        if (qbase + r < Tq) atomicAdd(&Dr[r], dot);
-      }
-    }
-    if (tid < QC) { L[tid] = rl; sD[buf ^ 1][tid] = 0.f; }
-    if (ch + 1 < nch) load_chunk(qbase + QC);
-    __syncthreads();
-    // ---- phase 2: wave w owns keys 16w + 128j: dV, dK accumulate, dS^T -> LDS
-#pragma unroll
-    for (int j = 0; j < NKC; ++j) {
-      const int kw0 = 16 * w + 128 * j, key_own = kw0 + (lane & 15);
-      for (int qs = 0; qs < QC; qs += 32) {
-        const int qa = qbase + qs;
-        if (kw0 >= klen || qa >= Tq || (P.causal && qa + 31 < kw0)) {
-          *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 4 * g) = h16x4{};
-          *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 16 + 4 * g) = h16x4{};
-          continue;
-        }
-        f32x4 pt[2], dst[2];
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          const int q0 = qs + 16 * tt;
-          f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = sc;
-#pragma unroll
-          for (int kk = 0; kk < NKK; ++kk) {
-            sc = mfma(frag_rows<HD>(sQ, q0, kk * 32, lane), frag_rows<HD>(sK, kw0, kk * 32, lane), sc);
-            dp = mfma(frag_rows<HD>(sDO, q0, kk * 32, lane), vf[j][kk], dp);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ql = q0 + 4 * g + r, q = qbase + ql;
-            const bool ok = q < Tq && key_own < klen && (!P.causal || key_own <= q);
-            const float pr = ok ? __expf(sc[r] * P.scale - L[ql]) : 0.f;
-            float mk = dscale;
-            if (P.thresh && ok)
-              mk = mms_keep(P.seed, P.offset + ((uint64_t)z * Tq + q) * (uint64_t)P.Tk + key_own, P.thresh) ? dscale : 0.f;
-            pt[tt][r] = pr * mk;
-            dst[tt][r] = pr * (dp[r] * mk - Dr[ql]);
-          }
-          *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + q0 + 4 * g) =
-              h16x4{(h16)dst[tt][0], (h16)dst[tt][1], (h16)dst[tt][2], (h16)dst[tt][3]};
-        }
-        const h16x8 pf = pack8(pt[0], pt[1]);
-        const h16x8 sf = pack8(dst[0], dst[1]);
-#pragma unroll
-        for (int i = 0; i < NDT; ++i) {
-          dv[j][i] = mfma(frag_tr<HD>(sDO, qs, 16 * i, lane), pf, dv[j][i]);
-          dk[j][i] = mfma(frag_tr<HD>(sQ, qs, 16 * i, lane), sf, dk[j][i]);
+          for (int e = 0; e < 8; ++e) dot += (float)o8[e] * (float)d8[e];
+          if (qbase + r < Tq) atomicAdd(&Dr[r], dot);
         }
       }
-    }
-    __syncthreads();
-    // ---- phase 3: query tile w % NQT, d tiles (w / NQT)*NDW ..: dQ^T[d][q] = K^T[d][keys] dS^T[keys][q]
-    {
-      const int q0 = 16 * (w % NQT), qa0 = qbase + q0, d0 = (w / NQT) * NDW, q_own = qa0 + (lane & 15);
-      if (qa0 < Tq) {
-        const int kend = P.causal ? min(klen, qa0 + 16) : klen;
-        f32x4 dq[NDW];
+      if (tid < QC) { L[tid] = rl; sD[buf ^ 1][tid] = 0.f; }
+      if (!LAST) load_chunk(z, qbase + QC);
+      else if (znext < Z) load_chunk(znext, 0);
+      __syncthreads();
+      // ---- phase 2: wave w owns keys 16w + 128j: dV, dK accumulate, dS^T -> LDS
 #pragma unroll
-        for (int i = 0; i < NDW; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int kc = 0; kc < kend; kc += 32) {
-          const h16x8 sf = frag_tr_ld<LDS_T>(sDS, kc, q0, lane);
+      for (int j = 0; j < NKC; ++j) {
+        const int kw0 = 16 * w + 128 * j, key_own = kw0 + (lane & 15);
+        for (int qs = 0; qs < QC; qs += 32) {
+          const int qa = qbase + qs;
+          if (kw0 >= klen || qa >= Tq || (P.causal && qa + 31 < kw0)) {
+            *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 4 * g) = h16x4{};
+            *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 16 + 4 * g) = h16x4{};
+            continue;
+          }
+          f32x4 pt[2], dst[2];
 #pragma unroll
-          for (int i = 0; i < NDW; ++i) dq[i] = mfma(frag_tr<HD>(sK, kc, 16 * (d0 + i), lane), sf, dq[i]);
-        }
-        if (q_own < Tq) {
-          h16* DQ = P.dq + b * P.sdqb + h * HD + (long)q_own * P.lddq;
+          for (int tt = 0; tt < 2; ++tt) {
+            const int q0 = qs + 16 * tt;
+            f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = sc;
 #pragma unroll
-          for (int i = 0; i < NDW; ++i) {
-            const f32x4 a = dq[i] * P.scale;
-            *reinterpret_cast<h16x4*>(DQ + 16 * (d0 + i) + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+            for (int kk = 0; kk < NKK; ++kk) {
+              sc = mfma(frag_rows<HD>(sQ, q0, kk * 32, lane), frag_rows<HD>(sK, kw0, kk * 32, lane), sc);
+              dp = mfma(frag_rows<HD>(sDO, q0, kk * 32, lane), vf[j][kk], dp);
+            }
+            const f32x4 Lv = *reinterpret_cast<const f32x4*>(L + q0 + 4 * g);
+            const f32x4 Dv = *reinterpret_cast<const f32x4*>(Dr + q0 + 4 * g);
+            // dropout keep flags, branch-free; one mixer per element on the fast path
+            bool keep[4] = {true, true, true, true};
+            if (P.thresh) {
+              const uint64_t c0 = zctr + (uint32_t)((qbase + q0 + 4 * g) * P.Tk + key_own);
+              if (hi_fast) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) keep[r] = mms_keep_hi(hi_mix, c0 + (uint32_t)(r * P.Tk), P.thresh);
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) keep[r] = mms_keep(P.seed, c0 + (uint32_t)(r * P.Tk), P.thresh);
+              }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int q = qbase + q0 + 4 * g + r;
+              const bool ok = q < Tq && key_own < klen && (!P.causal || key_own <= q);
+              const float pr = ok ? __expf(sc[r] * P.scale - Lv[r]) : 0.f;
+              const float mk = keep[r] ? dscale : 0.f;
+              pt[tt][r] = pr * mk;
+              dst[tt][r] = pr * (dp[r] * mk - Dv[r]);
+            }
+            *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + q0 + 4 * g) =
+                h16x4{(h16)dst[tt][0], (h16)dst[tt][1], (h16)dst[tt][2], (h16)dst[tt][3]};
+          }
+          const h16x8 pf = pack8(pt[0], pt[1]);
+          const h16x8 sf = pack8(dst[0], dst[1]);
+#pragma unroll
+          for (int i = 0; i < NDT; ++i) {
+            dv[j][i] = mfma(frag_tr<HD>(sDO, qs, 16 * i, lane), pf, dv[j][i]);
+            dk[j][i] = mfma(frag_tr<HD>(sQ, qs, 16 * i, lane), sf, dk[j][i]);
           }
         }
       }
-    }
-  }
-  // dK, dV of the wave's own keys (keys in [klen, Tk) are written as zeros)
+      if constexpr (LAST) {
+        // dK, dV of the wave's own keys (keys in [klen, Tk) are written as zeros); then the next
+        // head's K / V start loading behind phase 3
 #pragma unroll
-  for (int j = 0; j < NKC; ++j) {
-    const int key_own = 16 * w + 128 * j + (lane & 15);
-    if (key_own < P.Tk) {
-      h16* DK = P.dk + b * P.sdkb + h * HD + (long)key_own * P.lddk;
-      h16* DV = P.dv + b * P.sdvb + h * HD + (long)key_own * P.lddv;
+        for (int j = 0; j < NKC; ++j) {
+          const int key_own = 16 * w + 128 * j + (lane & 15);
+          if (key_own < P.Tk) {
+            h16* DK = P.dk + b * P.sdkb + h * HD + (long)key_own * P.lddk;
+            h16* DV = P.dv + b * P.sdvb + h * HD + (long)key_own * P.lddv;
 #pragma unroll
-      for (int i = 0; i < NDT; ++i) {
-        const f32x4 a = dk[j][i] * P.scale, c = dv[j][i];
-        *reinterpret_cast<h16x4*>(DK + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
-        *reinterpret_cast<h16x4*>(DV + 16 * i + 4 * g) = h16x4{(h16)c[0], (h16)c[1], (h16)c[2], (h16)c[3]};
+            for (int i = 0; i < NDT; ++i) {
+              const f32x4 a = dk[j][i] * P.scale, c = dv[j][i];
+              *reinterpret_cast<h16x4*>(DK + 16 * i + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+              *reinterpret_cast<h16x4*>(DV + 16 * i + 4 * g) = h16x4{(h16)c[0], (h16)c[1], (h16)c[2], (h16)c[3]};
+            }
+          }
+        }
+        if (znext < Z) load_kv(znext);
       }
-    }
+      __syncthreads();
+      // ---- phase 3: query tile w % NQT, d tiles (w / NQT)*NDW ..: dQ^T[d][q] = K^T[d][keys] dS^T[keys][q]
+      {
+        const int q0 = 16 * (w % NQT), qa0 = qbase + q0, d0 = (w / NQT) * NDW, q_own = qa0 + (lane & 15);
+        if (qa0 < Tq) {
+          const int kend = P.causal ? min(klen, qa0 + 16) : klen;
+          f32x4 dq[NDW];
+#pragma unroll
+          for (int i = 0; i < NDW; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int kc = 0; kc < kend; kc += 32) {
+            const h16x8 sf = frag_tr_ld<LDS_T>(sDS, kc, q0, lane);
+#pragma unroll
+            for (int i = 0; i < NDW; ++i) dq[i] = mfma(frag_tr<HD>(sK, kc, 16 * (d0 + i), lane), sf, dq[i]);
+          }
+          if (q_own < Tq) {
+            h16* DQ = P.dq + b * P.sdqb + h * HD + (long)q_own * P.lddq;
+#pragma unroll
+            for (int i = 0; i < NDW; ++i) {
+              const f32x4 a = dq[i] * P.scale;
+              *reinterpret_cast<h16x4*>(DQ + 16 * (d0 + i) + 4 * g) = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+            }
+          }
+        }
+      }
+      ++gc;
+    };
+    for (int ch = 0; ch + 1 < nch; ++ch) chunk(ch, std::false_type{});
+    chunk(nch - 1, std::true_type{});
   }
+}
+
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
+      n = c;
+    else
+      n = 256;
+  }
+  return n;
 }
 
 template <typename F>
@@ -738,10 +810,14 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
     return pick_hd(a->hd, [&](auto HDc) {
       constexpr int HD = decltype(HDc)::value;
       if constexpr (HD <= 96) {
+        // persistent grid: one block per CU (the kernel's LDS allows no second), each looping
+        // over heads so that the next head's loads overlap the current head's MFMA phases
+        const char* pe = getenv("MMS2UT_ATTN_PERSIST");
+        const int grid = (pe && pe[0] == '0') ? Z : std::min(Z, num_cus());
         if (a->Tk <= 128)
-          hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 1>), dim3(Z), dim3(512), 0, s, P);
+          hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 1>), dim3(grid), dim3(512), 0, s, P, Z);
         else
-          hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 2>), dim3(Z), dim3(512), 0, s, P);
+          hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 2>), dim3(grid), dim3(512), 0, s, P, Z);
         return mms::check_launch("mha_varlen_bwd_fused");
       } else {
         mms::set_error("unreachable");
