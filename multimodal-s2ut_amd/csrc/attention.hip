@@ -184,6 +184,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   float m = -INFINITY, l = 0.f;
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
+  const uint64_t zctr = P.offset + (uint64_t)z * P.Tq * P.Tk;
+  const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)P.Tq * P.Tk - 1);  // uniform per head
+  const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
   Pair64<HD, 64 * NW> pf;
   if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
   for (int kb = 0; kb < kmax; kb += KB) {
@@ -220,7 +223,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bool keep[4] = {true, true, true, true};
-      if (P.thresh) mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+      if (P.thresh) {
+        if (hi_fast) mms_keep4_hi(hi_mix, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+        else mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float e = (s[t][r] == -INFINITY) ? 0.f : __expf(s[t][r] - mn);
@@ -431,6 +437,9 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_q_kernel(AttnP P) {
   for (int i = 0; i < NDT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
+  const uint64_t zctr = P.offset + (uint64_t)z * P.Tq * P.Tk;
+  const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)P.Tq * P.Tk - 1);  // uniform per head
+  const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
   Pair64<HD, 64 * NW> pf;
   if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
   for (int kb = 0; kb < kmax; kb += KB) {
@@ -448,7 +457,10 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_q_kernel(AttnP P) {
         dp = mfma(frag_rows<HD>(sV, 16 * t, kk * 32, lane), df[kk], dp);
       }
       bool keep[4] = {true, true, true, true};
-      if (P.thresh) mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+      if (P.thresh) {
+        if (hi_fast) mms_keep4_hi(hi_mix, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+        else mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kb + 16 * t + 4 * g + r;

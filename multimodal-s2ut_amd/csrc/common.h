@@ -82,6 +82,19 @@ MMS_DEV bool mms_keep_hi(uint32_t hi_mix, uint64_t ctr, uint32_t thresh) {
   const uint32_t h = mms_mix32((uint32_t)(ctr >> 1) ^ hi_mix);
   return ((ctr & 1) ? (h >> 16) : (h & 0xffffU)) >= thresh;
 }
+MMS_DEV void mms_keep4_hi(uint32_t hi_mix, uint64_t ctr0, uint32_t thresh, bool (&k)[4]) {
+  if ((ctr0 & 1) == 0) {
+    const uint32_t p0 = (uint32_t)(ctr0 >> 1);
+    const uint32_t h0 = mms_mix32(p0 ^ hi_mix), h1 = mms_mix32((p0 + 1) ^ hi_mix);
+    k[0] = (h0 & 0xffffU) >= thresh;
+    k[1] = (h0 >> 16) >= thresh;
+    k[2] = (h1 & 0xffffU) >= thresh;
+    k[3] = (h1 >> 16) >= thresh;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) k[e] = mms_keep_hi(hi_mix, ctr0 + e, thresh);
+  }
+}
 static inline uint32_t mms_drop_thresh(float p) {
   if (p <= 0.f) return 0u;
   double t = (double)p * 65536.0 + 0.5;
