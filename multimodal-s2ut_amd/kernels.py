@@ -196,20 +196,17 @@ def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=Fa
 
 
 def _splitk_for(tiles, kred, slots=512):
-    """split-K count for a weight gradient (reduction over kred token rows).  8 slices map one
-    slice to each XCD (tile_coords keeps a z slice on one XCD), so every XCD streams its own rows
-    of dy and x exactly once through its private L2; measured faster than filling the 512 block
-    slots with more, thinner slices (scripts/gemm_bench.py).  Fewer slices when rows are scarce or
-    the tile grid alone fills the chip."""
-    if tiles >= 2 * slots:
-        return 1
-    cap = int(os.environ.get("MMS2UT_WGRAD_SPLITK", "8"))
-    for s in (8, 4, 2):
-        if s > cap:
-            continue
-        if kred // s >= 512:
-            return s
-    return 1
+    """split-K count for a weight gradient (reduction over kred token rows): the largest s whose
+    tiles*s blocks still fit one round of the 512 block slots (2 per CU), so every block runs
+    concurrently and no partial second round trails (scripts/wgrad_sweep.py, isolated GEMM +
+    slab reduction on the step's shapes: fc 3072x768 s3 vs the old fixed s8, qkv 2304x768 s4
+    49 vs 60 us, cross-KV 9216x768 s1 174 vs 234 us).  MMS2UT_WGRAD_SPLITK caps s."""
+    cap = int(os.environ.get("MMS2UT_WGRAD_SPLITK", "16"))
+    slots = int(os.environ.get("MMS2UT_WGRAD_SLOTS", slots))
+    s = max(1, min(cap, slots // max(tiles, 1)))
+    while s > 1 and kred // s < 256:
+        s -= 1
+    return s
 
 
 class _Side:
