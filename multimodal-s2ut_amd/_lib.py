@@ -6,7 +6,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libmms2ut_hip.so")
+LIB_PATH = os.environ.get("MMS2UT_LIB") or os.path.join(HERE, "lib", "libmms2ut_hip.so")  # override: A/B builds
 
 vp, i32, i64, u64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_float
 
