@@ -824,8 +824,11 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
       if constexpr (HD <= 96) {
         // persistent grid: one block per CU (the kernel's LDS allows no second), each looping
         // over heads so that the next head's loads overlap the current head's MFMA phases
+        // MMS2UT_ATTN_PERSIST=0: one block per head; =N>1: at most N blocks (tests use a small N
+        // so that every block walks several heads / chunks through the prefetch path)
         const char* pe = getenv("MMS2UT_ATTN_PERSIST");
-        const int grid = (pe && pe[0] == '0') ? Z : std::min(Z, num_cus());
+        const int cap = pe ? atoi(pe) : 0;
+        const int grid = (pe && pe[0] == '0') ? Z : std::min(Z, cap > 1 ? cap : num_cus());
         if (a->Tk <= 128)
           hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 1>), dim3(grid), dim3(512), 0, s, P, Z);
         else

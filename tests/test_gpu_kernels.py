@@ -219,11 +219,14 @@ def _attn_ref(q, k, v, lens, causal, scale, mask=None):
     (False, 100, 128, [128, 100, 1], 0.2), (False, 1, 17, [17, 9, 1], 0.0),
     (False, 300, 100, [100, 57, 2], 0.1), (True, 256, 256, [256, 200, 9], 0.1),
     (False, 301, 213, [213, 129, 1], 0.1), (True, 257, 257, [257, 130, 4], 0.0)])
-@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("fused", ["1", "0", "grid2"])
 def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p, fused, monkeypatch):
     """fused=1: Tk <= 256 takes the one-launch chunked backward (any Tq); fused=0 forces the
-    three-kernel one.  Tk = 257 exercises the fallback to the three-kernel path."""
-    monkeypatch.setenv("MMS2UT_ATTN_FUSED", fused)
+    three-kernel one.  Tk = 257 exercises the fallback to the three-kernel path.  grid2: the fused
+    kernel runs on 2 persistent blocks, so each block walks 3 heads (next-head prefetch path)."""
+    monkeypatch.setenv("MMS2UT_ATTN_FUSED", "0" if fused == "0" else "1")
+    if fused == "grid2":
+        monkeypatch.setenv("MMS2UT_ATTN_PERSIST", "2")
     B, H = 3, 2
     d = H * hd
     g = torch.Generator(device="cuda").manual_seed(5)
