@@ -130,6 +130,22 @@ int mms2ut_layernorm_bwd(const mms2ut_half* dy, const mms2ut_half* x, const mms2
                          mms2ut_half* dx, float* part, int64_t rows, int D, mms2ut_half* dxd,
                          float p, uint64_t seed, uint64_t offset, hipStream_t stream);
 int mms2ut_layernorm_bwd_parts(int64_t rows);
+/* layernorm_fwd with an output layout and dropout folded in (the fusion image path,
+ * mm_s2s_transformer.py:188-190 image_pre_norm -> SA_image_dropout -> [B, Ti(+1), Di] keys):
+ * input row r is written to output row (r / grp) * grp_out + r % grp (grp = 0: identity), and
+ * y = dropout_p(LN(x)) with counters offset + r*D + col (the unpadded element index).         */
+int mms2ut_layernorm_fwd_ex(const mms2ut_half* x, const mms2ut_half* gamma, const mms2ut_half* beta,
+                            mms2ut_half* y, float* mean, float* rstd, int64_t rows, int D, float eps,
+                            int64_t grp, int64_t grp_out, float p, uint64_t seed, uint64_t offset,
+                            hipStream_t stream);
+/* layernorm_bwd whose dy is read through the same layout (row r from (r / dy_grp) * dy_grp_out +
+ * r % dy_grp) and dropout (dy_p, dy_seed, dy_offset; unpadded counters): the backward of
+ * layernorm_fwd_ex without materialising the unpadded, dropped-out gradient.  D % 256 == 0.    */
+int mms2ut_layernorm_bwd_ex(const mms2ut_half* dy, const mms2ut_half* x, const mms2ut_half* gamma,
+                            const float* mean, const float* rstd, const mms2ut_half* dres,
+                            mms2ut_half* dx, float* part, int64_t rows, int D, mms2ut_half* dxd,
+                            float p, uint64_t seed, uint64_t offset, int64_t dy_grp, int64_t dy_grp_out,
+                            float dy_p, uint64_t dy_seed, uint64_t dy_offset, hipStream_t stream);
 /* column sums of fp32 partials [nparts][ncol] -> out (fp16), out += if accumulate */
 int mms2ut_colsum_parts(const float* part, int nparts, int ncol, mms2ut_half* out, int accumulate,
                         hipStream_t stream);

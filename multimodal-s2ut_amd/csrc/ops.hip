@@ -26,7 +26,8 @@ template <int CPL>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, const h16* __restrict__ g,
                                                      const h16* __restrict__ b, h16* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     long rows, int D, float eps) {
+                                                     long rows, int D, float eps, long grp, long grp_out,
+                                                     float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -58,7 +59,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, 
   }
   const float rstd = rsqrtf(wave_sum(ss) / D + eps);
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
-  h16* yr = y + row * D;
+  // optional output layout: row r of group r / grp lands at (r / grp) * grp_out + r % grp (the
+  // fusion attention's [B, Ti+1, Di] key layout); optional dropout on the fp16 result with the
+  // counters of the unpadded element index (as a separate dropout pass over y would use)
+  const long orow = grp ? (row / grp) * grp_out + row % grp : row;
+  h16* yr = y + orow * D;
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int ch = lane + c * 64;
@@ -67,6 +73,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, 
       float o[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (v[c][e] - mean) * rstd * (float)gg[e] + (float)bb[e];
+      if (thresh) {
+        bool k[4];
+        mms_keep4(seed, offset + (uint64_t)(row * D + ch * 4), thresh, k);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = k[e] ? (float)(h16)o[e] * ds : 0.f;
+      }
       st4(yr + ch * 4, o[0], o[1], o[2], o[3]);
     }
   }
@@ -198,7 +210,9 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
                                                        const float* __restrict__ rstd, const h16* __restrict__ dres,
                                                        h16* __restrict__ dx, float* __restrict__ part,
                                                        long rows, int D, h16* __restrict__ dxd, float p,
-                                                       uint32_t thresh, uint64_t seed, uint64_t offset) {
+                                                       uint32_t thresh, uint64_t seed, uint64_t offset,
+                                                       long dgrp, long dgrp_out, float pin, uint32_t thin,
+                                                       uint64_t sin, uint64_t oin) {
   __shared__ __attribute__((aligned(16))) float red[4][2][C8 * 256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
   const float dscale = thresh ? 1.f / (1.f - p) : 1.f;
@@ -225,9 +239,30 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
     for (int c = 0; c < C8; ++c) {
       const long off = row[k] * D + (hl + 32 * c) * 8;
       xv[k][c] = ok ? *reinterpret_cast<const h16x8*>(x + off) : z8;
-      dv[k][c] = ok ? *reinterpret_cast<const h16x8*>(dy + off) : z8;
+      // optional dy layout remap (rows grouped dgrp at a time into dgrp_out-row groups)
+      const long drow = dgrp ? (row[k] / dgrp) * dgrp_out + row[k] % dgrp : row[k];
+      dv[k][c] = ok ? *reinterpret_cast<const h16x8*>(dy + drow * D + (hl + 32 * c) * 8) : z8;
       rv[k][c] = (ok && dres && dx) ? *reinterpret_cast<const h16x8*>(dres + off) : z8;
     }
+  }
+  if (thin) {
+    // dy = dropout(dy_in) with the counters of the unpadded element index, rounded to fp16 as a
+    // separate dropout pass would store it
+    const float dsi = 1.f / (1.f - pin);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int c = 0; c < C8; ++c) {
+        bool k0[4], k1[4];
+        const uint64_t ctr = oin + (uint64_t)(row[k] * D + (hl + 32 * c) * 8);
+        mms_keep4(sin, ctr, thin, k0);
+        mms_keep4(sin, ctr + 4, thin, k1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          dv[k][c][e] = (h16)(k0[e] ? (float)dv[k][c][e] * dsi : 0.f);
+          dv[k][c][e + 4] = (h16)(k1[e] ? (float)dv[k][c][e + 4] * dsi : 0.f);
+        }
+      }
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -712,8 +747,26 @@ extern "C" int mms2ut_layernorm_fwd(const h16* x, const h16* gamma, const h16* b
   if (rows == 0) return 0;
   return pick_cpl(D / 4, [&](auto C) {
     hipLaunchKernelGGL((ln_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
-                       x, gamma, beta, y, mean, rstd, (long)rows, D, eps);
+                       x, gamma, beta, y, mean, rstd, (long)rows, D, eps, 0L, 0L, 0.f, 0u, (uint64_t)0,
+                       (uint64_t)0);
     return mms::check_launch("layernorm_fwd");
+  });
+}
+
+extern "C" int mms2ut_layernorm_fwd_ex(const h16* x, const h16* gamma, const h16* beta, h16* y,
+                                       float* mean, float* rstd, int64_t rows, int D, float eps,
+                                       int64_t grp, int64_t grp_out, float p, uint64_t seed,
+                                       uint64_t offset, hipStream_t s) {
+  MMS_REQUIRE(D % 4 == 0, "layernorm_fwd_ex: D must be a multiple of 4");
+  MMS_REQUIRE(grp >= 0 && (grp == 0 || grp_out >= grp), "layernorm_fwd_ex: need grp_out >= grp");
+  MMS_REQUIRE(p < 1.f, "layernorm_fwd_ex: p must be < 1");
+  if (rows == 0) return 0;
+  const uint32_t th = mms_drop_thresh(p);
+  return pick_cpl(D / 4, [&](auto C) {
+    hipLaunchKernelGGL((ln_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
+                       x, gamma, beta, y, mean, rstd, (long)rows, D, eps, (long)grp, (long)grp_out, p, th,
+                       seed, offset);
+    return mms::check_launch("layernorm_fwd_ex");
   });
 }
 
@@ -735,7 +788,8 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
   if (D % 256 == 0 && D <= 1024 && !(e16 && e16[0] == '0')) {
     switch (D / 256) {
 #define CASE(C) case C: hipLaunchKernelGGL((ln_bwd16_kernel<C>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, rstd, \
-                                          dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset); break;
+                                          dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset, 0L, 0L, \
+                                          0.f, 0u, (uint64_t)0, (uint64_t)0); break;
       CASE(1) CASE(2) CASE(3) CASE(4)
 #undef CASE
     }
@@ -752,6 +806,28 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
       return 1;
     }
   });
+}
+
+extern "C" int mms2ut_layernorm_bwd_ex(const h16* dy, const h16* x, const h16* gamma, const float* mean,
+                                       const float* rstd, const h16* dres, h16* dx, float* part,
+                                       int64_t rows, int D, h16* dxd, float p, uint64_t seed, uint64_t offset,
+                                       int64_t dy_grp, int64_t dy_grp_out, float dy_p, uint64_t dy_seed,
+                                       uint64_t dy_offset, hipStream_t s) {
+  MMS_REQUIRE(!dxd || dx, "layernorm_bwd_ex: dxd needs dx");
+  MMS_REQUIRE(p < 1.f && dy_p < 1.f, "layernorm_bwd_ex: p must be < 1");
+  MMS_REQUIRE(D % 256 == 0 && D <= 1024, "layernorm_bwd_ex: D must be a multiple of 256 and <= 1024");
+  MMS_REQUIRE(dy_grp >= 0 && (dy_grp == 0 || dy_grp_out >= dy_grp), "layernorm_bwd_ex: need dy_grp_out >= dy_grp");
+  if (rows == 0) return 0;
+  const int nb = mms2ut_layernorm_bwd_parts(rows);
+  const uint32_t thresh = mms_drop_thresh(p), thin = mms_drop_thresh(dy_p);
+  switch (D / 256) {
+#define CASE(C) case C: hipLaunchKernelGGL((ln_bwd16_kernel<C>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, rstd, \
+                                          dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset, \
+                                          (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset); break;
+    CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+  }
+  return mms::check_launch("layernorm_bwd_ex");
 }
 
 extern "C" int mms2ut_colsum_parts(const float* part, int nparts, int ncol, h16* out, int accumulate,

@@ -374,20 +374,45 @@ def bias_grad(dy, db, accumulate=False, side=True):
 # ============================================================================ LayerNorm
 
 
-def layernorm(x, g, b, eps=1e-5):
+def layernorm(x, g, b, eps=1e-5, *, out=None, grp=0, grp_out=0, p=0.0, drop=None):
+    """y = LN(x).  With out/grp/grp_out/p the result goes to row (r // grp) * grp_out + r % grp of
+    out (a padded layout) after dropout_p with the unpadded counters (layernorm_fwd_ex)."""
     R, D = x.shape
-    y = torch.empty_like(x)
     mean = torch.empty(R, dtype=torch.float32, device=x.device)
     rstd = torch.empty(R, dtype=torch.float32, device=x.device)
-    call("mms2ut_layernorm_fwd", x.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(),
-         mean.data_ptr(), rstd.data_ptr(), R, D, eps, _s())
+    if out is None and not grp and p == 0.0:
+        y = torch.empty_like(x)
+        call("mms2ut_layernorm_fwd", x.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(),
+             mean.data_ptr(), rstd.data_ptr(), R, D, eps, _s())
+        return y, mean, rstd
+    y = torch.empty_like(x) if out is None else out
+    assert y.is_contiguous() and y.shape[-1] == D
+    seed, off = drop if p > 0 else (0, 0)
+    call("mms2ut_layernorm_fwd_ex", x.data_ptr(), g.data_ptr(), b.data_ptr(), y.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), R, D, eps, int(grp), int(grp_out), float(p), seed, off, _s())
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None):
+def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None, dy_grp=0, dy_grp_out=0,
+                  dy_p=0.0, dy_drop=None):
     """Returns dx (+dres). dgb: fp16 view of [dgamma | dbeta] (2*D contiguous).
-    emit=(p, (seed, offset)): also return dropout(dx) for the sublayer below -> (dx, dxd)."""
+    emit=(p, (seed, offset)): also return dropout(dx) for the sublayer below -> (dx, dxd).
+    dy_grp/dy_grp_out/dy_p: dy is read through layernorm(out=, grp=, p=)'s layout and dropout."""
     R, D = x.shape
+    if dy_grp or dy_p > 0:
+        assert emit is None and D % 256 == 0 and D <= 1024
+        L = _lib.load()
+        nparts = L.mms2ut_layernorm_bwd_parts(R)
+        part = torch.empty(nparts, 2 * D, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x) if want_dx else None
+        seed, off = dy_drop if dy_p > 0 else (0, 0)
+        call("mms2ut_layernorm_bwd_ex", dy.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr(),
+             rstd.data_ptr(), _p(dres), _p(dx), part.data_ptr(), R, D, None, 0.0, 0, 0, int(dy_grp),
+             int(dy_grp_out), float(dy_p), seed, off, _s())
+        ctx = side_begin(part)
+        with (ctx or _NULLCTX):
+            call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), 0, _s())
+        return dx
     L = _lib.load()
     nparts = L.mms2ut_layernorm_bwd_parts(R)
     part = torch.empty(nparts, 2 * D, dtype=torch.float32, device=x.device)

@@ -624,22 +624,36 @@ class MMS2UTModel:
         c = {"B": B, "Te": Te, "Ti": Ti, "Di": Di, "Tk": Tk, "extra": extra}
         # image_pre_norm (+ dropout), laid out [B, Tk, Di] with a zero row per batch for bias_kv
         img2 = img.reshape(B * Ti, Di)
-        if cfg["image_pre_norm"]:
-            imgn, c["im"], c["ir"] = K.layernorm(img2, self.P("encoder.image_pre_norm_module.weight"),
-                                                 self.P("encoder.image_pre_norm_module.bias"))
-            c["img_in"] = img2
-        else:
-            imgn = img2
         pimg = self._p("SA_image_dropout")
         c["drop_img"] = self._drop(pimg, B * Ti * Di)
-        if pimg > 0:
-            imgn = K.dropout(imgn, pimg, c["drop_img"])
-        if extra:
-            imgd = torch.zeros(B, Tk, Di, dtype=F16, device=img.device)
-            K.copy2d(imgn.view(B, Ti * Di), imgd.view(B, Tk * Di), B, Ti * Di)
+        c["ln_fused"] = cfg["image_pre_norm"] and Di % 256 == 0 and Di <= 1024
+        if c["ln_fused"]:
+            # LN -> dropout -> [B, Tk, Di] key layout in one pass (layernorm_fwd_ex); the extra
+            # bias_kv row per batch is zeroed separately
+            imgd = torch.empty(B, Tk, Di, dtype=F16, device=img.device)
+            if extra:
+                imgd[:, Ti:].zero_()
+            _, c["im"], c["ir"] = K.layernorm(img2, self.P("encoder.image_pre_norm_module.weight"),
+                                              self.P("encoder.image_pre_norm_module.bias"), out=imgd,
+                                              grp=Ti if extra else 0, grp_out=Tk if extra else 0, p=pimg,
+                                              drop=c["drop_img"])
+            c["img_in"] = img2
             imgd = imgd.view(B * Tk, Di)
         else:
-            imgd = imgn
+            if cfg["image_pre_norm"]:
+                imgn, c["im"], c["ir"] = K.layernorm(img2, self.P("encoder.image_pre_norm_module.weight"),
+                                                     self.P("encoder.image_pre_norm_module.bias"))
+                c["img_in"] = img2
+            else:
+                imgn = img2
+            if pimg > 0:
+                imgn = K.dropout(imgn, pimg, c["drop_img"])
+            if extra:
+                imgd = torch.zeros(B, Tk, Di, dtype=F16, device=img.device)
+                K.copy2d(imgn.view(B, Ti * Di), imgd.view(B, Tk * Di), B, Ti * Di)
+                imgd = imgd.view(B * Tk, Di)
+            else:
+                imgd = imgn
         c["imgd"] = imgd
         ptxt = self._p("SA_text_dropout")
         c["drop_txt"] = self._drop(ptxt, B * Te * d)
@@ -740,7 +754,15 @@ class MMS2UTModel:
             rows.zero_()
         K.linear_wgrad(dkv, c["imgd"], gWkv,
                        db=gbkv)
-        if cfg["image_pre_norm"]:
+        if c["ln_fused"]:
+            # image LN gamma/beta grads read dimgd through the key layout + dropout directly
+            dimgd = K.linear_dgrad(dkv, Wkv)
+            K.layernorm_bwd(dimgd, c["img_in"], self.P("encoder.image_pre_norm_module.weight"), c["im"], c["ir"],
+                            self.params.span("encoder.image_pre_norm_module.weight",
+                                             "encoder.image_pre_norm_module.bias", grad=True),
+                            want_dx=False, dy_grp=Ti if extra else 0, dy_grp_out=Tk if extra else 0,
+                            dy_p=c["pimg"], dy_drop=c["drop_img"])
+        elif cfg["image_pre_norm"]:
             dimgd = K.linear_dgrad(dkv, Wkv)
             if extra:
                 dimg = torch.empty(B * Ti, Di, dtype=F16, device=dkv.device)

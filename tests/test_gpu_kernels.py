@@ -113,6 +113,36 @@ def test_wgrad_splitk(K):
     assert rel(dW, dy.float().t() @ x.float()) < 2e-3
 
 
+@pytest.mark.parametrize("extra", [True, False])
+def test_layernorm_padded_dropout(K, extra):
+    """layernorm_fwd_ex / layernorm_bwd_ex (the fusion image path) are bit-identical to the unfused
+    LN -> dropout -> copy into the [B, Ti+1, D] key layout, and to the copy-back -> dropout -> LN
+    backward (gamma/beta grads)."""
+    B, Ti, D, p, drop = 3, 37, 768, 0.1, (11, 8192)
+    Tk = Ti + 1 if extra else Ti
+    x = (2 * torch.randn(B * Ti, D, device="cuda") + 0.5).half()
+    g = (1 + 0.1 * torch.randn(D, device="cuda")).half()
+    b = (0.1 * torch.randn(D, device="cuda")).half()
+    y0, m0, r0 = K.layernorm(x, g, b)
+    ref = torch.zeros(B, Tk, D, dtype=torch.float16, device="cuda")
+    ref[:, :Ti] = K.dropout(y0, p, drop).view(B, Ti, D)
+    out = torch.full((B, Tk, D), 7.0, dtype=torch.float16, device="cuda")
+    if extra:
+        out[:, Ti:].zero_()
+    _, m1, r1 = K.layernorm(x, g, b, out=out, grp=Ti if extra else 0, grp_out=Tk if extra else 0, p=p,
+                            drop=drop)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and torch.equal(m0, m1) and torch.equal(r0, r1)
+    dyp = torch.randn(B * Tk, D, device="cuda").half()
+    dy = K.dropout(dyp.view(B, Tk, D)[:, :Ti].clone().view(B * Ti, D), p, drop)
+    dgb0, dgb1 = (torch.empty(2 * D, dtype=torch.float16, device="cuda") for _ in range(2))
+    K.layernorm_bwd(dy, x, g, m0, r0, dgb0, want_dx=False)
+    K.layernorm_bwd(dyp, x, g, m0, r0, dgb1, want_dx=False, dy_grp=Ti if extra else 0,
+                    dy_grp_out=Tk if extra else 0, dy_p=p, dy_drop=drop)
+    torch.cuda.synchronize()
+    assert torch.equal(dgb0, dgb1)
+
+
 @pytest.mark.parametrize("ln16", ["1", "0"])
 def test_layernorm_fwd_bwd(K, ln16, monkeypatch):
     """ln16=1: D % 256 == 0 takes the 16-B half-wave-per-row backward; 0 forces the 8-B one."""
