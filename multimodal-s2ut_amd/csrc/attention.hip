@@ -154,12 +154,16 @@ MMS_DEV float xsum16_32(float v) {
 }
 
 // ============================================================================ forward
-template <int HD, int NW>
+// SHORT (Tk <= 128): the head's whole K / V (<= 2 tiles) is loaded into LDS in one burst up front
+// — one load latency per block instead of one per 64-key tile — and the tile loop runs without
+// barriers.
+template <int HD, int NW, bool SHORT = false>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) attn_fwd_kernel(AttnP P) {
   constexpr int OWN = 16 * NW;  // query rows owned by the block (16 per wave)
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
-  __shared__ __attribute__((aligned(16))) h16 sK[KB * LD];
-  __shared__ __attribute__((aligned(16))) h16 sV[KB * LD];
+  constexpr int KROWS = SHORT ? 2 * KB : KB;
+  __shared__ __attribute__((aligned(16))) h16 sK[KROWS * LD];
+  __shared__ __attribute__((aligned(16))) h16 sV[KROWS * LD];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
   const int qblk = blockIdx.x * OWN;
@@ -188,12 +192,40 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)P.Tq * P.Tk - 1);  // uniform per head
   const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
   Pair64<HD, 64 * NW> pf;
-  if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
+  if constexpr (SHORT) {
+    constexpr int CH = HD / 8, NLS = (KROWS * CH + 64 * NW - 1) / (64 * NW);
+    const auto rK = rsrc_rows(K, kmax, P.ldk);
+    const auto rV = rsrc_rows(V, kmax, P.ldv);
+    s16x8 rk[NLS], rv[NLS];
+#pragma unroll
+    for (int n = 0; n < NLS; ++n) {
+      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
+      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) {
+        rk[n] = ld16b(rK, (r * (int)P.ldk + c * 8) * 2);  // rows >= kmax read as zero
+        rv[n] = ld16b(rV, (r * (int)P.ldv + c * 8) * 2);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NLS; ++n) {
+      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
+      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) {
+        *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
+        *reinterpret_cast<s16x8*>(sV + r * LD + c * 8) = rv[n];
+      }
+    }
+    __syncthreads();
+  } else {
+    if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
+  }
   for (int kb = 0; kb < kmax; kb += KB) {
-    __syncthreads();
-    pf.store(sK, sV);
-    __syncthreads();
-    if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
+    const h16* tK = SHORT ? sK + kb * LD : sK;
+    const h16* tV = SHORT ? sV + kb * LD : sV;
+    if constexpr (!SHORT) {
+      __syncthreads();
+      pf.store(sK, sV);
+      __syncthreads();
+      if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
+    }
     // a wave past the last query row, or whose rows all precede this key tile (causal), only
     // helps stage K/V
     if (w_row0 >= P.Tq || (P.causal && kb > w_row0 + 15)) continue;
@@ -203,7 +235,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
     for (int t = 0; t < 4; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) s[t] = mfma(frag_rows<HD>(sK, 16 * t, kk * 32, lane), qf[kk], s[t]);
+      for (int kk = 0; kk < NKK; ++kk) s[t] = mfma(frag_rows<HD>(tK, 16 * t, kk * 32, lane), qf[kk], s[t]);
     }
     float bmax = -INFINITY;
 #pragma unroll
@@ -244,7 +276,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
     for (int c = 0; c < 2; ++c) {
       const h16x8 pf = pack8(s[2 * c], s[2 * c + 1]);
 #pragma unroll
-      for (int i = 0; i < NDT; ++i) o[i] = mfma(frag_tr<HD>(sV, 32 * c, 16 * i, lane), pf, o[i]);
+      for (int i = 0; i < NDT; ++i) o[i] = mfma(frag_tr<HD>(tV, 32 * c, 16 * i, lane), pf, o[i]);
     }
   }
   if (q_own < P.Tq) {
@@ -792,10 +824,15 @@ extern "C" int mms2ut_mha_varlen_fwd(const mms2ut_attn_args* a, hipStream_t s) {
   dim3 grid((a->Tq + 16 * nw - 1) / (16 * nw), a->B * a->H);
   return pick_hd(a->hd, [&](auto HDc) {
     constexpr int HD = decltype(HDc)::value;
-    if (nw == ATTN_NW)
-      hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW>), grid, dim3(64 * ATTN_NW), 0, s, P);
-    else
-      hipLaunchKernelGGL((attn_fwd_kernel<HD, 2 * ATTN_NW>), grid, dim3(128 * ATTN_NW), 0, s, P);
+    const char* se = getenv("MMS2UT_ATTN_FWD_SHORT");
+    const bool short_k = a->Tk <= 2 * KB && !(se && se[0] == '0') && P.ldk < (1L << 24) && P.ldv < (1L << 24);
+    if (nw == ATTN_NW) {
+      if (short_k) hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW, true>), grid, dim3(64 * ATTN_NW), 0, s, P);
+      else hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW>), grid, dim3(64 * ATTN_NW), 0, s, P);
+    } else {
+      if (short_k) hipLaunchKernelGGL((attn_fwd_kernel<HD, 2 * ATTN_NW, true>), grid, dim3(128 * ATTN_NW), 0, s, P);
+      else hipLaunchKernelGGL((attn_fwd_kernel<HD, 2 * ATTN_NW>), grid, dim3(128 * ATTN_NW), 0, s, P);
+    }
     return mms::check_launch("mha_varlen_fwd");
   });
 }
