@@ -237,6 +237,10 @@ int mms2ut_glu_bwd(const mms2ut_half* x, const mms2ut_half* dy, mms2ut_half* dx,
  * ordered (c, k) to match the PyTorch weight [out][C][k] (fairseq Conv1dSubsampler)          */
 int mms2ut_im2col(const mms2ut_half* x, mms2ut_half* col, int B, int Tin, int Tout, int C, int k,
                   int stride, int pad, hipStream_t stream);
+/* im2col with a row stride ldcol >= C*k; columns [C*k, ldcol) are zero (K padded to whole GEMM
+ * k-tiles: the first conv's C*k = 80*5 = 400 -> 448)                                          */
+int mms2ut_im2col_ld(const mms2ut_half* x, mms2ut_half* col, int B, int Tin, int Tout, int C, int k,
+                     int stride, int pad, int ldcol, hipStream_t stream);
 int mms2ut_col2im(const mms2ut_half* dcol, mms2ut_half* dx, int B, int Tin, int Tout, int C, int k,
                   int stride, int pad, hipStream_t stream);
 /* fusion gate backward (mm_s2s_transformer.py:613-618):

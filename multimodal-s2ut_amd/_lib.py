@@ -90,6 +90,7 @@ SIGNATURES = {
     "mms2ut_glu_fwd": (i32, [vp, vp, i64, i32, vp]),
     "mms2ut_glu_bwd": (i32, [vp, vp, vp, i64, i32, vp]),
     "mms2ut_im2col": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+    "mms2ut_im2col_ld": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mms2ut_col2im": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mms2ut_gate_bwd": (i32, [vp, vp, vp, vp, vp, i64, i32, vp]),
     "mms2ut_copy2d": (i32, [vp, i64, vp, i64, i64, i32, vp]),

@@ -88,6 +88,9 @@ __global__ void __launch_bounds__(256) ls_xent_bwd_kernel(const h16* __restrict_
       *reinterpret_cast<h16x4*>(dz + row * ld + j0) = h16x4{(h16)o[0], (h16)o[1], (h16)o[2], (h16)o[3]};
     }
   }
+  // pad columns [V, ld) are written as zeros: the tied-embedding dgrad reduces over a K padded to
+  // whole 64-wide k-tiles
+  for (long j = V + lane; j < ld; j += 64) dz[row * ld + j] = (h16)0.f;
 }
 
 __global__ void grad_sqnorm_kernel(const h16* __restrict__ g, long n, float* __restrict__ part) {

@@ -657,17 +657,19 @@ __global__ void glu_bwd_kernel(const h16* __restrict__ x, const h16* __restrict_
 }
 
 // col[(b,t)][c*k + kk] = x[b][t*stride - pad + kk][c]
+// col rows are ldcol >= C*k wide; columns [C*k, ldcol) are written as zeros (a K padded to whole
+// 64-wide k-tiles for the LDS-DMA GEMM)
 __global__ void im2col_kernel(const h16* __restrict__ x, h16* __restrict__ col, int B, int Tin,
-                              int Tout, int C, int k, int stride, int pad) {
-  const long W = (long)C * k;
-  const long n = (long)B * Tout * W;
+                              int Tout, int C, int k, int stride, int pad, int ldcol) {
+  const int W = C * k;
+  const long n = (long)B * Tout * ldcol;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long bt = i / W;
-    const int rem = (int)(i % W);
+    const long bt = i / ldcol;
+    const int rem = (int)(i % ldcol);
     const int c = rem / k, kk = rem % k;
     const int b = (int)(bt / Tout), t = (int)(bt % Tout);
     const int ti = t * stride - pad + kk;
-    col[i] = (ti >= 0 && ti < Tin) ? x[((long)b * Tin + ti) * C + c] : (h16)0.f;
+    col[i] = (rem < W && ti >= 0 && ti < Tin) ? x[((long)b * Tin + ti) * C + c] : (h16)0.f;
   }
 }
 
@@ -976,13 +978,19 @@ extern "C" int mms2ut_glu_bwd(const h16* x, const h16* dy, h16* dx, int64_t rows
   return mms::check_launch("glu_bwd");
 }
 
-extern "C" int mms2ut_im2col(const h16* x, h16* col, int B, int Tin, int Tout, int C, int k, int stride,
-                             int pad, hipStream_t s) {
-  const long n = (long)B * Tout * C * k;
+extern "C" int mms2ut_im2col_ld(const h16* x, h16* col, int B, int Tin, int Tout, int C, int k, int stride,
+                                int pad, int ldcol, hipStream_t s) {
+  MMS_REQUIRE(ldcol >= C * k, "im2col: ldcol < C*k");
+  const long n = (long)B * Tout * ldcol;
   if (n == 0) return 0;
   hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, col, B, Tin, Tout, C, k,
-                     stride, pad);
+                     stride, pad, ldcol);
   return mms::check_launch("im2col");
+}
+
+extern "C" int mms2ut_im2col(const h16* x, h16* col, int B, int Tin, int Tout, int C, int k, int stride,
+                             int pad, hipStream_t s) {
+  return mms2ut_im2col_ld(x, col, B, Tin, Tout, C, k, stride, pad, C * k, s);
 }
 
 extern "C" int mms2ut_col2im(const h16* dcol, h16* dx, int B, int Tin, int Tout, int C, int k, int stride,

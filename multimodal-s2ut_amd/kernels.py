@@ -564,10 +564,12 @@ def glu_bwd(x, dy, C):
     return dx
 
 
-def im2col(x, B, Tin, Tout, C, k, stride=2, pad=None):
+def im2col(x, B, Tin, Tout, C, k, stride=2, pad=None, ldcol=None):
+    """col [B*Tout, ldcol] (ldcol >= C*k, zero columns past C*k)."""
     pad = k // 2 if pad is None else pad
-    col = torch.empty(B * Tout, C * k, dtype=F16, device=x.device)
-    call("mms2ut_im2col", x.data_ptr(), col.data_ptr(), B, Tin, Tout, C, k, stride, pad, _s())
+    ldcol = C * k if ldcol is None else ldcol
+    col = torch.empty(B * Tout, ldcol, dtype=F16, device=x.device)
+    call("mms2ut_im2col_ld", x.data_ptr(), col.data_ptr(), B, Tin, Tout, C, k, stride, pad, ldcol, _s())
     return col
 
 

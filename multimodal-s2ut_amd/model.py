@@ -361,6 +361,7 @@ class MMS2UTModel:
         # autograd anchor: the model's output is connected to the graph through this leaf
         self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
         self.wt = None  # K.TransposedWeights of the dgrad weights (built at the first training forward)
+        self._wpad = {}  # subsampler conv weights zero-padded to whole 64-wide k-tiles (subsample_fwd)
 
     def dgrad_weights(self):
         """Every weight matrix the hand-written backward multiplies a gradient by (dx = dy @ W),
@@ -506,8 +507,23 @@ class MMS2UTModel:
             W = self.P(f"encoder.subsample.conv_layers.{i}.weight")
             bias = self.P(f"encoder.subsample.conv_layers.{i}.bias")
             Tout = (Tin - 1) // 2 + 1
-            col = K.im2col(x, B, Tin, Tout, C, k)
-            y = K.linear(col, W.view(W.shape[0], -1), bias)
+            W2 = W.view(W.shape[0], -1)
+            ck = C * k
+            if ck % 64:
+                # K = C*k padded to whole 64-wide k-tiles (zero columns in col and in a padded copy
+                # of W) so the projection runs on the LDS-DMA GEMM instead of the predicated one
+                kp = -(-ck // 64) * 64
+                col = K.im2col(x, B, Tin, Tout, C, k, ldcol=kp)
+                Wp = self._wpad.get(i)
+                if Wp is None or Wp.shape != (W2.shape[0], kp):
+                    Wp = torch.zeros(W2.shape[0], kp, dtype=F16, device=W.device)
+                    self._wpad[i] = Wp
+                K.copy2d(W2, Wp, W2.shape[0], ck)
+                y = K.linear(col, Wp, bias)
+                col = col[:, :ck]
+            else:
+                col = K.im2col(x, B, Tin, Tout, C, k)
+                y = K.linear(col, W2, bias)
             Cg = W.shape[0] // 2
             g = K.glu(y, Cg)
             ctx["layers"].append(dict(col=col, y=y, Tin=Tin, Tout=Tout, C=C, k=k, Cg=Cg))
@@ -999,7 +1015,7 @@ class MMS2UTModel:
         self.params.await_all()   # "dec_ln" and anything not consumed above
         xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("decoder.layer_norm.weight"), self.P("decoder.layer_norm.bias"))
         ctx["lx"], ctx["xl"] = x, xl
-        Vp = round_up(V, 8)
+        Vp = round_up(V, 64)  # whole k-tiles for the tied-embedding dgrad (pad columns of dlogits are 0)
         logits = torch.empty(B * Tt, Vp, dtype=F16, device=x.device)
         E = self.P("decoder.embed_tokens.weight")
         K.gemm(xl, E, logits, B * Tt, V, d, lda=d, ldb=d, ldc=Vp)
@@ -1017,7 +1033,15 @@ class MMS2UTModel:
         # order, accumulating into dE32 (zeroed here on the main stream before the fork).
         K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32)
         dxl = torch.empty(B * Tt, d, dtype=F16, device=E.device)
-        K.gemm(dlogits, E, dxl, B * Tt, d, V, a_kc=True, b_kc=False, lda=ctx["Vp"], ldb=d, ldc=d)
+        # dxl = dlogits E over K = Vp: E zero-padded to Vp rows (refreshed per step), so the GEMM
+        # runs on the LDS-DMA path (K % 64 == 0) instead of the predicated one
+        Vp = ctx["Vp"]
+        Ep = self._wpad.get("embed")
+        if Ep is None or Ep.shape != (Vp, d):
+            Ep = torch.zeros(Vp, d, dtype=F16, device=E.device)
+            self._wpad["embed"] = Ep
+        K.copy2d(E, Ep, V, d)
+        K.gemm(dlogits, Ep, dxl, B * Tt, d, Vp, a_kc=True, b_kc=False, lda=Vp, ldb=d, ldc=d)
         layers = ctx["layers"]
         L = cfg["decoder_layers"]
         emit = lambda l: (layers[l]["pd"], layers[l]["drop3"]) if l >= 0 else None  # noqa: E731

@@ -112,7 +112,7 @@ class _ModelFn(torch.autograd.Function):
 
 
 def model_logits(model, batch):
-    """Padded logits [B*Tt, round8(V)] fp16 (autograd-connected through the hand-written bwd)."""
+    """Padded logits [B*Tt, round64(V)] fp16 (autograd-connected through the hand-written bwd)."""
     return _ModelFn.apply(model.anchor, model, batch)
 
 

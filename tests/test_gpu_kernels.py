@@ -312,9 +312,11 @@ def test_ls_xent(K):
     loss.backward()
     g = torch.tensor([3.0], device="cuda")
     dz = torch.empty_like(logits)
+    dz.fill_(float("nan"))
     K.ls_xent_bwd(logits, Vp, target, rows, V, eps, pad, lse, g, dz)
     torch.cuda.synchronize()
     assert rel(dz[:, :V], 3 * z.grad) < 2e-3
+    assert torch.equal(dz[:, V:], torch.zeros_like(dz[:, V:]))  # pad columns zeroed
 
 
 def test_glu_im2col_col2im(K):
