@@ -22,6 +22,13 @@
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+#ifndef MMS_GEMM_PRIO
+#define MMS_GEMM_PRIO 1
+#endif
+// raise wave priority around the MFMA block of a k-step — for the fp16-output (forward / dgrad,
+// critical-path) GEMMs only, so that their waves win issue slots over the side stream's
+// weight-gradient (fp32 slab) GEMM waves sharing a CU
+constexpr bool PRIO = MMS_GEMM_PRIO;
 constexpr int TILE_BYTES = 128 * 64 * 2;  // 16 KiB per operand per stage
 
 struct GemmP {
@@ -610,11 +617,13 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
       for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
+      if (PRIO && EPI != MMS_EPI_F32) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      if (PRIO && EPI != MMS_EPI_F32) __builtin_amdgcn_s_setprio(0);
       if (RS && do_rs) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) rs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, fa[i], rs[i], 0, 0, 0);
