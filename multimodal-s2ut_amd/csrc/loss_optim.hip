@@ -1,4 +1,6 @@
 // Label-smoothed cross entropy (fused fp32 log-softmax) and the FP16Optimizer/Adam update.
+#include <algorithm>
+
 #include "common.h"
 #include "../../include/mms2ut.h"
 
@@ -12,9 +14,10 @@ __global__ void __launch_bounds__(256) ls_xent_fwd_kernel(const h16* __restrict_
                                                           float* __restrict__ loss_out) {
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long row = (long)blockIdx.x * 4 + w;
   float loss = 0.f, nll = 0.f;
-  if (row < rows) {
+  // grid-stride over rows: a bounded grid keeps the two same-address float atomics per block few
+  // (one per block for ~3k blocks serialised into a ~70 us tail)
+  for (long row = (long)blockIdx.x * 4 + w; row < rows; row += (long)gridDim.x * 4) {
     const h16* zr = z + row * ld;
     float v[CPL][4];
     float mx = -INFINITY, sum = 0.f;
@@ -44,9 +47,10 @@ __global__ void __launch_bounds__(256) ls_xent_fwd_kernel(const h16* __restrict_
     if (t != pad) {
       const float zt = (float)zr[t];
       const float eps_i = eps / (V - 1);
-      nll = lse - zt;
+      const float nl = lse - zt;
       const float smooth = V * lse - sum;
-      loss = (1.f - eps - eps_i) * nll + eps_i * smooth;
+      nll += nl;
+      loss += (1.f - eps - eps_i) * nl + eps_i * smooth;
     }
   }
   if (lane == 0) { red[0][w] = loss; red[1][w] = nll; }
@@ -211,7 +215,8 @@ extern "C" int mms2ut_ls_xent_fwd(const h16* logits, int64_t ld, const int64_t* 
   MMS_REQUIRE(ld % 4 == 0 && ld >= V, "ls_xent: ld must be a multiple of 4 and >= V");
   if (rows == 0) return 0;
   return pick_cpl_v(V, [&](auto C) {
-    hipLaunchKernelGGL((ls_xent_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
+    const long nb = std::min<long>((rows + 3) / 4, 512);
+    hipLaunchKernelGGL((ls_xent_fwd_kernel<decltype(C)::value>), dim3(nb), dim3(256), 0, s,
                        logits, (long)ld, target, (long)rows, V, eps, pad_idx, lse, loss_out);
     return mms::check_launch("ls_xent_fwd");
   });
