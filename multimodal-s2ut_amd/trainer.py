@@ -59,7 +59,9 @@ class Trainer:
         # zeroed after the forward: by then every deferred optimizer chunk of the previous step
         # (which reads the gradients) has been waited for (ParamStore.await_group)
         m.params.await_all()
-        m.params.grad.zero_()
+        if not getattr(m.params, "grad_zeroed", False):
+            m.params.grad.zero_()
+        m.params.grad_zeroed = False
         loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
                                               cfg["label_smoothing"], cfg["padding_idx"])
         del logits
