@@ -1,4 +1,4 @@
-"""Per-step breakdown of a rocprofv3 kernel trace of bench.py (steps delimited by adam_kernel).
+"""Per-step breakdown of a rocprofv3 kernel trace of bench.py (steps start at fbank_kernel).
 
 usage: python scripts/analyze_trace.py gpurun_out/prof/run_kernel_trace.csv [--step -2] [--list]
 Prints: step wall time, busy time per stream, per-kernel totals for that step, and with --list every
@@ -25,10 +25,9 @@ def main():
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    starts = [i for i, r in enumerate(rows) if "fbank_kernel" in r["Kernel_Name"]] + [len(rows)]
     s = a.step
-    lo = ends[s - 1] + 1 if (s - 1) >= -len(ends) else 0
-    hi = ends[s] + 1
+    lo, hi = starts[s - 1], starts[s]
     step = rows[lo:hi]
     t0 = int(step[0]["Start_Timestamp"])
     t1 = max(int(r["End_Timestamp"]) for r in step)

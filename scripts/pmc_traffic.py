@@ -30,8 +30,9 @@ def main():
     a = ap.parse_args()
     F = load(a.fetch + "/run_counter_collection.csv")
     W = {r["Dispatch_Id"]: float(r["Counter_Value"]) for r in load(a.write + "/run_counter_collection.csv")}
-    ends = [i for i, r in enumerate(F) if "adam_kernel" in r["Kernel_Name"]]
-    step = F[ends[-2] + 1: ends[-1] + 1]
+    # steps start at the fbank launch (the optimizer is chunked and deferred into the next step)
+    starts = [i for i, r in enumerate(F) if "fbank_kernel" in r["Kernel_Name"]]
+    step = F[starts[-2]: starts[-1]]
     per = defaultdict(lambda: [0, 0.0, 0.0])
     tot = [0.0, 0.0]
     for r in step:

@@ -14,8 +14,8 @@ def short(name):
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 8
-ends = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
-rows = rows[ends[-n - 1] + 1: ends[-1] + 1]
+starts = [i for i, r in enumerate(rows) if "fbank_kernel" in r["Kernel_Name"]]
+rows = rows[starts[-n - 1]: starts[-1]]
 t0, t1 = int(rows[0]["Start_Timestamp"]), max(int(r["End_Timestamp"]) for r in rows)
 print(f"{n} steps, wall {(t1 - t0) / 1e3 / n:.1f} us/step")
 agg = defaultdict(lambda: defaultdict(float))
