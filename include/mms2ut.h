@@ -306,6 +306,15 @@ int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, const int32_t* 
                      float* feats, hipStream_t stream);
 int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
                               int nbins, int cmvn, mms2ut_half* out, hipStream_t stream);
+/* fairseq SpecAugmentTransform (feature_transforms/specaugment.py, the `specaugment` entry of
+ * the data config's `_train` transforms, applied after utterance_cmvn by
+ * speech_to_speech_dataset.py:271-272), in place on the collated features x [B][Tmax][nbins].
+ * masks[b]: n_freq (f0, width) pairs then n_time (t0, width) pairs, drawn on the host; width 0 =
+ * no mask.  use_const = 0: mask value = the utterance's mean over its valid [T][nbins] region
+ * (the transform's mask_value=None default); otherwise mask_value.  Time warp is not built.   */
+int mms2ut_specaugment_f16(mms2ut_half* x, const int32_t* frame_off, int B, int Tmax, int nbins,
+                           const int32_t* masks, int n_freq, int n_time, int use_const,
+                           float mask_value, hipStream_t stream);
 
 #ifdef __cplusplus
 }

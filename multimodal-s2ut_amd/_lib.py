@@ -104,6 +104,7 @@ SIGNATURES = {
     "mms2ut_fbank_frames": (i32, [vp, i32, vp, vp]),
     "mms2ut_fbank_f32": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
     "mms2ut_fbank_cmvn_collate": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "mms2ut_specaugment_f16": (i32, [vp, vp, i32, i32, i32, vp, i32, i32, i32, f32, vp]),
 }
 
 _lib = None

@@ -1,11 +1,15 @@
 """``mms2ut-train``: the canonical fairseq-train command (scripts/textless/1_train.sh:105-125) on the
-HIP path.  Accepts the same flags; data is synthetic Speech-Multi30K-shaped (``--synthetic``), the
-TSV/.pth manifest reader being SURVEY §8f's next row.  One process per GPU under
+HIP path.  Accepts the same flags; data is the on-disk manifest (see
+below) or synthetic Speech-Multi30K-shaped batches (``--synthetic``).  One process per GPU under
 ``python -m torch.distributed.run``; batches are dealt round-robin to ranks (fairseq's
 ShardedIterator), gradients summed over RCCL (parallel.GradAllReducer).
 
 Log lines follow fairseq's progress format: loss / nll_loss in base 2 per target token, ppl,
 wps (target tokens/s), ups, lr, gnorm, loss_scale.
+
+Data: the manifest directory (fairseq's positional DATA: ``{split}.tsv``, ``config.yaml``, WAVs,
+image features from the fusion YAML's ``image_feat_path``) through ``manifest.DeviceLoader``, or
+``--synthetic``.
 """
 import ast
 import json
@@ -31,8 +35,8 @@ def main(argv=None):
     for kind, name in (("task", args.task), ("arch", args.arch), ("criterion", args.criterion)):
         if name not in REGISTRY[kind]:
             raise SystemExit(f"mms2ut-train: unknown {kind} {name!r}; have {sorted(REGISTRY[kind])}")
-    if not args.synthetic:
-        raise SystemExit("mms2ut-train: manifest (TSV) data loading is not built yet; pass --synthetic")
+    if not args.synthetic and not args.data:
+        raise SystemExit("mms2ut-train: give the manifest directory (fairseq's DATA argument) or --synthetic")
     rank, world, local = init_from_env()
     dev = torch.device("cuda", local)
     task = REGISTRY["task"][args.task].setup_task(args)
@@ -44,6 +48,8 @@ def main(argv=None):
                  warmup_updates=args.warmup_updates, warmup_init_lr=args.warmup_init_lr,
                  init_scale=float(args.fp16_init_scale), world_size=world)
     fus = task.multimodal_translation_config
+    if not args.synthetic:
+        return _train_manifest(args, task, cfg, tr, fus, rank, world, dev)
     ds = SyntheticSpeechMulti30K(n_utts=max(64, 2 * args.max_tokens // 400), seed=args.seed,
                                  vocab=cfg["vocab_size"], img_dim=cfg["image_feat_dim"],
                                  with_images=bool(fus is not None and cfg["fusion"]))
@@ -61,18 +67,60 @@ def main(argv=None):
             ntok += batch.ntokens * world  # rank-local count scaled (no per-step host sync)
             upd += 1
             if upd % args.log_interval == 0 or upd == args.max_update:
-                lg = log.tolist()
-                st = tr.opt.stats()
-                el = time.time() - t0
-                if rank == 0:
-                    ln2 = math.log(2)
-                    rec = {"num_updates": upd, "loss": lg[0] / lg[2] / ln2, "nll_loss": lg[1] / lg[2] / ln2,
-                           "ppl": 2 ** (lg[1] / lg[2] / ln2), "wps": ntok / max(el, 1e-9),
-                           "ups": upd / max(el, 1e-9), "lr": st["lr"], "gnorm": st["gnorm"],
-                           "loss_scale": st["loss_scale"], "overflow": st["overflow"]}
-                    print(json.dumps(rec), flush=True)
+                _log(args, upd, log, tr, ntok, t0, rank)
             if upd >= args.max_update:
                 break
+    torch.cuda.synchronize(dev)
+    return 0
+
+
+def _log(args, upd, log, tr, ntok, t0, rank):
+    if rank != 0:
+        return
+    lg = log.tolist()
+    st = tr.opt.stats()
+    el = time.time() - t0
+    ln2 = math.log(2)
+    rec = {"num_updates": upd, "loss": lg[0] / lg[2] / ln2, "nll_loss": lg[1] / lg[2] / ln2,
+           "ppl": 2 ** (lg[1] / lg[2] / ln2), "wps": ntok / max(el, 1e-9), "ups": upd / max(el, 1e-9),
+           "lr": st["lr"], "gnorm": st["gnorm"], "loss_scale": st["loss_scale"], "overflow": st["overflow"]}
+    print(json.dumps(rec), flush=True)
+
+
+def _train_manifest(args, task, cfg, tr, fus, rank, world, dev):
+    """On-disk data: ``{data}/{train_subset}.tsv`` + ``{data}/{config_yaml}``,
+    image features from the fusion YAML's ``image_feat_path``; per epoch the length-ordered batches
+    are shuffled with (seed, epoch) and dealt round-robin to ranks (fairseq ShardedIterator)."""
+    import os
+
+    import numpy as np
+
+    from . import manifest as M
+    if args.target_code_size is None:
+        raise SystemExit("mms2ut-train: --target-is-code --target-code-size N is required for unit targets")
+    data_cfg = M.load_data_config(os.path.join(args.data, args.config_yaml))
+    feat = getattr(fus, "image_feat_path", None) if (fus is not None and cfg["fusion"]) else None
+    ds = M.MultiModalS2SManifest(args.data, args.train_subset, M.UnitDictionary.for_codes(args.target_code_size),
+                                 data_cfg=data_cfg, image_feat_path=feat,
+                                 max_source_positions=cfg.get("max_source_positions", 6000),
+                                 max_target_positions=cfg.get("max_target_positions", 1024))
+    upd, t0, ntok, epoch = 0, time.time(), 0.0, 1
+    while upd < args.max_update:
+        batches = ds.batches(args.max_tokens, seed=args.seed, epoch=epoch, skip_invalid=True)
+        order = np.random.RandomState((args.seed + epoch) % 2 ** 32).permutation(len(batches)).tolist()
+        order = order[: len(order) // world * world]
+        mine = [batches[i] for i in order[rank::world]]
+        if not mine:
+            raise SystemExit(f"mms2ut-train: {len(batches)} batches cannot feed {world} ranks")
+        for batch, _ in M.DeviceLoader(ds, mine, cfg, dev, seed=args.seed + rank, epoch=epoch):
+            log = tr.train_step(batch)
+            ntok += batch.ntokens * world
+            upd += 1
+            if upd % args.log_interval == 0 or upd == args.max_update:
+                _log(args, upd, log, tr, ntok, t0, rank)
+            if upd >= args.max_update:
+                break
+        epoch += 1
     torch.cuda.synchronize(dev)
     return 0
 

@@ -164,6 +164,60 @@ __global__ void __launch_bounds__(256) cmvn_collate_kernel(const float* __restri
   }
 }
 
+// fairseq SpecAugmentTransform (feature_transforms/specaugment.py), applied on the device to the
+// collated fp16 features after CMVN: the host draws each utterance's masks (freq (f0, f) pairs
+// then time (t0, t) pairs, width 0 = no mask); the mask value is the utterance's mean over its
+// valid [T, nbins] region (the transform's default, mask_value=None) or the given constant.
+// One block per utterance: a 4-wide reduction for the mean, then one pass that rewrites only the
+// 4-bin groups touching a masked row or column.
+__global__ void __launch_bounds__(256) specaugment_kernel(h16* __restrict__ x, const int* __restrict__ frame_off,
+                                                          int Tmax, int nbins, const int* __restrict__ masks,
+                                                          int n_freq, int n_time, int use_const, float mask_const) {
+  const int b = blockIdx.x;
+  const int T = frame_off[b + 1] - frame_off[b];
+  const int* m = masks + (long)b * 2 * (n_freq + n_time);
+  h16* xb = x + (long)b * Tmax * nbins;
+  const long n = (long)T * nbins;
+  __shared__ float s_red[256 / 64];
+  __shared__ float s_val;
+  if (!use_const) {
+    float acc = 0.f;
+    for (long i = 4 * threadIdx.x; i < n; i += 4 * blockDim.x) {
+      const h16x4 v = *reinterpret_cast<const h16x4*>(xb + i);
+      acc += ((float)v[0] + (float)v[1]) + ((float)v[2] + (float)v[3]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int w = 0; w < (int)blockDim.x / 64; ++w) t += s_red[w];
+      s_val = n > 0 ? t / (float)n : 0.f;
+    }
+    __syncthreads();
+  }
+  const h16 mv = (h16)(use_const ? mask_const : s_val);
+  for (long i = 4 * threadIdx.x; i < n; i += 4 * blockDim.x) {
+    const int t = (int)(i / nbins), c = (int)(i % nbins);
+    bool row = false;
+    for (int k = 0; k < n_time; ++k) row |= (t >= m[2 * (n_freq + k)]) & (t < m[2 * (n_freq + k)] + m[2 * (n_freq + k) + 1]);
+    int hit = row ? 0xF : 0;
+    for (int k = 0; k < n_freq && hit != 0xF; ++k) {
+      const int f0 = m[2 * k], f1 = m[2 * k] + m[2 * k + 1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hit |= ((c + e >= f0) & (c + e < f1)) << e;
+    }
+    if (hit) {
+      h16x4 v = *reinterpret_cast<const h16x4*>(xb + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (hit & (1 << e)) v[e] = mv;
+      *reinterpret_cast<h16x4*>(xb + i) = v;
+    }
+  }
+}
+
 int init_consts(hipStream_t s) {
   if (g_fb_init) return 0;
   FbankConst h;
@@ -214,4 +268,15 @@ extern "C" int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* fram
   if (B == 0) return 0;
   hipLaunchKernelGGL(cmvn_collate_kernel, dim3(B), dim3(256), 0, s, feats, frame_off, B, Tmax, nbins, cmvn, out);
   return mms::check_launch("fbank_cmvn_collate");
+}
+
+extern "C" int mms2ut_specaugment_f16(h16* x, const int32_t* frame_off, int B, int Tmax, int nbins,
+                                      const int32_t* masks, int n_freq, int n_time, int use_const,
+                                      float mask_value, hipStream_t s) {
+  MMS_REQUIRE(nbins % 4 == 0 && ((uintptr_t)x & 7) == 0, "specaugment: nbins % 4 / alignment");
+  MMS_REQUIRE(n_freq >= 0 && n_time >= 0, "specaugment: negative mask count");
+  if (B == 0 || n_freq + n_time == 0) return 0;
+  hipLaunchKernelGGL(specaugment_kernel, dim3(B), dim3(256), 0, s, x, frame_off, Tmax, nbins, masks, n_freq,
+                     n_time, use_const, mask_value);
+  return mms::check_launch("specaugment");
 }

@@ -32,19 +32,24 @@ def collate_tokens(values, pad_idx, eos_idx, move_eos_to_beginning=False):
 
 
 def collater(items, pad=PAD, eos=EOS):
-    """items: list of dicts {index, source [T, C] float, target [Tt] long (ends with eos),
-    img [Ti, Di] or None, img_mask [Ti] bool or None}.  Returns the reference's sample dict."""
+    """items: list of dicts {index, source [T, C] float (or n_frames: int when the features are
+    computed on the GPU), target [Tt] long (ends with eos), img [Ti, Di] or None, img_mask [Ti]
+    bool or None}.  Returns the reference's sample dict (src_tokens None without "source")."""
     if len(items) == 0:
         return {}
     indices = torch.tensor([x["index"] for x in items], dtype=torch.long)
-    n_frames = torch.tensor([x["source"].size(0) for x in items], dtype=torch.long)
-    C = items[0]["source"].size(1)
-    frames = torch.zeros(len(items), int(n_frames.max()), C, dtype=torch.float32)
-    for i, x in enumerate(items):
-        frames[i, : x["source"].size(0)] = x["source"]
+    feats = "source" in items[0]
+    n_frames = torch.tensor([x["source"].size(0) if feats else x["n_frames"] for x in items], dtype=torch.long)
+    frames = None  # items without "source": the GPU front end produces src_tokens from waveforms
+    if feats:
+        C = items[0]["source"].size(1)
+        frames = torch.zeros(len(items), int(n_frames.max()), C, dtype=torch.float32)
+        for i, x in enumerate(items):
+            frames[i, : x["source"].size(0)] = x["source"]
     n_frames, order = n_frames.sort(descending=True)
     indices = indices.index_select(0, order)
-    frames = frames.index_select(0, order)
+    if feats:
+        frames = frames.index_select(0, order)
     targets = [x["target"] for x in items]
     target = collate_tokens(targets, pad, eos).index_select(0, order)
     prev = collate_tokens(targets, pad, eos, move_eos_to_beginning=True).index_select(0, order)
@@ -73,9 +78,11 @@ def synth_lengths(n, rng, mean=400.0, std=120.0, lo=150, hi=1000):
     return np.clip(np.round(rng.normal(mean, std, n)), lo, hi).astype(np.int64)
 
 
-def batch_by_size(lengths, max_tokens):
-    """fairseq batch_by_size (num_tokens_fn = src length), on length-sorted indices."""
-    order = np.argsort(lengths, kind="stable")
+def batch_by_size(lengths, max_tokens, order=None):
+    """fairseq batch_by_size (num_tokens_fn = src length, required_batch_size_multiple 1): walk the
+    indices in ``order`` (default: length-sorted) and close a batch when (n+1)*max_len > max_tokens."""
+    if order is None:
+        order = np.argsort(lengths, kind="stable")
     batches, cur, cur_max = [], [], 0
     for i in order:
         L = int(lengths[i])

@@ -42,11 +42,54 @@ def n_frames(n_samples):
     return 0 if n_samples < WIN else 1 + (n_samples - WIN) // SHIFT
 
 
+class SpecAugment:
+    """fairseq ``SpecAugmentTransform`` (data/audio/feature_transforms/specaugment.py) parameters
+    and its per-utterance mask draws; the masking itself runs on the GPU
+    (``mms2ut_specaugment_f16``).  Draw order per utterance is the transform's: freq_mask_N ×
+    (f ~ U[0, F), f0 ~ U[0, nbins - f)), then, if max_t = min(T_mask, floor(T·p)) >= 1,
+    time_mask_N × (t ~ U[0, max_t), t0 ~ U[0, T - t)); a zero width masks nothing.  The draws use
+    a seeded numpy stream per batch (the reference's global np.random in DataLoader workers is not
+    replayable, so mask positions are not bit-matched to it)."""
+
+    def __init__(self, time_warp_W=0, freq_mask_N=0, freq_mask_F=0, time_mask_N=0, time_mask_T=0,
+                 time_mask_p=0.0, mask_value=None):
+        if time_warp_W:
+            raise NotImplementedError("SpecAugment time warping (time_warp_W > 0) is not built")
+        self.fn, self.ff = int(freq_mask_N), int(freq_mask_F)
+        self.tn, self.tt, self.tp = int(time_mask_N), int(time_mask_T), float(time_mask_p)
+        self.mask_value = mask_value
+
+    @classmethod
+    def from_config_dict(cls, d):
+        d = d or {}
+        return cls(d.get("time_warp_W", 0), d.get("freq_mask_N", 0), d.get("freq_mask_F", 0),
+                   d.get("time_mask_N", 0), d.get("time_mask_T", 0), d.get("time_mask_p", 0.0),
+                   d.get("mask_value", None))
+
+    def draws(self, n_frames, nbins, rng):
+        """int32 [B, 2*(freq_mask_N + time_mask_N)] of (start, width) pairs."""
+        out = np.zeros((len(n_frames), 2 * (self.fn + self.tn)), dtype=np.int32)
+        for b, T in enumerate(n_frames):
+            T = int(T)
+            for k in range(self.fn):
+                f = int(rng.randint(0, self.ff)) if self.ff > 0 else 0
+                out[b, 2 * k: 2 * k + 2] = (int(rng.randint(0, nbins - f)), f)
+            max_t = min(self.tt, math.floor(T * self.tp))
+            if max_t < 1:
+                continue
+            for k in range(self.tn):
+                t = int(rng.randint(0, max_t))
+                j = 2 * (self.fn + k)
+                out[b, j: j + 2] = (int(rng.randint(0, T - t)), t)
+        return out
+
+
 class FbankFrontend:
-    def __init__(self, device="cuda", num_bins=80, cmvn=True):
+    def __init__(self, device="cuda", num_bins=80, cmvn=True, specaugment=None):
         self.device = torch.device(device)
         self.num_bins = num_bins
         self.cmvn = cmvn
+        self.specaugment = specaugment
         banks = mel_banks(num_bins)
         self.banks = torch.from_numpy(banks).to(self.device)
         nz = banks > 0
@@ -56,9 +99,10 @@ class FbankFrontend:
         rng = np.stack([lo, hi], 1).astype(np.int32)
         self.mel_range = torch.from_numpy(rng.reshape(-1)).to(self.device)
 
-    def upload(self, waves):
+    def upload(self, waves, pin=False):
         """waves: list of 1-D float32 arrays already in int16 range (get_waveform(normalization=False)).
-        Returns a device-resident wave batch (sorted by frames, descending, like the collater)."""
+        Returns a device-resident wave batch (sorted by frames, descending, like the collater).
+        pin=True stages the samples in pinned host memory and copies asynchronously."""
         lens = [n_frames(len(w)) for w in waves]
         order = sorted(range(len(waves)), key=lambda i: -lens[i])
         waves = [waves[i] for i in order]
@@ -67,18 +111,28 @@ class FbankFrontend:
         wave_off = np.concatenate([[0], np.cumsum(wl)]).astype(np.int64)
         frame_off = np.concatenate([[0], np.cumsum(fr)]).astype(np.int32)
         flat = np.concatenate(waves).astype(np.float32)
+        def dev(a):
+            t = torch.from_numpy(a)
+            return t.pin_memory().to(self.device, non_blocking=True) if pin else t.to(self.device)
+
         return {
-            "wave": torch.from_numpy(flat).to(self.device),
-            "wave_off": torch.from_numpy(wave_off).to(self.device),
-            "frame_off": torch.from_numpy(frame_off).to(self.device),
+            "wave": dev(flat), "wave_off": dev(wave_off), "frame_off": dev(frame_off),
             "n_frames": torch.from_numpy(fr), "total": int(fr.sum()), "Tmax": int(fr.max()),
             "B": len(waves), "order": order,
         }
 
-    def __call__(self, wb):
+    def __call__(self, wb, rng=None):
+        """-> fp16 [B, Tmax, nbins].  With a SpecAugment policy and a numpy RandomState ``rng``
+        (training batches), the masks are drawn on the host and applied in place after CMVN."""
         feats = K.fbank(wb["wave"], wb["wave_off"], wb["frame_off"], wb["total"], self.banks, self.mel_range,
                         self.num_bins)
-        return K.cmvn_collate(feats, wb["frame_off"], wb["B"], wb["Tmax"], self.num_bins, self.cmvn)
+        out = K.cmvn_collate(feats, wb["frame_off"], wb["B"], wb["Tmax"], self.num_bins, self.cmvn)
+        sa = self.specaugment
+        if sa is not None and rng is not None and sa.fn + sa.tn > 0:
+            m = sa.draws(wb["n_frames"].tolist(), self.num_bins, rng)
+            masks = torch.from_numpy(m).pin_memory().to(self.device, non_blocking=True)
+            K.specaugment(out, wb["frame_off"], masks, sa.fn, sa.tn, sa.mask_value)
+        return out
 
     def features_f32(self, wb):
         """Raw log-mel features [total_frames, nbins] fp32 (no CMVN) — for parity tests."""

@@ -648,6 +648,17 @@ def cmvn_collate(feats, frame_off, B, Tmax, nbins=80, cmvn=True):
     return out
 
 
+def specaugment(x, frame_off, masks, n_freq, n_time, mask_value=None):
+    """In place on collated fp16 features x [B, Tmax, nbins]; masks int32 [B, 2*(n_freq+n_time)]
+    on x's device (see include/mms2ut.h)."""
+    B, Tmax, nbins = x.shape
+    if masks.shape != (B, 2 * (n_freq + n_time)) or masks.dtype != torch.int32 or masks.device != x.device:
+        raise ValueError(f"specaugment: masks {tuple(masks.shape)} {masks.dtype} for B={B}, {n_freq}+{n_time} masks")
+    call("mms2ut_specaugment_f16", x.data_ptr(), frame_off.data_ptr(), B, Tmax, nbins, masks.data_ptr(),
+         int(n_freq), int(n_time), int(mask_value is not None), float(mask_value or 0.0), _s())
+    return x
+
+
 def round_up(x, m):
     return (x + m - 1) // m * m
 

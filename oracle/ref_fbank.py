@@ -8,7 +8,8 @@ with its defaults (dither 0, snip_edges, round_to_power_of_two, povey window, pr
 remove_dc_offset, low_freq 20, high_freq = Nyquist, use_power, use_log_fbank, eps = FLT_EPSILON,
 no energy).  torchaudio is absent from the container (unpinned version) — the restatement is
 cross-checked against transformers.audio_utils' independent Kaldi-compatible implementation.
-Then the data-config ``utterance_cmvn`` transform (fairseq UtteranceCMVN; speech_to_speech_dataset.py:271-272).
+Then the data-config ``utterance_cmvn`` transform (fairseq UtteranceCMVN; speech_to_speech_dataset.py:271-272)
+and, for training splits whose config lists it, ``specaugment`` (fairseq SpecAugmentTransform).
 """
 import numpy as np
 
@@ -82,6 +83,25 @@ def utterance_cmvn(x, norm_means=True, norm_vars=True):
         var = sq / x.shape[0] - mean ** 2
         x = x / np.sqrt(np.maximum(var, 1e-10))
     return x.astype(np.float32)
+
+
+def specaugment(x, draws, n_freq, n_time, mask_value=None):
+    """fairseq ``SpecAugmentTransform.__call__`` (data/audio/feature_transforms/specaugment.py;
+    time_warp_W = 0) with its random draws given: draws = [f0, f]*n_freq + [t0, t]*n_time, a zero
+    width masking nothing; mask value = ``spectrogram.mean()`` of the undistorted input when
+    mask_value is None.  x: [T, F] float32 (one utterance, unpadded)."""
+    x = np.asarray(x, dtype=np.float32)
+    out = x.copy()
+    mv = x.mean() if mask_value is None else mask_value
+    for k in range(n_freq):
+        f0, f = int(draws[2 * k]), int(draws[2 * k + 1])
+        if f != 0:
+            out[:, f0:f0 + f] = mv
+    for k in range(n_time):
+        t0, t = int(draws[2 * (n_freq + k)]), int(draws[2 * (n_freq + k) + 1])
+        if t != 0:
+            out[t0:t0 + t, :] = mv
+    return out
 
 
 def synth_wave(n_frames, rng, tone_hz=440.0):

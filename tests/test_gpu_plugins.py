@@ -84,3 +84,24 @@ def test_cli_trains_synthetic(tmp_path, capsys):
     for r in recs:
         assert r["loss"] > 0 and r["nll_loss"] > 0 and r["loss_scale"] > 0
         assert r["wps"] > 0
+
+
+def test_cli_trains_on_manifest(tmp_path, capsys):
+    """mms2ut-train DATA ...: TSV + WAVs + config.yaml (utterance_cmvn, specaugment) + .pth image
+    features named by the fusion YAML — the on-disk path of SURVEY §8f row 1."""
+    from manifest_corpus import write_corpus
+    sa = {"freq_mask_F": 27, "freq_mask_N": 1, "time_mask_N": 1, "time_mask_T": 100, "time_mask_p": 1.0}
+    d = tmp_path / "data"
+    d.mkdir()
+    c = write_corpus(str(d), frames=(150, 97, 200, 61, 88, 131, 45, 170), di=768, ti=12,
+                     transforms=("utterance_cmvn", "specaugment"), specaugment=sa)
+    y = tmp_path / "mm.yaml"
+    y.write_text(FUSION_YAML.replace('["/feats/vit_base_patch16_384"]', f'["{c["feat_dir"]}"]'))
+    argv = (f"{d} --task multimodal_speech_to_speech --arch mm_s2ut_transformer --criterion speech_to_unit "
+            f"--config-yaml config.yaml --target-is-code --target-code-size 1000 "
+            f"--share-decoder-input-output-embed --fp16 --multimodal-translation-config-yaml {y} {TINY} "
+            f"--max-update 5 --max-tokens 600 --log-interval 5 --warmup-updates 4 --lr 1e-3").split()
+    assert pkg("cli").main(argv) == 0
+    recs = [json.loads(l) for l in capsys.readouterr().out.splitlines() if l.startswith("{")]
+    assert [r["num_updates"] for r in recs] == [5]
+    assert recs[0]["loss"] > 0 and recs[0]["wps"] > 0

@@ -115,12 +115,12 @@ def test_selective_attention_yaml(tmp_path):
     assert cfg["use_selective_gate"] is False and cfg["fusion"] is True
 
 
-def test_cli_rejects_non_fp16_and_real_data():
+def test_cli_rejects_non_fp16_and_missing_data():
     cli = pkg("cli")
     with pytest.raises(SystemExit, match="fp16"):
         cli.main(["/d", "--share-decoder-input-output-embed"])
-    with pytest.raises(SystemExit, match="synthetic"):
-        cli.main(["/d", "--fp16", "--share-decoder-input-output-embed"])
+    with pytest.raises(SystemExit, match="DATA"):
+        cli.main(["--fp16", "--share-decoder-input-output-embed"])
     with pytest.raises(SystemExit, match="unknown criterion"):
         cli.main(["/d", "--fp16", "--criterion", "cross_entropy", "--synthetic"])
 
