@@ -293,6 +293,20 @@ int mms2ut_adam_fp16_master(mms2ut_half* param, const mms2ut_half* grad, float* 
                             float* exp_avg, float* exp_avg_sq, int64_t n, const float* ost,
                             float beta1, float beta2, float eps, float weight_decay, hipStream_t stream);
 
+/* ---------------------------------------------------------------- beam-search decoding
+ * fairseq SequenceGenerator._generate (fairseq-generate --beam 10 --max-len-a 1, SURVEY §8f row 2;
+ * scripts/textless/2_inference.sh:34-44).  log_softmax_step: log_softmax(logits.float()) of each
+ * hypothesis row (get_normalized_probs) fused with the step's masking: NaN -> -inf, pad -> -inf,
+ * mode 1 (step >= max_len): every token but eos -> -inf, mode 2 (step < min_len): eos -> -inf.
+ * lprobs [rows][V] fp32.                                                                    */
+int mms2ut_log_softmax_step(const mms2ut_half* logits, int64_t ld, int64_t rows, int V, int pad_idx,
+                            int eos_idx, int mode, float* lprobs, hipStream_t stream);
+/* reorder_incremental_state: src [L][Nsrc][maxT][width], dst [L][N][maxT][width] (each decoder
+ * layer's self-attention K|V rows); dst[l][n][0:rows] = src[l][idx[n]][0:rows], idx[n] < Nsrc.
+ * width % 8 == 0, 16-B aligned.                                                              */
+int mms2ut_kv_cache_gather(const mms2ut_half* src, mms2ut_half* dst, const int64_t* idx, int L, int Nsrc,
+                           int N, int maxT, int rows, int width, hipStream_t stream);
+
 /* ---------------------------------------------------------------- fbank front end
  * fairseq get_fbank -> torchaudio.compliance.kaldi.fbank (audio_utils.py:326-349), 80 bins,
  * 25 ms / 10 ms, snip_edges, DC removal, pre-emphasis 0.97, povey window, 512-pt FFT, power,

@@ -474,10 +474,12 @@ def _attn_args(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len,
 
 
 def mha_fwd(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len=None, causal=False,
-            p=0.0, drop=None):
-    """Fused attention forward; returns the row log-sum-exp [B*H*Tq] (fp32) for the backward."""
+            p=0.0, drop=None, sq=0, sk=0, sv=0, so=0):
+    """Fused attention forward; returns the row log-sum-exp [B*H*Tq] (fp32) for the backward.
+    s*: batch strides in elements (0 = rows of one batch follow each other: T * ld)."""
     lse = torch.empty(B * H * Tq, dtype=torch.float32, device=q.device)
-    a = _attn_args(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len, causal, p, drop, lse)
+    a = _attn_args(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len, causal, p, drop, lse,
+                   sq, sk, sv, so)
     call("mms2ut_mha_varlen_fwd", a, _s())
     return lse
 
@@ -657,6 +659,26 @@ def specaugment(x, frame_off, masks, n_freq, n_time, mask_value=None):
     call("mms2ut_specaugment_f16", x.data_ptr(), frame_off.data_ptr(), B, Tmax, nbins, masks.data_ptr(),
          int(n_freq), int(n_time), int(mask_value is not None), float(mask_value or 0.0), _s())
     return x
+
+
+def log_softmax_step(logits, V, pad, eos, mode=0, out=None):
+    """fp32 [rows, V] = log_softmax(logits[:, :V].float()) with the beam-search step masks
+    (mode 0: pad; 1: force eos; 2: forbid eos)."""
+    rows = logits.shape[0]
+    out = torch.empty(rows, V, dtype=torch.float32, device=logits.device) if out is None else out
+    call("mms2ut_log_softmax_step", logits.data_ptr(), logits.stride(0), rows, int(V), int(pad), int(eos),
+         int(mode), out.data_ptr(), _s())
+    return out
+
+
+def kv_cache_gather(src, dst, idx, rows):
+    """dst[l, n, :rows] = src[l, idx[n], :rows] for caches [L, N, maxT, width] (idx int64 on device)."""
+    L, Ns, T, W = src.shape
+    Ld, N, Td, Wd = dst.shape
+    if (L, T, W) != (Ld, Td, Wd) or idx.numel() != N or idx.dtype != torch.int64 or rows > T:
+        raise ValueError(f"kv_cache_gather: src {tuple(src.shape)} dst {tuple(dst.shape)} idx {tuple(idx.shape)}")
+    call("mms2ut_kv_cache_gather", src.data_ptr(), dst.data_ptr(), idx.data_ptr(), L, Ns, N, T, int(rows), W, _s())
+    return dst
 
 
 def round_up(x, m):
