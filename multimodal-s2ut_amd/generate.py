@@ -56,7 +56,6 @@ class IncrementalDecoder:
         self.pos = model._ensure_pos(self.maxT + 2, "dec")
         self.scale = 1.0 if cfg["no_scale_embedding"] else math.sqrt(self.d)
         self.Vp = K.round_up(self.V, 64)
-        self.key_len = None
         self.step_no = 0
 
     @property
@@ -245,7 +244,8 @@ class SequenceGenerator:
         return newly
 
 
-def generate(model, batch, beam_size=10, max_len_a=1.0, max_len_b=200, max_len=None, len_penalty=1.0):
+def generate(model, batch, beam_size=10, max_len_a=1.0, max_len_b=200, max_len=None, len_penalty=1.0,
+             min_len=1):
     """fairseq-generate on one DeviceBatch: encoder (eval, fusion included) -> beam search.
     Returns, per sentence in batch order, the hypotheses sorted by score (fairseq's dicts)."""
     was = model.training
@@ -254,8 +254,8 @@ def generate(model, batch, beam_size=10, max_len_a=1.0, max_len_b=200, max_len=N
         enc, enc_len32, Te, _ = model.encoder_forward(batch)
         bsz = batch.src.shape[0]
         gen = SequenceGenerator(beam_size, max_len_a, max_len_b,
-                                max_len or model.cfg["max_target_positions"], len_penalty=len_penalty,
-                                pad=model.cfg["padding_idx"])
+                                max_len or model.cfg["max_target_positions"], min_len=min_len,
+                                len_penalty=len_penalty, pad=model.cfg["padding_idx"])
         T = gen.max_steps(batch.src.shape[1])
         dec = IncrementalDecoder(model, enc, enc_len32, Te, bsz, beam_size, T)
         return gen.generate(dec, bsz, T, model.cfg["vocab_size"], enc.device)

@@ -197,6 +197,60 @@ class MultiModalSpeechToSpeechTask:
     def build_criterion(self, args):
         return SpeechToUnitCriterion(self, getattr(args, "label_smoothing", 0.2))
 
+    def load_dataset(self, split, epoch=1, **kw):
+        """speech_to_speech.py:100-123 -> the on-disk manifest (manifest.MultiModalS2SManifest)."""
+        import os
+
+        from . import manifest as M
+        a = self.args
+        fus = self.multimodal_translation_config
+        data_cfg = M.load_data_config(os.path.join(a.data, getattr(a, "config_yaml", "config.yaml")))
+        feat = getattr(fus, "image_feat_path", None) if fus is not None else None
+        if not hasattr(self, "datasets"):
+            self.datasets = {}
+        self.datasets[split] = M.MultiModalS2SManifest(
+            a.data, split, M.UnitDictionary.for_codes(self.vocab_size - 4), data_cfg=data_cfg,
+            image_feat_path=feat, is_train=split.startswith("train"))
+        return self.datasets[split]
+
+    def build_generator(self, models, args, **kw):
+        """fairseq SpeechToSpeechTask.build_generator for unit targets: beam search
+        (--beam, --max-len-a, --max-len-b, --lenpen, --min-len; 2_inference.sh:34-44)."""
+        return UnitSequenceGenerator(models, beam_size=getattr(args, "beam", 5),
+                                     max_len_a=getattr(args, "max_len_a", 0.0),
+                                     max_len_b=getattr(args, "max_len_b", 200),
+                                     len_penalty=getattr(args, "lenpen", 1.0),
+                                     min_len=getattr(args, "min_len", 1))
+
+    def inference_step(self, generator, models, sample, prefix_tokens=None, constraints=None):
+        if prefix_tokens is not None or constraints is not None:
+            raise NotImplementedError("prefix tokens / constraints in beam search")
+        return generator.generate(models, sample)
+
+
+class UnitSequenceGenerator:
+    """fairseq SequenceGenerator surface (``generate(models, sample)`` -> per sentence, hypotheses
+    sorted by score: {"tokens", "score", "attention", "alignment", "positional_scores"}) over
+    generate.IncrementalDecoder (HIP) + generate.SequenceGenerator."""
+
+    def __init__(self, models, beam_size=5, max_len_a=0.0, max_len_b=200, len_penalty=1.0, min_len=1):
+        if len(models) != 1:
+            raise NotImplementedError("ensembles in beam search")
+        self.model = models[0]
+        self.beam_size, self.max_len_a, self.max_len_b = beam_size, max_len_a, max_len_b
+        self.len_penalty, self.min_len = len_penalty, min_len
+
+    def generate(self, models, sample, **kw):
+        from . import generate as G
+        net = (models[0] if models else self.model).net
+        batch = runtime.prepare_batch(sample, net.cfg, net.device)
+        hyps = G.generate(net, batch, self.beam_size, self.max_len_a, self.max_len_b,
+                          len_penalty=self.len_penalty, min_len=self.min_len)
+        for hs in hyps:
+            for h in hs:
+                h["attention"], h["alignment"] = None, None
+        return hyps
+
 # ------------------------------------------------------------------------------------ model
 
 
@@ -331,4 +385,10 @@ def build_parser():
     p.add_argument("--gen-subset", default="test")
     p.add_argument("--required-batch-size-multiple", type=int, default=1)
     p.add_argument("--synthetic", action="store_true", help="synthetic Speech-Multi30K-shaped data")
+    # fairseq-generate (scripts/textless/2_inference.sh:34-44)
+    p.add_argument("--beam", type=int, default=5)
+    p.add_argument("--max-len-a", type=float, default=0.0)
+    p.add_argument("--max-len-b", type=int, default=200)
+    p.add_argument("--lenpen", type=float, default=1.0)
+    p.add_argument("--min-len", type=int, default=1)
     return p

@@ -121,3 +121,25 @@ def test_generate_matches_oracle_search():
         assert abs(hyps[s][0]["score"] - ref[s][0]["score"]) < 2e-2
         for h in hyps[s]:
             assert h["tokens"][-1].item() == 2 and len(h["tokens"]) <= maxlen_b + 1
+
+
+def test_task_generator_surface(tmp_path):
+    """fairseq-generate's calls: task.build_generator(models, args) -> task.inference_step(...)."""
+    mm, cfg, P, model, batch, enc_ref, pad_ref = _setup(sharpen=6.0, lengths=(61, 40), seed=5)
+    from test_gpu_plugins import _args
+    args = _args(tmp_path, "--beam 4 --max-len-a 0 --max-len-b 10")
+    task = mm.plugins.REGISTRY["task"][args.task].setup_task(args)
+
+    class Wrapped:     # the plugin model object around the already-loaded network
+        net = model
+
+    gen = task.build_generator([Wrapped], args)
+    sample = mm.data.make_sample([61, 40], [9, 9], img_tokens=17, img_dim=768, seed=1)
+    sample["net_input"]["src_tokens"] = sample["net_input"]["src_tokens"].half().float()
+    sample["net_input"]["imgs_list"][0] = sample["net_input"]["imgs_list"][0].half().float()
+    hyps = task.inference_step(gen, [Wrapped], sample)
+    direct = mm.generate.generate(model, batch, beam_size=4, max_len_a=0.0, max_len_b=10)
+    assert len(hyps) == 2
+    for h, d in zip(hyps, direct):
+        assert len(h) == 4 and h[0]["tokens"].tolist() == d[0]["tokens"].tolist()
+        assert set(h[0]) >= {"tokens", "score", "attention", "alignment", "positional_scores"}
