@@ -301,6 +301,20 @@ int mms2ut_adam_fp16_master(mms2ut_half* param, const mms2ut_half* grad, float* 
  * lprobs [rows][V] fp32.                                                                    */
 int mms2ut_log_softmax_step(const mms2ut_half* logits, int64_t ld, int64_t rows, int V, int pad_idx,
                             int eos_idx, int mode, float* lprobs, hipStream_t stream);
+/* One step of decoder self-attention against the K|V cache of one layer,
+ * cache [slots][maxT][width = 2*H*hd] (K in columns [0, H*hd), V in [H*hd, 2*H*hd)), addressed
+ * through slot [N][maxT] int32: key/value row t (t < T) of hypothesis n is row t of cache slot
+ * slot[n][t] (beam reorders permute the table, not the cache).  q [N][ldq] (head h at column
+ * h*hd), out [N][ldo] fp16; softmax(scale q k^T) v per head in fp32.                           */
+int mms2ut_decode_self_attn(const mms2ut_half* q, int64_t ldq, const mms2ut_half* cache, const int32_t* slot,
+                            int N, int H, int hd, int maxT, int T, int64_t width, mms2ut_half* out,
+                            int64_t ldo, float scale, hipStream_t stream);
+/* Decoder-step split-K epilogue: out[rows][cols] (fp16, row stride ldo) = act(sum of nsplit fp32
+ * slabs [rows][cols] (slab elements apart) + bias) (+ aux, row stride ldaux); act = ReLU if relu.
+ * bias / aux may be null.                                                                      */
+int mms2ut_splitk_epilogue_f16(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                               const mms2ut_half* bias, const mms2ut_half* aux, int64_t ldaux, int relu,
+                               mms2ut_half* out, int64_t ldo, hipStream_t stream);
 /* reorder_incremental_state: src [L][Nsrc][maxT][width], dst [L][N][maxT][width] (each decoder
  * layer's self-attention K|V rows); dst[l][n][0:rows] = src[l][idx[n]][0:rows], idx[n] < Nsrc.
  * width % 8 == 0, 16-B aligned.                                                              */

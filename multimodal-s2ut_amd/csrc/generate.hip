@@ -59,6 +59,126 @@ __global__ void __launch_bounds__(256) kv_cache_gather_kernel(const h16* __restr
   }
 }
 
+// One decoder step of self-attention over the cache, addressed through a slot table (so a beam
+// reorder moves N*T int32 indices instead of every layer's K/V rows): key/value row t of
+// hypothesis n is row t of cache slot slot[n][t].  One 256-thread block per (hypothesis, head):
+// phase 1 — threads over keys, q.k by packed fp16 dot products (q in registers), scores and row
+// offsets to LDS, block max / sum; phase 2 — HD/8 threads per V row (16-B loads), 256/(HD/8) rows
+// in flight, fp32 partials reduced across row groups through LDS; output fp16.  Reads
+// T*hd*2*2 B per (hypothesis, head): HBM/latency-bound.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+constexpr int DEC_THREADS = 256;
+
+template <int HD>
+__global__ void __launch_bounds__(DEC_THREADS) decode_attn_kernel(const h16* __restrict__ q, long ldq,
+                                                                  const h16* __restrict__ cache,
+                                                                  const int* __restrict__ slot, int H, int maxT,
+                                                                  int T, long width, h16* __restrict__ out,
+                                                                  long ldo, float scale) {
+  constexpr int VL = HD / 8;                  // threads per V row (16-B vectors)
+  constexpr int G = DEC_THREADS / VL;         // V rows in flight
+  extern __shared__ float s_dyn[];
+  float* s_p = s_dyn;                                         // [T] scores -> probabilities
+  long* s_off = reinterpret_cast<long*>(s_dyn + ((T + 1) & ~1));  // [T] element offsets of the rows
+  __shared__ float s_part[G][HD];
+  __shared__ float s_red[DEC_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = blockIdx.x / H, h = blockIdx.x % H;
+  s16x8 qv[VL];
+  const h16* qr = q + (long)n * ldq + h * HD;
+#pragma unroll
+  for (int i = 0; i < VL; ++i) qv[i] = reinterpret_cast<const s16x8*>(qr)[i];
+  const int* sl = slot + (long)n * maxT;
+  float mx = -INFINITY;
+  for (int t = tid; t < T; t += DEC_THREADS) {
+    const long off = ((long)sl[t] * maxT + t) * width + h * HD;
+    const h16* kr = cache + off;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < VL; ++i) {
+      const h16x8 kk = __builtin_bit_cast(h16x8, reinterpret_cast<const s16x8*>(kr)[i]);
+      const h16x8 qq = __builtin_bit_cast(h16x8, qv[i]);
+#pragma unroll
+      for (int e = 0; e < 8; e += 2)
+        acc = __builtin_amdgcn_fdot2(h16x2{qq[e], qq[e + 1]}, h16x2{kk[e], kk[e + 1]}, acc, false);
+    }
+    acc *= scale;
+    s_p[t] = acc;
+    s_off[t] = off;
+    mx = fmaxf(mx, acc);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) s_red[w] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int t = tid; t < T; t += DEC_THREADS) {
+    const float e = __expf(s_p[t] - mx);
+    s_p[t] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) s_red[w] = sum;
+  __syncthreads();
+  const float inv = 1.f / ((s_red[0] + s_red[1]) + (s_red[2] + s_red[3]));
+  const int g = tid / VL, c = tid % VL;
+  if (g < G) {
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const long vcol = width / 2 + c * 8;
+#pragma unroll 4
+    for (int t = g; t < T; t += G) {
+      const h16x8 v = __builtin_bit_cast(h16x8, *reinterpret_cast<const s16x8*>(cache + s_off[t] + vcol));
+      const float pt = s_p[t];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pt * (float)v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s_part[g][c * 8 + e] = o[e];
+  }
+  __syncthreads();
+  if (tid < HD) {
+    float a = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < G; ++gg) a += s_part[gg][tid];
+    out[(long)n * ldo + h * HD + tid] = (h16)(a * inv);
+  }
+}
+
+// Split-K epilogue for the decoder step's small-M GEMMs (M = hypotheses, ~100-300 rows: one or two
+// tile rows, so K = 768 / 3072 runs as a long serial k-loop on a dozen blocks): the GEMM writes
+// `nsplit` fp32 slabs, this sums them and applies the layer's epilogue — + bias, ReLU, + residual
+// — to fp16 (the same arithmetic as the fused GEMM epilogue, summed in fp32).
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(const float* __restrict__ slabs, int nsplit, long slab,
+                                                              int M, int N, const h16* __restrict__ bias,
+                                                              const h16* __restrict__ aux, long ldaux, int relu,
+                                                              h16* __restrict__ out, long ldo) {
+  const long nv = (long)M * N / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (long)gridDim.x * blockDim.x) {
+    const long e = 4 * i;
+    const int r = (int)(e / N), c = (int)(e % N);
+    f32x4 a = *reinterpret_cast<const f32x4*>(slabs + e);
+    for (int k = 1; k < nsplit; ++k) a += *reinterpret_cast<const f32x4*>(slabs + k * slab + e);
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = a[j];
+      if (bias) v += (float)bias[c + j];
+      if (relu) v = fmaxf(v, 0.f);
+      o[j] = v;
+    }
+    if (aux) {
+      const h16x4 x = *reinterpret_cast<const h16x4*>(aux + (long)r * ldaux + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (float)(h16)o[j] + (float)x[j];
+    }
+    h16x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) y[j] = (h16)o[j];
+    *reinterpret_cast<h16x4*>(out + (long)r * ldo + c) = y;
+  }
+}
+
 }  // namespace
 
 extern "C" int mms2ut_log_softmax_step(const h16* logits, int64_t ld, int64_t rows, int V, int pad_idx,
@@ -82,4 +202,40 @@ extern "C" int mms2ut_kv_cache_gather(const h16* src, h16* dst, const int64_t* i
   hipLaunchKernelGGL(kv_cache_gather_kernel, dim3(nb), dim3(256), 0, s, src, dst, idx, L, Nsrc, N, maxT, rows,
                      width);
   return mms::check_launch("kv_cache_gather");
+}
+
+extern "C" int mms2ut_decode_self_attn(const h16* q, int64_t ldq, const h16* cache, const int32_t* slot, int N,
+                                       int H, int hd, int maxT, int T, int64_t width, h16* out, int64_t ldo,
+                                       float scale, hipStream_t s) {
+  MMS_REQUIRE(T >= 1 && T <= maxT, "decode_self_attn: T must be in [1, maxT]");
+  MMS_REQUIRE(width == 2L * H * hd && ldq % 8 == 0 && width % 8 == 0,
+              "decode_self_attn: width must be 2*H*hd, ldq / width multiples of 8");
+  const size_t lds = (size_t)((T + 1) & ~1) * 4 + (size_t)T * 8;
+  MMS_REQUIRE(lds <= 96 * 1024, "decode_self_attn: T too long for the LDS score rows");
+  if (N == 0) return 0;
+  const dim3 grid(N * H);
+  switch (hd) {
+    case 64: hipLaunchKernelGGL(decode_attn_kernel<64>, grid, dim3(DEC_THREADS), lds, s, q, (long)ldq, cache,
+                                slot, H, maxT, T, (long)width, out, (long)ldo, scale); break;
+    case 96: hipLaunchKernelGGL(decode_attn_kernel<96>, grid, dim3(DEC_THREADS), lds, s, q, (long)ldq, cache,
+                                slot, H, maxT, T, (long)width, out, (long)ldo, scale); break;
+    case 128: hipLaunchKernelGGL(decode_attn_kernel<128>, grid, dim3(DEC_THREADS), lds, s, q, (long)ldq, cache,
+                                 slot, H, maxT, T, (long)width, out, (long)ldo, scale); break;
+    default: mms::set_error("decode_self_attn: head dim must be 64, 96 or 128"); return 1;
+  }
+  return mms::check_launch("decode_self_attn");
+}
+
+extern "C" int mms2ut_splitk_epilogue_f16(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                                          const h16* bias, const h16* aux, int64_t ldaux, int relu, h16* out,
+                                          int64_t ldo, hipStream_t s) {
+  MMS_REQUIRE(cols % 4 == 0 && ldo % 4 == 0 && (!aux || ldaux % 4 == 0) && slab % 4 == 0,
+              "splitk_epilogue: cols / strides must be multiples of 4");
+  MMS_REQUIRE(nsplit >= 1, "splitk_epilogue: nsplit >= 1");
+  const long nv = (long)rows * cols / 4;
+  if (nv == 0) return 0;
+  const int nb = (int)std::min<long>((nv + 255) / 256, 4096);
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(nb), dim3(256), 0, s, slabs, nsplit, (long)slab, rows, cols,
+                     bias, aux, (long)ldaux, relu, out, (long)ldo);
+  return mms::check_launch("splitk_epilogue");
 }

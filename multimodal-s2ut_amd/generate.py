@@ -5,10 +5,11 @@ Two parts:
 
 * ``IncrementalDecoder`` — fairseq ``TransformerDecoder`` with ``incremental_state``: one new
   token per hypothesis per step.  Every layer's self-attention K|V rows live in a cache
-  [L_d, N, maxT, 2d] that the layer's K|V projection GEMM writes into directly (row stride
-  maxT·2d); the step's attention is the flash kernel with one query row and key_len = step + 1.
-  ``reorder_incremental_state`` is one ``kv_cache_gather`` launch over all layers (ping-pong
-  buffers).  Cross-attention K/V of all layers are one GEMM over the encoder output at the start
+  [L_d, slots, maxT, 2d] that the layer's K|V projection GEMM writes into directly (row stride
+  maxT·2d; hypothesis n writes row `step` of slot n).  Rows never move: a slot table
+  [N, maxT] int32 says which slot holds row t of hypothesis n, so ``reorder_incremental_state``
+  permutes N·step indices instead of copying every layer's K/V (fairseq's index_select of the
+  cache), and ``decode_self_attn`` reads K/V through the table (one wave per hypothesis·head).  Cross-attention K/V of all layers are one GEMM over the encoder output at the start
   (the training path's batched slab); they stay per *sentence*: the beam hypotheses of sentence s
   are the query rows [s·beam, (s+1)·beam) of one attention problem (B = sentences, Tq = beam), so
   nothing is expanded by the beam (``reorder_encoder_out`` is the identity within a sentence and
@@ -29,6 +30,20 @@ from . import kernels as K
 from .kernels import F16
 
 MODE_NONE, MODE_FORCE_EOS, MODE_NO_EOS = 0, 1, 2
+
+
+def _lin(x, W, b, *, aux=None, relu=False, out=None):
+    """Decoder-step projection: split-K over fp32 slabs when the hypothesis rows leave most of the
+    chip idle (tiles * s <= ~256 blocks, k-chunks >= 256), else the fused-epilogue GEMM."""
+    M, Kd = x.shape
+    N = W.shape[0]
+    tiles = -(-M // 128) * -(-N // 128)
+    s = min(8, max(1, 256 // tiles), Kd // 256)
+    if s > 1:
+        return K.linear_splitk(x, W, b, aux=aux, relu=relu, splitk=s, out=out)
+    if aux is not None:
+        return K.linear(x, W, b, out=out, epi=K.EPI_DROP_RESID, aux=aux, p=0.0)
+    return K.linear(x, W, b, out=out, epi=K.EPI_RELU_DROP if relu else K.EPI_F16, p=0.0)
 
 
 class IncrementalDecoder:
@@ -52,7 +67,8 @@ class IncrementalDecoder:
         self.enc_len32 = enc_len32
         N = bsz * beam
         self.cache = torch.empty(self.L, N, self.maxT, 2 * self.d, dtype=F16, device=dev)
-        self.spare = torch.empty_like(self.cache)
+        self.slot = torch.zeros(N, self.maxT, dtype=torch.int32, device=dev)
+        self.slot_ids = torch.arange(N, dtype=torch.int32, device=dev)
         self.pos = model._ensure_pos(self.maxT + 2, "dec")
         self.scale = 1.0 if cfg["no_scale_embedding"] else math.sqrt(self.d)
         self.Vp = K.round_up(self.V, 64)
@@ -65,7 +81,9 @@ class IncrementalDecoder:
     def reorder(self, reorder_state, batch_idxs=None):
         """reorder_incremental_state(reorder_state) + reorder_encoder_out: reorder_state [N_new]
         indexes the current hypotheses (fairseq's corrected index into the previous batch)."""
-        rows = self.step_no                      # cache rows written so far
+        # cache rows are write-once (row `step` of slot n is fresh at every step), so surviving
+        # hypotheses keep referencing their ancestors' rows wherever they live
+        self.slot = self.slot.index_select(0, reorder_state)
         if batch_idxs is not None:
             nb = batch_idxs.numel()
             kv = torch.empty(nb * self.Te, self.kv_all.shape[1], dtype=F16, device=self.dev)
@@ -74,47 +92,37 @@ class IncrementalDecoder:
             self.kv_all = kv
             self.enc_len32 = self.enc_len32.index_select(0, batch_idxs)
             self.bsz = nb
-            if self.spare.shape[1] != self.N:
-                self.spare = torch.empty(self.L, self.N, self.maxT, 2 * self.d, dtype=F16, device=self.dev)
-        K.kv_cache_gather(self.cache, self.spare, reorder_state.to(torch.int64), rows)
-        self.cache, self.spare = self.spare, self.cache
-        if self.spare.shape[1] != self.N:
-            self.spare = torch.empty_like(self.cache)
 
     def step(self, tokens_last, step, mode=MODE_NONE):
         """tokens_last [N] int64 (the token at position `step` of every hypothesis) -> lprobs [N, V]."""
         m, d, H, hd, N = self.m, self.d, self.H, self.hd, self.N
-        assert self.step_no == step and self.cache.shape[1] == N
+        assert self.step_no == step and self.slot.shape[0] == N
         tok = tokens_last.view(N, 1).contiguous()
         # SinusoidalPositionalEmbedding with incremental_state: position pad + 1 + step
         x = K.token_embed(tok, m.P("decoder.embed_tokens.weight"), self.pos[step:], N, 1, d, self.pad,
                           self.scale, 0.0, None)
-        klen = torch.full((N,), step + 1, dtype=torch.int32, device=self.dev)
+        self.slot[:, step] = self.slot_ids[:N]
         for l in range(self.L):
             p = f"decoder.layers.{l}"
             h1, _, _ = K.layernorm(x, m.P(p + ".self_attn_layer_norm.weight"), m.P(p + ".self_attn_layer_norm.bias"))
-            q = K.linear(h1, m.P(p + ".self_attn.q_proj.weight"), m.P(p + ".self_attn.q_proj.bias"))
+            q = _lin(h1, m.P(p + ".self_attn.q_proj.weight"), m.P(p + ".self_attn.q_proj.bias"))
             Wkv = m.params.span(p + ".self_attn.k_proj.weight", p + ".self_attn.v_proj.weight").view(2 * d, d)
             bkv = m.params.span(p + ".self_attn.k_proj.bias", p + ".self_attn.v_proj.bias")
             cl = self.cache[l]
-            K.linear(h1, Wkv, bkv, out=cl[:, step, :])   # K|V of this position, row stride maxT*2d
-            O = torch.empty(N, d, dtype=F16, device=self.dev)
-            K.mha_fwd(q, cl, cl[:, :, d:], O, d, 2 * d, 2 * d, d, N, H, 1, self.maxT, hd, hd ** -0.5,
-                      key_len=klen, sk=self.maxT * 2 * d, sv=self.maxT * 2 * d)
-            x2 = K.linear(O, m.P(p + ".self_attn.out_proj.weight"), m.P(p + ".self_attn.out_proj.bias"),
-                          epi=K.EPI_DROP_RESID, aux=x, p=0.0)
+            _lin(h1, Wkv, bkv, out=cl[:N, step, :])   # K|V of this position into slot n, row stride maxT*2d
+            O = K.decode_self_attn(q, cl, self.slot, N, H, hd, step + 1, hd ** -0.5)
+            x2 = _lin(O, m.P(p + ".self_attn.out_proj.weight"), m.P(p + ".self_attn.out_proj.bias"), aux=x)
             h2, _, _ = K.layernorm(x2, m.P(p + ".encoder_attn_layer_norm.weight"), m.P(p + ".encoder_attn_layer_norm.bias"))
-            q2 = K.linear(h2, m.P(p + ".encoder_attn.q_proj.weight"), m.P(p + ".encoder_attn.q_proj.bias"))
+            q2 = _lin(h2, m.P(p + ".encoder_attn.q_proj.weight"), m.P(p + ".encoder_attn.q_proj.bias"))
             kv = self.kv_all[:, 2 * d * l:2 * d * (l + 1)]
             ldkv = self.kv_all.stride(0)
             O2 = torch.empty(N, d, dtype=F16, device=self.dev)
             K.mha_fwd(q2, kv, kv[:, d:], O2, d, ldkv, ldkv, d, self.bsz, H, self.beam, self.Te, hd, hd ** -0.5,
                       key_len=self.enc_len32)
-            x3 = K.linear(O2, m.P(p + ".encoder_attn.out_proj.weight"), m.P(p + ".encoder_attn.out_proj.bias"),
-                          epi=K.EPI_DROP_RESID, aux=x2, p=0.0)
+            x3 = _lin(O2, m.P(p + ".encoder_attn.out_proj.weight"), m.P(p + ".encoder_attn.out_proj.bias"), aux=x2)
             h3, _, _ = K.layernorm(x3, m.P(p + ".final_layer_norm.weight"), m.P(p + ".final_layer_norm.bias"))
-            f1 = K.linear(h3, m.P(p + ".fc1.weight"), m.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP, p=0.0)
-            x = K.linear(f1, m.P(p + ".fc2.weight"), m.P(p + ".fc2.bias"), epi=K.EPI_DROP_RESID, aux=x3, p=0.0)
+            f1 = _lin(h3, m.P(p + ".fc1.weight"), m.P(p + ".fc1.bias"), relu=True)
+            x = _lin(f1, m.P(p + ".fc2.weight"), m.P(p + ".fc2.bias"), aux=x3)
         xl, _, _ = K.layernorm(x, m.P("decoder.layer_norm.weight"), m.P("decoder.layer_norm.bias"))
         logits = torch.empty(N, self.Vp, dtype=F16, device=self.dev)
         K.gemm(xl, m.P("decoder.embed_tokens.weight"), logits, N, self.V, d, lda=d, ldb=d, ldc=self.Vp)

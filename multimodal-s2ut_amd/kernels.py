@@ -681,6 +681,32 @@ def kv_cache_gather(src, dst, idx, rows):
     return dst
 
 
+def decode_self_attn(q, cache_l, slot, N, H, hd, T, scale, out=None):
+    """One decoder step of self-attention: cache_l [slots, maxT, 2*H*hd], slot int32 [>=N, maxT]."""
+    S, maxT, W = cache_l.shape
+    if W != 2 * H * hd or slot.dtype != torch.int32 or slot.shape[1] != maxT or slot.shape[0] < N or T > maxT:
+        raise ValueError(f"decode_self_attn: cache {tuple(cache_l.shape)} slot {tuple(slot.shape)} N={N} T={T}")
+    out = torch.empty(N, H * hd, dtype=F16, device=q.device) if out is None else out
+    call("mms2ut_decode_self_attn", q.data_ptr(), q.stride(0), cache_l.data_ptr(), slot.data_ptr(), N, H, hd,
+         maxT, int(T), W, out.data_ptr(), out.stride(0), float(scale), _s())
+    return out
+
+
+def linear_splitk(x, W, bias=None, *, aux=None, relu=False, splitk=4, out=None):
+    """out[M,N] = act(x @ W^T + bias) (+ aux) through `splitk` fp32 slabs and one reduction
+    launch — for small-M GEMMs (the decoder step) whose dozen tiles would otherwise run long
+    serial k-loops."""
+    M, Kd = x.shape
+    N = W.shape[0]
+    out = torch.empty(M, N, dtype=F16, device=x.device) if out is None else out
+    slabs = torch.empty(splitk, M, N, dtype=torch.float32, device=x.device)
+    gemm(x, W, slabs, M, N, Kd, lda=x.stride(0), ldb=W.stride(0), ldc=N, epi=EPI_F32, splitk=splitk,
+         sCsplit=M * N)
+    call("mms2ut_splitk_epilogue_f16", slabs.data_ptr(), splitk, M * N, M, N, _p(bias), _p(aux),
+         aux.stride(0) if aux is not None else 0, int(relu), out.data_ptr(), out.stride(0), _s())
+    return out
+
+
 def round_up(x, m):
     return (x + m - 1) // m * m
 

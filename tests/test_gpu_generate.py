@@ -143,3 +143,43 @@ def test_task_generator_surface(tmp_path):
     for h, d in zip(hyps, direct):
         assert len(h) == 4 and h[0]["tokens"].tolist() == d[0]["tokens"].tolist()
         assert set(h[0]) >= {"tokens", "score", "attention", "alignment", "positional_scores"}
+
+
+@pytest.mark.parametrize("hd,H,T", [(96, 8, 1), (96, 8, 77), (64, 4, 300), (128, 2, 65)])
+def test_decode_self_attn_through_slot_table(hd, H, T):
+    """decode_self_attn vs a torch fp32 reference on rows gathered through a random slot table."""
+    K = pkg("kernels")
+    g = torch.Generator().manual_seed(T)
+    N, S, maxT = 6, 9, T + 5
+    W = 2 * H * hd
+    cache = torch.randn(S, maxT, W, generator=g).half()
+    slot = torch.randint(0, S, (N, maxT), generator=g, dtype=torch.int32)
+    q = torch.randn(N, H * hd + 8, generator=g).half()          # padded row stride
+    out = K.decode_self_attn(q.cuda(), cache.cuda(), slot.cuda(), N, H, hd, T, hd ** -0.5).cpu().float()
+    rows = cache[slot[:, :T].long(), torch.arange(T)[None, :]].float()     # [N, T, W]
+    k = rows[:, :, : H * hd].view(N, T, H, hd)
+    v = rows[:, :, H * hd:].view(N, T, H, hd)
+    qq = q[:, : H * hd].float().view(N, H, hd)
+    p = torch.softmax(torch.einsum("nhd,nthd->nht", qq, k) * hd ** -0.5, -1)
+    ref = torch.einsum("nht,nthd->nhd", p, v).reshape(N, H * hd)
+    assert (out - ref).abs().max() < 2e-3 + 2e-3 * ref.abs().max()
+
+
+@pytest.mark.parametrize("M,N,Kd,s,relu,res", [(160, 768, 3072, 8, False, True), (37, 3072, 768, 3, True, False),
+                                                (200, 1536, 768, 2, False, False)])
+def test_linear_splitk_epilogue(M, N, Kd, s, relu, res):
+    """Split-K slabs + epilogue vs torch fp32: act(x W^T + b) (+ residual), fp16 out."""
+    K = pkg("kernels")
+    g = torch.Generator().manual_seed(M)
+    x = (torch.randn(M, Kd, generator=g) * 0.5).half()
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).half()
+    b = torch.randn(N, generator=g).half()
+    aux = torch.randn(M, N, generator=g).half() if res else None
+    out = K.linear_splitk(x.cuda(), W.cuda(), b.cuda(), aux=aux.cuda() if res else None, relu=relu,
+                          splitk=s).cpu().float()
+    ref = x.float() @ W.float().t() + b.float()
+    if relu:
+        ref = ref.clamp_min(0)
+    if res:
+        ref = ref.half().float() + aux.float()
+    assert (out - ref).abs().max() < 1e-2 + 2e-3 * ref.abs().max()
