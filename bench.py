@@ -56,10 +56,10 @@ def fwd_flops_per_utt(Ts, Tt, cfg, Ti=577, Di=768, fusion=True, split=False):
     return (f, mha) if split else f
 
 
-def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000):
+def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000, img_tokens=577):
     """nb length-bucketed batches (fairseq batch_by_size), spread evenly over the length
     distribution of a synthetic corpus; everything moved to HBM before timing."""
-    corpus = data.SyntheticSpeechMulti30K(n_utts=n_utts, seed=1 + rank, img_tokens=577,
+    corpus = data.SyntheticSpeechMulti30K(n_utts=n_utts, seed=1 + rank, img_tokens=img_tokens,
                                           img_dim=cfg["image_feat_dim"], with_images=cfg["fusion"])
     all_b = corpus.batches(max_tokens)
     pick = [all_b[int(i)] for i in np.linspace(0, len(all_b) - 1, nb).round()]
@@ -82,7 +82,8 @@ def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000):
         batch = runtime.prepare_batch(sample, cfg, device, src_override=src_dummy)
         tl = sample["target_lengths"].numpy()
         sl = sample["net_input"]["src_lengths"].numpy()
-        parts = [fwd_flops_per_utt(int(s), int(t), cfg, fusion=cfg["fusion"], split=True) for s, t in zip(sl, tl)]
+        parts = [fwd_flops_per_utt(int(s), int(t), cfg, Ti=img_tokens, Di=cfg["image_feat_dim"], fusion=cfg["fusion"],
+                                   split=True) for s, t in zip(sl, tl)]
         flops = sum(p[0] for p in parts)
         mha = sum(p[1] for p in parts)
         # GEMM-kernel share of the algorithmic FLOPs: everything but the multi-head attention
@@ -155,7 +156,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--max-tokens", type=int, default=40000)
     ap.add_argument("--nbatches", type=int, default=8)
-    ap.add_argument("--audio-only", action="store_true")
+    ap.add_argument("--audio-only", action="store_true", help="BASELINE configs[3]: no fusion tail")
+    ap.add_argument("--image-feats", choices=("vit", "detr"), default="vit",
+                    help="detr = BASELINE configs[4]: DETR feats [100, 256], SA_image_dropout 0.5, "
+                         "modality_dropout = audio_dropout = 0.5")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-timing", action="store_true")
@@ -165,11 +169,15 @@ def main():
     rank, world, local = parallel.init_from_env()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    cfg = mm.default_cfg(fusion=not args.audio_only)
+    detr = args.image_feats == "detr"
+    img_tokens = 100 if detr else 577
+    cfg = mm.default_cfg(fusion=not args.audio_only, **(dict(image_feat_dim=256, SA_image_dropout=0.5,
+                                                             modality_dropout=0.5, audio_dropout=0.5)
+                                                        if detr else {}))
     model = mm.MMS2UTModel(cfg, device=device).init_params(seed=1)
     tr = trainer_mod.Trainer(model, lr=5e-4, world_size=world, bucket_mb=args.bucket_mb)
     fe = frontend_mod.FbankFrontend(device)
-    batches = make_batches(cfg, rank, args.nbatches, args.max_tokens, device, fe)
+    batches = make_batches(cfg, rank, args.nbatches, args.max_tokens, device, fe, img_tokens=img_tokens)
 
     def step(i):
         wb, batch = batches[i % len(batches)][:2]
@@ -229,6 +237,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp16", "data": "synthetic (Speech-Multi30K-shaped; random-init weights)",
             "config": {"workload": ("mm_s2ut_transformer base audio-only" if args.audio_only else
+                                    "mm_s2ut_transformer base (DETR-256 x 100 image feats, SA_image_dropout 0.5, "
+                                    "modality/audio dropout 0.5)" if detr else
                                     "mm_s2ut_transformer base (ViT-768 image feats, multimodal_attention+gate)"),
                        "model": "mm_s2ut_transformer", "max_tokens": args.max_tokens,
                        "global_batch_frames_per_step": frames_all / args.steps,
