@@ -184,8 +184,19 @@ def main():
         batch.src = fe(wb)
         tr.train_step(batch)
 
+    # untimed loss-scale settling: the fp16 optimizer starts at scale 128 (fairseq --fp16-init-scale)
+    # and skips the update of every overflowing step while it halves the scale; run until a step
+    # completes (the overflow flag is the all-reduced one, identical on every rank) so the timed
+    # steps are complete optimizer steps
+    settle = 0
+    while settle < 16:
+        step(settle)
+        settle += 1
+        if not tr.opt.stats()["overflow"]:
+            break
     for i in range(args.warmup):
         step(i)
+    base = args.warmup   # the timed batch sequence does not depend on how many settling steps ran
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -196,7 +207,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(base + i)
     t_issue = time.perf_counter()  # host finished enqueueing (host-bound if ~ t1)
     torch.cuda.synchronize()
     if world > 1:
@@ -205,9 +216,9 @@ def main():
     gemm_ms, n_launch, launched_flops, gemm_bytes = (kernels.gemm_profile_end() if not args.no_gemm_timing
                                                      else (0.0, 0, 0.0, 0.0))
     elapsed = t1 - t0
-    frames = sum(int(batches[(args.warmup + i) % len(batches)][1].n_src_frames) for i in range(args.steps))
-    alg_flops = sum(batches[(args.warmup + i) % len(batches)][4] for i in range(args.steps))
-    total_flops = sum(batches[(args.warmup + i) % len(batches)][3] for i in range(args.steps))
+    frames = sum(int(batches[(base + i) % len(batches)][1].n_src_frames) for i in range(args.steps))
+    alg_flops = sum(batches[(base + i) % len(batches)][4] for i in range(args.steps))
+    total_flops = sum(batches[(base + i) % len(batches)][3] for i in range(args.steps))
     stats = torch.tensor([elapsed, frames, alg_flops, gemm_ms, n_launch, total_flops], dtype=torch.float64,
                          device=device)
     if world > 1:
@@ -221,7 +232,7 @@ def main():
     else:
         frames_all, flops_all, gemm_all, nl_all = float(frames), float(alg_flops), gemm_ms, float(n_launch)
         total_flops_all = float(total_flops)
-    ost = tr.opt.stats()
+    ost = dict(tr.opt.stats(), untimed_scale_settling_steps=settle)
     traffic, traffic_src = gemm_pmc_traffic()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -15,11 +15,20 @@ import torch.distributed as dist
 
 
 def init_from_env(backend=None):
-    """One process per GPU, launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE)."""
+    """One process per GPU, launched by torch.distributed.run (RANK/LOCAL_RANK/WORLD_SIZE).
+    Returns (rank, world, device index).  MMS2UT_DIST_BACKEND overrides the backend; with more
+    local ranks than devices (a gloo rehearsal of the N > 1 path on a one-GPU box) ranks share
+    devices round-robin."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if ndev > 0 and local >= ndev:
+        if os.environ.get("MMS2UT_DIST_BACKEND", "") != "gloo":
+            raise RuntimeError(f"LOCAL_RANK {local} but only {ndev} GPUs (RCCL needs one GPU per rank)")
+        local = local % ndev
     if world > 1 and not dist.is_initialized():
+        backend = backend or os.environ.get("MMS2UT_DIST_BACKEND") or None
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
