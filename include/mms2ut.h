@@ -130,6 +130,8 @@ int mms2ut_layernorm_bwd(const mms2ut_half* dy, const mms2ut_half* x, const mms2
                          mms2ut_half* dx, float* part, int64_t rows, int D, mms2ut_half* dxd,
                          float p, uint64_t seed, uint64_t offset, hipStream_t stream);
 int mms2ut_layernorm_bwd_parts(int64_t rows);
+/* number of [2*D] fp32 partial rows mms2ut_layernorm_bwd{,_ex} write for (rows, D) */
+int mms2ut_layernorm_bwd_nparts(int64_t rows, int D);
 /* layernorm_fwd with an output layout and dropout folded in (the fusion image path,
  * mm_s2s_transformer.py:188-190 image_pre_norm -> SA_image_dropout -> [B, Ti(+1), Di] keys):
  * input row r is written to output row (r / grp) * grp_out + r % grp (grp = 0: identity), and

@@ -66,6 +66,7 @@ SIGNATURES = {
     "mms2ut_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
     "mms2ut_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp, f32, u64, u64, vp]),
     "mms2ut_layernorm_bwd_parts": (i32, [i64]),
+    "mms2ut_layernorm_bwd_nparts": (i32, [i64, i32]),
     "mms2ut_layernorm_fwd_ex": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, f32, i64, i64, f32, u64, u64, vp]),
     "mms2ut_layernorm_bwd_ex": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp, f32, u64, u64, i64, i64,
                                       f32, u64, u64, vp]),

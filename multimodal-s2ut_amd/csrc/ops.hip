@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy,
 // blocking as ln_bwd_kernel (16 rows per block, part[block][2][D]); wave w takes row pairs w and
 // w + 4, all their loads (x, dy, dres) in flight at once.  dgamma / dbeta column partials are
 // folded across the two half-waves by a lane-32 shuffle and across the 4 waves through LDS.
-template <int C8>  // 16-B chunks per lane per row = D / 256
+template <int C8, int NP>  // 16-B chunks per lane per row = D / 256; row pairs per wave (8*NP rows per block)
 __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ dy, const h16* __restrict__ x,
                                                        const h16* __restrict__ g, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, const h16* __restrict__ dres,
@@ -224,13 +224,13 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
 #pragma unroll
     for (int e = 0; e < 8; ++e) { gam[c][e] = (float)gg[e]; dg[c][e] = 0.f; db[c][e] = 0.f; }
   }
-  const long rb = (long)blockIdx.x * LN_BWD_ROWS;
+  const long rb = (long)blockIdx.x * 8 * NP;
   const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
-  h16x8 xv[2][C8], dv[2][C8], rv[2][C8];
-  float mu[2], rs[2];
-  long row[2];
+  h16x8 xv[NP][C8], dv[NP][C8], rv[NP][C8];
+  float mu[NP], rs[NP];
+  long row[NP];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < NP; ++k) {
     row[k] = rb + 2 * (w + 4 * k) + half;
     const bool ok = row[k] < rows;
     mu[k] = ok ? mean[row[k]] : 0.f;
@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
     // separate dropout pass would store it
     const float dsi = 1.f / (1.f - pin);
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < NP; ++k)
 #pragma unroll
       for (int c = 0; c < C8; ++c) {
         bool k0[4], k1[4];
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
       }
   }
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < NP; ++k) {
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < C8; ++c)
@@ -772,8 +772,25 @@ extern "C" int mms2ut_layernorm_fwd_ex(const h16* x, const h16* gamma, const h16
   });
 }
 
+// row pairs per wave of ln_bwd16 (D % 256 == 0): MMS2UT_LN_NP in {1, 2, 4}, default 2
+static int ln16_np() {
+  const char* e = getenv("MMS2UT_LN_NP");
+  const int v = e ? atoi(e) : 2;
+  return (v == 1 || v == 4) ? v : 2;
+}
+
+static bool ln16_path(int D) {
+  const char* e16 = getenv("MMS2UT_LN16");
+  return D % 256 == 0 && D <= 1024 && !(e16 && e16[0] == '0');
+}
+
 extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
   return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
+}
+
+extern "C" int mms2ut_layernorm_bwd_nparts(int64_t rows, int D) {
+  const int rpb = ln16_path(D) ? 8 * ln16_np() : LN_BWD_ROWS;
+  return (int)((rows + rpb - 1) / rpb);
 }
 
 extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamma, const float* mean,
@@ -785,16 +802,17 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
   const uint32_t thresh = mms_drop_thresh(p);
   MMS_REQUIRE(D % 4 == 0 && D <= 1024, "layernorm_bwd: D must be a multiple of 4 and <= 1024");
   if (rows == 0) return 0;
-  const int nb = mms2ut_layernorm_bwd_parts(rows);
-  const char* e16 = getenv("MMS2UT_LN16");
-  if (D % 256 == 0 && D <= 1024 && !(e16 && e16[0] == '0')) {
-    switch (D / 256) {
-#define CASE(C) case C: hipLaunchKernelGGL((ln_bwd16_kernel<C>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, rstd, \
-                                          dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset, 0L, 0L, \
-                                          0.f, 0u, (uint64_t)0, (uint64_t)0); break;
-      CASE(1) CASE(2) CASE(3) CASE(4)
-#undef CASE
+  const int nb = mms2ut_layernorm_bwd_nparts(rows, D);
+  if (ln16_path(D)) {
+    const int np = ln16_np();
+#define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
+                                          gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
+                                          offset, 0L, 0L, 0.f, 0u, (uint64_t)0, (uint64_t)0); break;
+    switch ((D / 256) * 8 + np) {
+      CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1) CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
+      CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
     }
+#undef CASE
     return mms::check_launch("layernorm_bwd16");
   }
   return pick_cpl(D / 4, [&](auto C) {
@@ -820,15 +838,18 @@ extern "C" int mms2ut_layernorm_bwd_ex(const h16* dy, const h16* x, const h16* g
   MMS_REQUIRE(D % 256 == 0 && D <= 1024, "layernorm_bwd_ex: D must be a multiple of 256 and <= 1024");
   MMS_REQUIRE(dy_grp >= 0 && (dy_grp == 0 || dy_grp_out >= dy_grp), "layernorm_bwd_ex: need dy_grp_out >= dy_grp");
   if (rows == 0) return 0;
-  const int nb = mms2ut_layernorm_bwd_parts(rows);
+  MMS_REQUIRE(ln16_path(D), "layernorm_bwd_ex: the 16-B path is disabled (MMS2UT_LN16=0)");
+  const int nb = mms2ut_layernorm_bwd_nparts(rows, D);
   const uint32_t thresh = mms_drop_thresh(p), thin = mms_drop_thresh(dy_p);
-  switch (D / 256) {
-#define CASE(C) case C: hipLaunchKernelGGL((ln_bwd16_kernel<C>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, rstd, \
-                                          dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset, \
-                                          (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset); break;
-    CASE(1) CASE(2) CASE(3) CASE(4)
-#undef CASE
+  const int np = ln16_np();
+#define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
+                                          gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
+                                          offset, (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset); break;
+  switch ((D / 256) * 8 + np) {
+    CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1) CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
+    CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
   }
+#undef CASE
   return mms::check_launch("layernorm_bwd_ex");
 }
 

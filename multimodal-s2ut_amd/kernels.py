@@ -402,7 +402,7 @@ def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None,
     if dy_grp or dy_p > 0:
         assert emit is None and D % 256 == 0 and D <= 1024
         L = _lib.load()
-        nparts = L.mms2ut_layernorm_bwd_parts(R)
+        nparts = L.mms2ut_layernorm_bwd_nparts(R, D)
         part = torch.empty(nparts, 2 * D, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x) if want_dx else None
         seed, off = dy_drop if dy_p > 0 else (0, 0)
@@ -414,7 +414,7 @@ def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None,
             call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), 0, _s())
         return dx
     L = _lib.load()
-    nparts = L.mms2ut_layernorm_bwd_parts(R)
+    nparts = L.mms2ut_layernorm_bwd_nparts(R, D)
     part = torch.empty(nparts, 2 * D, dtype=torch.float32, device=x.device)
     dx = torch.empty_like(x) if want_dx else None
     dxd, p, seed, off = None, 0.0, 0, 0
