@@ -306,11 +306,17 @@ int mms2ut_log_softmax_step(const mms2ut_half* logits, int64_t ld, int64_t rows,
 /* One step of decoder self-attention against the K|V cache of one layer,
  * cache [slots][maxT][width = 2*H*hd] (K in columns [0, H*hd), V in [H*hd, 2*H*hd)), addressed
  * through slot [N][maxT] int32: key/value row t (t < T) of hypothesis n is row t of cache slot
- * slot[n][t] (beam reorders permute the table, not the cache).  q [N][ldq] (head h at column
- * h*hd), out [N][ldo] fp16; softmax(scale q k^T) v per head in fp32.                           */
-int mms2ut_decode_self_attn(const mms2ut_half* q, int64_t ldq, const mms2ut_half* cache, const int32_t* slot,
-                            int N, int H, int hd, int maxT, int T, int64_t width, mms2ut_half* out,
-                            int64_t ldo, float scale, hipStream_t stream);
+ * slot[n][t] (beam reorders permute the table, not the cache).  T = *step + 1 is read on the
+ * device (the step replays as a graph); row T-1 is this step's K|V, read from kv_new [N][ld_new]
+ * and stored into row T-1 of slot n (slot[n][T-1] = n).  q [N][ldq] (head h at column h*hd),
+ * out [N][ldo] fp16; softmax(scale q k^T) v per head in fp32.                                 */
+int mms2ut_decode_self_attn(const mms2ut_half* q, int64_t ldq, mms2ut_half* cache, int32_t* slot, int N, int H,
+                            int hd, int maxT, const int32_t* step, const mms2ut_half* kv_new, int64_t ld_new,
+                            int64_t width, mms2ut_half* out, int64_t ldo, float scale, hipStream_t stream);
+/* fairseq TransformerDecoder incremental embedding: x[n] = scale*E[tok[n]] + pos[pad+1+*step]
+ * (E [V][D], pos sinusoid table [>= pad+2+step][D], fp16; step on the device).             */
+int mms2ut_decode_embed(const int64_t* tok, const mms2ut_half* E, const mms2ut_half* pos, const int32_t* step,
+                        int pad_idx, mms2ut_half* x, int N, int D, float scale, hipStream_t stream);
 /* Decoder-step split-K epilogue: out[rows][cols] (fp16, row stride ldo) = act(sum of nsplit fp32
  * slabs [rows][cols] (slab elements apart) + bias) (+ aux, row stride ldaux); act = ReLU if relu.
  * bias / aux may be null.                                                                      */

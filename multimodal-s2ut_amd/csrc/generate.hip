@@ -71,28 +71,39 @@ constexpr int DEC_THREADS = 256;
 
 template <int HD>
 __global__ void __launch_bounds__(DEC_THREADS) decode_attn_kernel(const h16* __restrict__ q, long ldq,
-                                                                  const h16* __restrict__ cache,
-                                                                  const int* __restrict__ slot, int H, int maxT,
-                                                                  int T, long width, h16* __restrict__ out,
-                                                                  long ldo, float scale) {
+                                                                  h16* __restrict__ cache, int* __restrict__ slot,
+                                                                  int H, int maxT, const int* __restrict__ step_ptr,
+                                                                  const h16* __restrict__ kv_new, long ld_new,
+                                                                  long width, h16* __restrict__ out, long ldo,
+                                                                  float scale) {
   constexpr int VL = HD / 8;                  // threads per V row (16-B vectors)
   constexpr int G = DEC_THREADS / VL;         // V rows in flight
   extern __shared__ float s_dyn[];
-  float* s_p = s_dyn;                                         // [T] scores -> probabilities
-  long* s_off = reinterpret_cast<long*>(s_dyn + ((T + 1) & ~1));  // [T] element offsets of the rows
+  float* s_p = s_dyn;                                           // [maxT] scores -> probabilities
+  long* s_off = reinterpret_cast<long*>(s_dyn + ((maxT + 1) & ~1));  // [maxT] element offsets of the rows
   __shared__ float s_part[G][HD];
   __shared__ float s_red[DEC_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = blockIdx.x / H, h = blockIdx.x % H;
+  // T = step + 1 read on the device (graph-replayable); row T-1 is this step's K|V, taken from the
+  // projection's staging rows and stored into row T-1 of slot n for the steps that follow
+  const int T = min(*step_ptr + 1, maxT);
+  const h16* kvn = kv_new + (long)n * ld_new;
+  if (tid < 2 * VL) {
+    const long col = (tid < VL ? 0 : width / 2) + h * HD + (tid % VL) * 8;
+    *reinterpret_cast<s16x8*>(cache + ((long)n * maxT + (T - 1)) * width + col) =
+        *reinterpret_cast<const s16x8*>(kvn + col);
+  }
+  if (h == 0 && tid == 0) slot[(long)n * maxT + T - 1] = n;
   s16x8 qv[VL];
   const h16* qr = q + (long)n * ldq + h * HD;
 #pragma unroll
   for (int i = 0; i < VL; ++i) qv[i] = reinterpret_cast<const s16x8*>(qr)[i];
-  const int* sl = slot + (long)n * maxT;
+  const int* sl = slot + (long)n * maxT;   // entry T-1 is n (written above, not read back)
   float mx = -INFINITY;
   for (int t = tid; t < T; t += DEC_THREADS) {
     const long off = ((long)sl[t] * maxT + t) * width + h * HD;
-    const h16* kr = cache + off;
+    const h16* kr = t == T - 1 ? kvn + h * HD : cache + off;
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < VL; ++i) {
@@ -128,7 +139,8 @@ __global__ void __launch_bounds__(DEC_THREADS) decode_attn_kernel(const h16* __r
     const long vcol = width / 2 + c * 8;
 #pragma unroll 4
     for (int t = g; t < T; t += G) {
-      const h16x8 v = __builtin_bit_cast(h16x8, *reinterpret_cast<const s16x8*>(cache + s_off[t] + vcol));
+      const h16* vr = t == T - 1 ? kvn + h * HD + vcol : cache + s_off[t] + vcol;
+      const h16x8 v = __builtin_bit_cast(h16x8, *reinterpret_cast<const s16x8*>(vr));
       const float pt = s_p[t];
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] += pt * (float)v[e];
@@ -179,6 +191,28 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(const float* __res
   }
 }
 
+// fairseq TransformerDecoder embedding for one incremental step: x[n] = scale * E[tok[n]] +
+// pos[pad + 1 + step] (SinusoidalPositionalEmbedding with incremental_state), step read on the
+// device so the decoder step can be replayed as a graph.  fp32 arithmetic, one fp16 rounding (as
+// token_embed_fwd).  One wave per hypothesis row.
+__global__ void __launch_bounds__(256) decode_embed_kernel(const int64_t* __restrict__ tok, const h16* __restrict__ E,
+                                                           const h16* __restrict__ pos, const int* __restrict__ step_ptr,
+                                                           int pad, h16* __restrict__ x, int N, int D, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const long prow = (long)(pad + 1 + *step_ptr) * D;
+  const long erow = tok[n] * (long)D;
+  for (int d0 = lane * 4; d0 < D; d0 += 256) {
+    const h16x4 ev = *reinterpret_cast<const h16x4*>(E + erow + d0);
+    const h16x4 pv = *reinterpret_cast<const h16x4*>(pos + prow + d0);
+    h16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (h16)(scale * (float)ev[e] + (float)pv[e]);
+    *reinterpret_cast<h16x4*>(x + (long)n * D + d0) = o;
+  }
+}
+
 }  // namespace
 
 extern "C" int mms2ut_log_softmax_step(const h16* logits, int64_t ld, int64_t rows, int V, int pad_idx,
@@ -204,26 +238,33 @@ extern "C" int mms2ut_kv_cache_gather(const h16* src, h16* dst, const int64_t* i
   return mms::check_launch("kv_cache_gather");
 }
 
-extern "C" int mms2ut_decode_self_attn(const h16* q, int64_t ldq, const h16* cache, const int32_t* slot, int N,
-                                       int H, int hd, int maxT, int T, int64_t width, h16* out, int64_t ldo,
-                                       float scale, hipStream_t s) {
-  MMS_REQUIRE(T >= 1 && T <= maxT, "decode_self_attn: T must be in [1, maxT]");
-  MMS_REQUIRE(width == 2L * H * hd && ldq % 8 == 0 && width % 8 == 0,
-              "decode_self_attn: width must be 2*H*hd, ldq / width multiples of 8");
-  const size_t lds = (size_t)((T + 1) & ~1) * 4 + (size_t)T * 8;
-  MMS_REQUIRE(lds <= 96 * 1024, "decode_self_attn: T too long for the LDS score rows");
+extern "C" int mms2ut_decode_self_attn(const h16* q, int64_t ldq, h16* cache, int32_t* slot, int N, int H,
+                                       int hd, int maxT, const int32_t* step, const h16* kv_new, int64_t ld_new,
+                                       int64_t width, h16* out, int64_t ldo, float scale, hipStream_t s) {
+  MMS_REQUIRE(width == 2L * H * hd && ldq % 8 == 0 && width % 8 == 0 && ld_new % 8 == 0,
+              "decode_self_attn: width must be 2*H*hd, ldq / width / ld_new multiples of 8");
+  const size_t lds = (size_t)((maxT + 1) & ~1) * 4 + (size_t)maxT * 8;
+  MMS_REQUIRE(lds <= 64 * 1024, "decode_self_attn: maxT too long for the LDS score rows (<= 5400)");
   if (N == 0) return 0;
   const dim3 grid(N * H);
   switch (hd) {
-    case 64: hipLaunchKernelGGL(decode_attn_kernel<64>, grid, dim3(DEC_THREADS), lds, s, q, (long)ldq, cache,
-                                slot, H, maxT, T, (long)width, out, (long)ldo, scale); break;
-    case 96: hipLaunchKernelGGL(decode_attn_kernel<96>, grid, dim3(DEC_THREADS), lds, s, q, (long)ldq, cache,
-                                slot, H, maxT, T, (long)width, out, (long)ldo, scale); break;
-    case 128: hipLaunchKernelGGL(decode_attn_kernel<128>, grid, dim3(DEC_THREADS), lds, s, q, (long)ldq, cache,
-                                 slot, H, maxT, T, (long)width, out, (long)ldo, scale); break;
+#define CASE(HD) case HD: hipLaunchKernelGGL(decode_attn_kernel<HD>, grid, dim3(DEC_THREADS), lds, s, q, (long)ldq, \
+                                             cache, slot, H, maxT, step, kv_new, (long)ld_new, (long)width, out, \
+                                             (long)ldo, scale); break;
+    CASE(64) CASE(96) CASE(128)
+#undef CASE
     default: mms::set_error("decode_self_attn: head dim must be 64, 96 or 128"); return 1;
   }
   return mms::check_launch("decode_self_attn");
+}
+
+extern "C" int mms2ut_decode_embed(const int64_t* tok, const h16* E, const h16* pos, const int32_t* step, int pad_idx,
+                                   h16* x, int N, int D, float scale, hipStream_t s) {
+  MMS_REQUIRE(D % 4 == 0, "decode_embed: D must be a multiple of 4");
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(decode_embed_kernel, dim3((N + 3) / 4), dim3(256), 0, s, tok, E, pos, step, pad_idx, x, N, D,
+                     scale);
+  return mms::check_launch("decode_embed");
 }
 
 extern "C" int mms2ut_splitk_epilogue_f16(const float* slabs, int nsplit, int64_t slab, int rows, int cols,

@@ -23,6 +23,7 @@ Two parts:
   (the CPU tests drive it with a toy decoder against oracle/ref_generate.py).
 """
 import math
+import os
 
 import torch
 
@@ -47,7 +48,7 @@ def _lin(x, W, b, *, aux=None, relu=False, out=None):
 
 
 class IncrementalDecoder:
-    def __init__(self, model, enc, enc_len32, Te, bsz, beam, max_len):
+    def __init__(self, model, enc, enc_len32, Te, bsz, beam, max_len, graphs=None):
         """enc [bsz*Te, d] fp16 (rows b*Te + t, the encoder's output incl. fusion), enc_len32 [bsz]."""
         self.m = model
         cfg = model.cfg
@@ -68,11 +69,21 @@ class IncrementalDecoder:
         N = bsz * beam
         self.cache = torch.empty(self.L, N, self.maxT, 2 * self.d, dtype=F16, device=dev)
         self.slot = torch.zeros(N, self.maxT, dtype=torch.int32, device=dev)
-        self.slot_ids = torch.arange(N, dtype=torch.int32, device=dev)
+        self.slot_tmp = torch.empty_like(self.slot)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.tok = torch.zeros(N, dtype=torch.long, device=dev)
         self.pos = model._ensure_pos(self.maxT + 2, "dec")
         self.scale = 1.0 if cfg["no_scale_embedding"] else math.sqrt(self.d)
         self.Vp = K.round_up(self.V, 64)
+        self.logits = torch.empty(N, self.Vp, dtype=F16, device=dev)
         self.step_no = 0
+        # the decoder step is ~100 launches of fixed shapes: replay it as one HIP graph (recaptured
+        # when finished sentences shrink the batch); MMS2UT_DECODE_GRAPH=0 runs it eagerly
+        if graphs is None:
+            graphs = os.environ.get("MMS2UT_DECODE_GRAPH", "1") != "0"
+        self.use_graphs = graphs
+        self.graph = None
+        self.eager_steps = 0
 
     @property
     def N(self):
@@ -80,37 +91,41 @@ class IncrementalDecoder:
 
     def reorder(self, reorder_state, batch_idxs=None):
         """reorder_incremental_state(reorder_state) + reorder_encoder_out: reorder_state [N_new]
-        indexes the current hypotheses (fairseq's corrected index into the previous batch)."""
-        # cache rows are write-once (row `step` of slot n is fresh at every step), so surviving
-        # hypotheses keep referencing their ancestors' rows wherever they live
+        indexes the current hypotheses (fairseq's corrected index into the previous batch).
+        Cache rows are write-once (row `step` of slot n is fresh at every step), so surviving
+        hypotheses keep referencing their ancestors' rows wherever they live: only the slot table
+        moves (in place while the batch keeps its size, so a captured step graph stays valid)."""
+        if batch_idxs is None:
+            torch.index_select(self.slot, 0, reorder_state, out=self.slot_tmp)
+            self.slot.copy_(self.slot_tmp)
+            return
         self.slot = self.slot.index_select(0, reorder_state)
-        if batch_idxs is not None:
-            nb = batch_idxs.numel()
-            kv = torch.empty(nb * self.Te, self.kv_all.shape[1], dtype=F16, device=self.dev)
-            K.kv_cache_gather(self.kv_all.view(1, self.bsz, self.Te, -1), kv.view(1, nb, self.Te, -1),
-                              batch_idxs.to(torch.int64), self.Te)
-            self.kv_all = kv
-            self.enc_len32 = self.enc_len32.index_select(0, batch_idxs)
-            self.bsz = nb
+        self.slot_tmp = torch.empty_like(self.slot)
+        nb = batch_idxs.numel()
+        kv = torch.empty(nb * self.Te, self.kv_all.shape[1], dtype=F16, device=self.dev)
+        K.kv_cache_gather(self.kv_all.view(1, self.bsz, self.Te, -1), kv.view(1, nb, self.Te, -1),
+                          batch_idxs.to(torch.int64), self.Te)
+        self.kv_all = kv
+        self.enc_len32 = self.enc_len32.index_select(0, batch_idxs)
+        self.bsz = nb
+        self.tok = torch.zeros(self.N, dtype=torch.long, device=self.dev)
+        self.logits = torch.empty(self.N, self.Vp, dtype=F16, device=self.dev)
+        self.graph = None
+        self.eager_steps = 0
 
-    def step(self, tokens_last, step, mode=MODE_NONE):
-        """tokens_last [N] int64 (the token at position `step` of every hypothesis) -> lprobs [N, V]."""
+    def _body(self):
+        """One decoder step over the static buffers (tok, step_dev, slot, cache) -> self.logits."""
         m, d, H, hd, N = self.m, self.d, self.H, self.hd, self.N
-        assert self.step_no == step and self.slot.shape[0] == N
-        tok = tokens_last.view(N, 1).contiguous()
-        # SinusoidalPositionalEmbedding with incremental_state: position pad + 1 + step
-        x = K.token_embed(tok, m.P("decoder.embed_tokens.weight"), self.pos[step:], N, 1, d, self.pad,
-                          self.scale, 0.0, None)
-        self.slot[:, step] = self.slot_ids[:N]
+        x = K.decode_embed(self.tok, m.P("decoder.embed_tokens.weight"), self.pos, self.step_dev, self.pad, N, d,
+                           self.scale)
         for l in range(self.L):
             p = f"decoder.layers.{l}"
             h1, _, _ = K.layernorm(x, m.P(p + ".self_attn_layer_norm.weight"), m.P(p + ".self_attn_layer_norm.bias"))
             q = _lin(h1, m.P(p + ".self_attn.q_proj.weight"), m.P(p + ".self_attn.q_proj.bias"))
             Wkv = m.params.span(p + ".self_attn.k_proj.weight", p + ".self_attn.v_proj.weight").view(2 * d, d)
             bkv = m.params.span(p + ".self_attn.k_proj.bias", p + ".self_attn.v_proj.bias")
-            cl = self.cache[l]
-            _lin(h1, Wkv, bkv, out=cl[:N, step, :])   # K|V of this position into slot n, row stride maxT*2d
-            O = K.decode_self_attn(q, cl, self.slot, N, H, hd, step + 1, hd ** -0.5)
+            kvn = _lin(h1, Wkv, bkv)                 # this step's K|V rows, stored into the cache by the attention
+            O = K.decode_self_attn(q, self.cache[l], self.slot, N, H, hd, self.step_dev, kvn, hd ** -0.5)
             x2 = _lin(O, m.P(p + ".self_attn.out_proj.weight"), m.P(p + ".self_attn.out_proj.bias"), aux=x)
             h2, _, _ = K.layernorm(x2, m.P(p + ".encoder_attn_layer_norm.weight"), m.P(p + ".encoder_attn_layer_norm.bias"))
             q2 = _lin(h2, m.P(p + ".encoder_attn.q_proj.weight"), m.P(p + ".encoder_attn.q_proj.bias"))
@@ -124,10 +139,26 @@ class IncrementalDecoder:
             f1 = _lin(h3, m.P(p + ".fc1.weight"), m.P(p + ".fc1.bias"), relu=True)
             x = _lin(f1, m.P(p + ".fc2.weight"), m.P(p + ".fc2.bias"), aux=x3)
         xl, _, _ = K.layernorm(x, m.P("decoder.layer_norm.weight"), m.P("decoder.layer_norm.bias"))
-        logits = torch.empty(N, self.Vp, dtype=F16, device=self.dev)
-        K.gemm(xl, m.P("decoder.embed_tokens.weight"), logits, N, self.V, d, lda=d, ldb=d, ldc=self.Vp)
+        K.gemm(xl, m.P("decoder.embed_tokens.weight"), self.logits, N, self.V, d, lda=d, ldb=d, ldc=self.Vp)
+
+    def step(self, tokens_last, step, mode=MODE_NONE):
+        """tokens_last [N] int64 (the token at position `step` of every hypothesis) -> lprobs [N, V]."""
+        assert self.step_no == step and self.slot.shape[0] == self.N and step + 1 < self.maxT
+        self.tok.copy_(tokens_last)
+        self.step_dev.fill_(step)
+        if self.graph is not None:
+            self.graph.replay()
+        elif self.use_graphs and self.eager_steps >= 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body()
+            self.graph = g
+            g.replay()
+        else:
+            self._body()
+            self.eager_steps += 1
         self.step_no += 1
-        return K.log_softmax_step(logits, self.V, self.pad, self.eos, mode)
+        return K.log_softmax_step(self.logits, self.V, self.pad, self.eos, mode)
 
 
 class SequenceGenerator:

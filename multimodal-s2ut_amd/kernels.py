@@ -681,14 +681,24 @@ def kv_cache_gather(src, dst, idx, rows):
     return dst
 
 
-def decode_self_attn(q, cache_l, slot, N, H, hd, T, scale, out=None):
-    """One decoder step of self-attention: cache_l [slots, maxT, 2*H*hd], slot int32 [>=N, maxT]."""
+def decode_self_attn(q, cache_l, slot, N, H, hd, step_dev, kv_new, scale, out=None):
+    """One decoder step of self-attention: cache_l [slots, maxT, 2*H*hd], slot int32 [>=N, maxT],
+    step_dev int32 [1] (T = step + 1), kv_new [N, 2*H*hd] this step's K|V rows (stored into the cache)."""
     S, maxT, W = cache_l.shape
-    if W != 2 * H * hd or slot.dtype != torch.int32 or slot.shape[1] != maxT or slot.shape[0] < N or T > maxT:
-        raise ValueError(f"decode_self_attn: cache {tuple(cache_l.shape)} slot {tuple(slot.shape)} N={N} T={T}")
+    if W != 2 * H * hd or slot.dtype != torch.int32 or slot.shape[1] != maxT or slot.shape[0] < N or S < N \
+            or kv_new.shape[1] != W or step_dev.dtype != torch.int32:
+        raise ValueError(f"decode_self_attn: cache {tuple(cache_l.shape)} slot {tuple(slot.shape)} N={N}")
     out = torch.empty(N, H * hd, dtype=F16, device=q.device) if out is None else out
     call("mms2ut_decode_self_attn", q.data_ptr(), q.stride(0), cache_l.data_ptr(), slot.data_ptr(), N, H, hd,
-         maxT, int(T), W, out.data_ptr(), out.stride(0), float(scale), _s())
+         maxT, step_dev.data_ptr(), kv_new.data_ptr(), kv_new.stride(0), W, out.data_ptr(), out.stride(0),
+         float(scale), _s())
+    return out
+
+
+def decode_embed(tok, E, pos, step_dev, pad, N, D, scale, out=None):
+    out = torch.empty(N, D, dtype=F16, device=E.device) if out is None else out
+    call("mms2ut_decode_embed", tok.data_ptr(), E.data_ptr(), pos.data_ptr(), step_dev.data_ptr(), int(pad),
+         out.data_ptr(), N, D, float(scale), _s())
     return out
 
 

@@ -147,22 +147,50 @@ def test_task_generator_surface(tmp_path):
 
 @pytest.mark.parametrize("hd,H,T", [(96, 8, 1), (96, 8, 77), (64, 4, 300), (128, 2, 65)])
 def test_decode_self_attn_through_slot_table(hd, H, T):
-    """decode_self_attn vs a torch fp32 reference on rows gathered through a random slot table."""
+    """decode_self_attn vs a torch fp32 reference: rows t < T-1 gathered through a random slot table,
+    row T-1 = this step's K|V (kv_new), which the kernel also stores into row T-1 of slot n and
+    records in the table."""
     K = pkg("kernels")
     g = torch.Generator().manual_seed(T)
-    N, S, maxT = 6, 9, T + 5
+    N, maxT = 6, T + 5
     W = 2 * H * hd
-    cache = torch.randn(S, maxT, W, generator=g).half()
-    slot = torch.randint(0, S, (N, maxT), generator=g, dtype=torch.int32)
-    q = torch.randn(N, H * hd + 8, generator=g).half()          # padded row stride
-    out = K.decode_self_attn(q.cuda(), cache.cuda(), slot.cuda(), N, H, hd, T, hd ** -0.5).cpu().float()
+    cache = torch.randn(N, maxT, W, generator=g).half()
+    slot = torch.randint(0, N, (N, maxT), generator=g, dtype=torch.int32)
+    kv_new = torch.randn(N, W + 16, generator=g).half()              # padded row stride
+    q = torch.randn(N, H * hd + 8, generator=g).half()
+    step = torch.tensor([T - 1], dtype=torch.int32)
+    cache_d, slot_d = cache.cuda(), slot.cuda()
+    out = K.decode_self_attn(q.cuda(), cache_d, slot_d, N, H, hd, step.cuda(), kv_new.cuda()[:, :W],
+                             hd ** -0.5).cpu().float()
     rows = cache[slot[:, :T].long(), torch.arange(T)[None, :]].float()     # [N, T, W]
+    rows[:, T - 1] = kv_new[:, :W].float()
     k = rows[:, :, : H * hd].view(N, T, H, hd)
     v = rows[:, :, H * hd:].view(N, T, H, hd)
     qq = q[:, : H * hd].float().view(N, H, hd)
     p = torch.softmax(torch.einsum("nhd,nthd->nht", qq, k) * hd ** -0.5, -1)
     ref = torch.einsum("nht,nthd->nhd", p, v).reshape(N, H * hd)
     assert (out - ref).abs().max() < 2e-3 + 2e-3 * ref.abs().max()
+    cache_h, slot_h = cache_d.cpu(), slot_d.cpu()
+    assert torch.equal(cache_h[:, T - 1], kv_new[:, :W])                # stored into slot n, row T-1
+    assert torch.equal(slot_h[:, T - 1], torch.arange(N, dtype=torch.int32))
+    keep = torch.ones(maxT, dtype=torch.bool)
+    keep[T - 1] = False
+    assert torch.equal(cache_h[:, keep], cache[:, keep]) and torch.equal(slot_h[:, keep], slot[:, keep])
+
+
+def test_decode_graph_replay_matches_eager():
+    """The step replayed as a HIP graph gives the eager step's lprobs bit for bit (same kernels)."""
+    import os
+    mm, cfg, P, model, batch, enc_ref, pad_ref = _setup(sharpen=6.0, lengths=(61, 47, 40), seed=5)
+    os.environ["MMS2UT_DECODE_GRAPH"] = "0"
+    try:
+        eager = mm.generate.generate(model, batch, beam_size=4, max_len_a=0.0, max_len_b=10)
+    finally:
+        os.environ.pop("MMS2UT_DECODE_GRAPH")
+    graph = mm.generate.generate(model, batch, beam_size=4, max_len_a=0.0, max_len_b=10)
+    for he, hg in zip(eager, graph):
+        for a, b in zip(he, hg):
+            assert torch.equal(a["tokens"], b["tokens"]) and a["score"] == b["score"]
 
 
 @pytest.mark.parametrize("M,N,Kd,s,relu,res", [(160, 768, 3072, 8, False, True), (37, 3072, 768, 3, True, False),
