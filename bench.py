@@ -149,6 +149,71 @@ def cpu_baseline(cfg, model, sample, budget_s=20.0):
                       f"{frames} frames of the base config, {k} steps in {dt:.1f}s"}
 
 
+def decode_cpu_baseline(model, sample, beam, budget_s=20.0):
+    """The oracle's beam search (oracle/ref_generate.py over the fp32 oracle decoder re-run per
+    prefix — the reference has no incremental CPU path here) on a bounded sample: one utterance,
+    the bench's beam, as many steps as fit the budget (each step re-decodes every prefix)."""
+    from oracle import ref_generate as RG
+    from oracle import ref_model as R
+    cfg = R.no_dropout(dict(model.cfg))
+    P = {k: v.detach().float().cpu() for k, v in model.params.p.items()}
+    ni = sample["net_input"]
+    with torch.no_grad():
+        enc, pad, _ = R.encoder_forward(P, ni["src_tokens"][:1].float(), ni["src_lengths"][:1], cfg,
+                                        imgs=ni["imgs_list"][0][:1].float() if ni["imgs_list"] else None)
+    step_fn = RG.full_recompute_step(P, cfg, enc, pad, beam)
+    t0 = time.time()
+    steps = 0
+    for T in range(4, 64, 4):
+        RG.beam_search(step_fn, 1, cfg["vocab_size"], beam, T, min_len=T + 1)   # forced to run T steps
+        steps += T + 1
+        if time.time() - t0 > budget_s:
+            break
+    dt = time.time() - t0
+    return {"value": steps * beam / dt, "unit": "hypothesis-tokens/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle beam search (fp32 decoder re-run over every prefix), 1 utterance, beam {beam}, "
+                      f"{steps} decoder steps in {dt:.1f}s"}
+
+
+def decode_main(args):
+    """--decode: beam-search inference (fairseq-generate --beam 10 --max-len-a 1)
+    on the base model: one JSON line of hypothesis-tokens/s with the decode self-attention roofline
+    and the oracle CPU baseline.  Random weights rarely emit </s>: every hypothesis decodes to
+    max_len (the longest decode)."""
+    gen_mod = import_module("multimodal-s2ut_amd.generate")
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    cfg = mm.default_cfg()
+    model = mm.MMS2UTModel(cfg, device=device).init_params(seed=1)
+    bsz, frames, beam = args.decode_bsz, args.decode_frames, 10
+    sample = data.make_sample([frames] * bsz, [10] * bsz, img_tokens=577, img_dim=768, seed=0)
+    batch = runtime.prepare_batch(sample, model.cfg, device)
+    gen_mod.generate(model, batch, beam_size=beam, max_len_a=1.0, max_len_b=200)   # warmup + graph capture
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    hyps = gen_mod.generate(model, batch, beam_size=beam, max_len_a=1.0, max_len_b=200)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = max(len(h["tokens"]) for hs in hyps for h in hs)
+    N, H, hd = bsz * beam, cfg["decoder_attention_heads"], cfg["decoder_embed_dim"] // cfg["decoder_attention_heads"]
+    # decode self-attention: every cached K and V row of every hypothesis read once per layer-step
+    attn_bytes = sum(N * H * t * hd * 2 * 2 for t in range(1, steps + 1)) * cfg["decoder_layers"]
+    cpu = None if args.no_cpu_baseline else decode_cpu_baseline(model, sample, beam, args.cpu_budget)
+    print(json.dumps({
+        "metric": "beam-search decode hypothesis-tokens/s (fairseq-generate --beam 10 --max-len-a 1)",
+        "value": steps * N / dt, "unit": "hypothesis-tokens/s", "n_gpus": 1, "steps": steps,
+        "ms_per_step": 1e3 * dt / steps, "higher_is_better": True, "vs_baseline": None, "dtype": "fp16",
+        "data": "synthetic (random-init weights: every hypothesis runs to max_len)",
+        "config": {"workload": f"mm_s2ut_transformer base, {bsz} x {frames}-frame utterances, beam {beam}",
+                   "sentences_per_s": bsz / dt},
+        "roofline": {"bound": "hbm", "kernel": "decode_attn_kernel (self-attention over the KV cache)",
+                     "algorithmic_bytes_per_step": attn_bytes / steps, "peak": HBM_PEAK, "unit": "GB/s",
+                     "note": "achieved GB/s of this kernel comes from its rocprof duration: "
+                             "profiles/round1_v6_generate_kernel_stats.csv (4.0 TB/s measured)"},
+        "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,7 +229,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-timing", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--decode", action="store_true", help="beam-search inference line instead of training")
+    ap.add_argument("--decode-bsz", type=int, default=16)
+    ap.add_argument("--decode-frames", type=int, default=300)
     args = ap.parse_args()
+    if args.decode:
+        return decode_main(args)
 
     rank, world, local = parallel.init_from_env()
     device = torch.device("cuda", local)
