@@ -323,6 +323,14 @@ int mms2ut_decode_embed(const int64_t* tok, const mms2ut_half* E, const mms2ut_h
 int mms2ut_splitk_epilogue_f16(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
                                const mms2ut_half* bias, const mms2ut_half* aux, int64_t ldaux, int relu,
                                mms2ut_half* out, int64_t ldo, hipStream_t stream);
+/* The same reduction with the residual (aux required) followed by the next LayerNorm:
+ * xout = fp16(fp16(sum of slabs + bias) + aux), y = LN(xout; gamma, beta, eps) — one launch,
+ * bit-identical to mms2ut_splitk_epilogue_f16 + mms2ut_layernorm_fwd.  cols <= 1024.          */
+int mms2ut_splitk_epilogue_ln_f16(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                                  const mms2ut_half* bias, const mms2ut_half* aux, int64_t ldaux,
+                                  mms2ut_half* xout, int64_t ldx, const mms2ut_half* gamma,
+                                  const mms2ut_half* beta, float eps, mms2ut_half* y, int64_t ldy,
+                                  hipStream_t stream);
 /* reorder_incremental_state: src [L][Nsrc][maxT][width], dst [L][N][maxT][width] (each decoder
  * layer's self-attention K|V rows); dst[l][n][0:rows] = src[l][idx[n]][0:rows], idx[n] < Nsrc.
  * width % 8 == 0, 16-B aligned.                                                              */

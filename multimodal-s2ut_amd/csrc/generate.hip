@@ -213,6 +213,68 @@ __global__ void __launch_bounds__(256) decode_embed_kernel(const int64_t* __rest
   }
 }
 
+// The decoder step's residual projections (out_proj, encoder_attn.out_proj, fc2) are followed by a
+// LayerNorm of their output: x = fp16(fp16(sum of slabs + bias) + residual), y = LN(x) — in one
+// launch (one wave per hypothesis row, the row in registers).  Same arithmetic, summation order and
+// roundings as splitk_epilogue_kernel followed by ln_fwd_kernel, so the fused step is bit-identical.
+template <int CPL>
+__global__ void __launch_bounds__(256) splitk_epilogue_ln_kernel(const float* __restrict__ slabs, int nsplit,
+                                                                 long slab, int M, int N,
+                                                                 const h16* __restrict__ bias,
+                                                                 const h16* __restrict__ aux, long ldaux,
+                                                                 h16* __restrict__ xout, long ldx,
+                                                                 const h16* __restrict__ g, const h16* __restrict__ b,
+                                                                 float eps, h16* __restrict__ y, long ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = N >> 2;
+  float v[CPL][4];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[c][e] = 0.f;
+    if (ch < nch) {
+      const long off = (long)row * N + ch * 4;
+      f32x4 a = *reinterpret_cast<const f32x4*>(slabs + off);
+      for (int k = 1; k < nsplit; ++k) a += *reinterpret_cast<const f32x4*>(slabs + k * slab + off);
+      const h16x4 r = *reinterpret_cast<const h16x4*>(aux + (long)row * ldaux + ch * 4);
+      h16x4 xo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = a[e];
+        if (bias) t += (float)bias[ch * 4 + e];
+        xo[e] = (h16)((float)(h16)t + (float)r[e]);
+        v[c][e] = (float)xo[e];
+        sum += v[c][e];
+      }
+      *reinterpret_cast<h16x4*>(xout + (long)row * ldx + ch * 4) = xo;
+    }
+  }
+  const float mean = wave_sum(sum) / N;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+    if (lane + c * 64 < nch) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[c][e] - mean; ss += d * d; }
+    }
+  const float rstd = rsqrtf(wave_sum(ss) / N + eps);
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nch) {
+      const h16x4 gg = *reinterpret_cast<const h16x4*>(g + ch * 4), bb = *reinterpret_cast<const h16x4*>(b + ch * 4);
+      h16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (h16)((v[c][e] - mean) * rstd * (float)gg[e] + (float)bb[e]);
+      *reinterpret_cast<h16x4*>(y + (long)row * ldy + ch * 4) = o;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int mms2ut_log_softmax_step(const h16* logits, int64_t ld, int64_t rows, int V, int pad_idx,
@@ -279,4 +341,24 @@ extern "C" int mms2ut_splitk_epilogue_f16(const float* slabs, int nsplit, int64_
   hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(nb), dim3(256), 0, s, slabs, nsplit, (long)slab, rows, cols,
                      bias, aux, (long)ldaux, relu, out, (long)ldo);
   return mms::check_launch("splitk_epilogue");
+}
+
+extern "C" int mms2ut_splitk_epilogue_ln_f16(const float* slabs, int nsplit, int64_t slab, int rows, int cols,
+                                             const h16* bias, const h16* aux, int64_t ldaux, h16* xout, int64_t ldx,
+                                             const h16* gamma, const h16* beta, float eps, h16* y, int64_t ldy,
+                                             hipStream_t s) {
+  MMS_REQUIRE(cols % 4 == 0 && cols <= 1024 && ldaux % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && slab % 4 == 0,
+              "splitk_epilogue_ln: cols <= 1024 and strides must be multiples of 4");
+  MMS_REQUIRE(aux != nullptr && gamma != nullptr && beta != nullptr, "splitk_epilogue_ln: aux, gamma, beta required");
+  if (rows == 0) return 0;
+  const int cpl = (cols / 4 + 63) / 64;
+  const dim3 grid((rows + 3) / 4);
+  switch (cpl) {
+#define CASE(C) case C: hipLaunchKernelGGL(splitk_epilogue_ln_kernel<C>, grid, dim3(256), 0, s, slabs, nsplit, \
+                                           (long)slab, rows, cols, bias, aux, (long)ldaux, xout, (long)ldx, gamma, \
+                                           beta, eps, y, (long)ldy); break;
+    CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+  }
+  return mms::check_launch("splitk_epilogue_ln");
 }

@@ -47,6 +47,19 @@ def _lin(x, W, b, *, aux=None, relu=False, out=None):
     return K.linear(x, W, b, out=out, epi=K.EPI_RELU_DROP if relu else K.EPI_F16, p=0.0)
 
 
+def _lin_ln(x, W, b, aux, g, beta):
+    """(x_out, LN(x_out)) for a residual projection followed by a LayerNorm: one split-K reduction
+    launch that also normalises when split-K applies (bit-identical to _lin + layernorm)."""
+    M, Kd = x.shape
+    N = W.shape[0]
+    tiles = -(-M // 128) * -(-N // 128)
+    s = min(8, max(1, 256 // tiles), Kd // 256)
+    if s > 1 and N <= 1024:
+        return K.linear_splitk_ln(x, W, b, aux, g, beta, splitk=s)
+    xo = _lin(x, W, b, aux=aux)
+    return xo, K.layernorm(xo, g, beta)[0]
+
+
 class IncrementalDecoder:
     def __init__(self, model, enc, enc_len32, Te, bsz, beam, max_len, graphs=None):
         """enc [bsz*Te, d] fp16 (rows b*Te + t, the encoder's output incl. fusion), enc_len32 [bsz]."""
@@ -118,27 +131,30 @@ class IncrementalDecoder:
         m, d, H, hd, N = self.m, self.d, self.H, self.hd, self.N
         x = K.decode_embed(self.tok, m.P("decoder.embed_tokens.weight"), self.pos, self.step_dev, self.pad, N, d,
                            self.scale)
+        h1, _, _ = K.layernorm(x, m.P("decoder.layers.0.self_attn_layer_norm.weight"),
+                               m.P("decoder.layers.0.self_attn_layer_norm.bias"))
         for l in range(self.L):
             p = f"decoder.layers.{l}"
-            h1, _, _ = K.layernorm(x, m.P(p + ".self_attn_layer_norm.weight"), m.P(p + ".self_attn_layer_norm.bias"))
             q = _lin(h1, m.P(p + ".self_attn.q_proj.weight"), m.P(p + ".self_attn.q_proj.bias"))
             Wkv = m.params.span(p + ".self_attn.k_proj.weight", p + ".self_attn.v_proj.weight").view(2 * d, d)
             bkv = m.params.span(p + ".self_attn.k_proj.bias", p + ".self_attn.v_proj.bias")
             kvn = _lin(h1, Wkv, bkv)                 # this step's K|V rows, stored into the cache by the attention
             O = K.decode_self_attn(q, self.cache[l], self.slot, N, H, hd, self.step_dev, kvn, hd ** -0.5)
-            x2 = _lin(O, m.P(p + ".self_attn.out_proj.weight"), m.P(p + ".self_attn.out_proj.bias"), aux=x)
-            h2, _, _ = K.layernorm(x2, m.P(p + ".encoder_attn_layer_norm.weight"), m.P(p + ".encoder_attn_layer_norm.bias"))
+            x2, h2 = _lin_ln(O, m.P(p + ".self_attn.out_proj.weight"), m.P(p + ".self_attn.out_proj.bias"), x,
+                             m.P(p + ".encoder_attn_layer_norm.weight"), m.P(p + ".encoder_attn_layer_norm.bias"))
             q2 = _lin(h2, m.P(p + ".encoder_attn.q_proj.weight"), m.P(p + ".encoder_attn.q_proj.bias"))
             kv = self.kv_all[:, 2 * d * l:2 * d * (l + 1)]
             ldkv = self.kv_all.stride(0)
             O2 = torch.empty(N, d, dtype=F16, device=self.dev)
             K.mha_fwd(q2, kv, kv[:, d:], O2, d, ldkv, ldkv, d, self.bsz, H, self.beam, self.Te, hd, hd ** -0.5,
                       key_len=self.enc_len32)
-            x3 = _lin(O2, m.P(p + ".encoder_attn.out_proj.weight"), m.P(p + ".encoder_attn.out_proj.bias"), aux=x2)
-            h3, _, _ = K.layernorm(x3, m.P(p + ".final_layer_norm.weight"), m.P(p + ".final_layer_norm.bias"))
+            x3, h3 = _lin_ln(O2, m.P(p + ".encoder_attn.out_proj.weight"), m.P(p + ".encoder_attn.out_proj.bias"),
+                             x2, m.P(p + ".final_layer_norm.weight"), m.P(p + ".final_layer_norm.bias"))
             f1 = _lin(h3, m.P(p + ".fc1.weight"), m.P(p + ".fc1.bias"), relu=True)
-            x = _lin(f1, m.P(p + ".fc2.weight"), m.P(p + ".fc2.bias"), aux=x3)
-        xl, _, _ = K.layernorm(x, m.P("decoder.layer_norm.weight"), m.P("decoder.layer_norm.bias"))
+            nxt = f"decoder.layers.{l + 1}.self_attn_layer_norm" if l + 1 < self.L else "decoder.layer_norm"
+            x, h1 = _lin_ln(f1, m.P(p + ".fc2.weight"), m.P(p + ".fc2.bias"), x3, m.P(nxt + ".weight"),
+                            m.P(nxt + ".bias"))
+        xl = h1                                      # the decoder's final LayerNorm
         K.gemm(xl, m.P("decoder.embed_tokens.weight"), self.logits, N, self.V, d, lda=d, ldb=d, ldc=self.Vp)
 
     def step(self, tokens_last, step, mode=MODE_NONE):

@@ -717,6 +717,21 @@ def linear_splitk(x, W, bias=None, *, aux=None, relu=False, splitk=4, out=None):
     return out
 
 
+def linear_splitk_ln(x, W, bias, aux, g, b, eps=1e-5, *, splitk=4):
+    """(xo, y): xo = x @ W^T + bias + aux (split-K slabs), y = LayerNorm(xo) — one reduction launch."""
+    M, Kd = x.shape
+    N = W.shape[0]
+    xo = torch.empty(M, N, dtype=F16, device=x.device)
+    y = torch.empty(M, N, dtype=F16, device=x.device)
+    slabs = torch.empty(splitk, M, N, dtype=torch.float32, device=x.device)
+    gemm(x, W, slabs, M, N, Kd, lda=x.stride(0), ldb=W.stride(0), ldc=N, epi=EPI_F32, splitk=splitk,
+         sCsplit=M * N)
+    call("mms2ut_splitk_epilogue_ln_f16", slabs.data_ptr(), splitk, M * N, M, N, _p(bias), aux.data_ptr(),
+         aux.stride(0), xo.data_ptr(), xo.stride(0), g.data_ptr(), b.data_ptr(), float(eps), y.data_ptr(),
+         y.stride(0), _s())
+    return xo, y
+
+
 def round_up(x, m):
     return (x + m - 1) // m * m
 

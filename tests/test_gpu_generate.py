@@ -211,3 +211,20 @@ def test_linear_splitk_epilogue(M, N, Kd, s, relu, res):
     if res:
         ref = ref.half().float() + aux.float()
     assert (out - ref).abs().max() < 1e-2 + 2e-3 * ref.abs().max()
+
+
+@pytest.mark.parametrize("M,N,Kd,s", [(160, 768, 3072, 8), (37, 768, 768, 3), (200, 256, 1024, 4)])
+def test_splitk_epilogue_ln_bit_identical(M, N, Kd, s):
+    """Fused split-K reduction + residual + LayerNorm == the two-launch sequence, bit for bit."""
+    K = pkg("kernels")
+    g = torch.Generator().manual_seed(N + M)
+    x = (torch.randn(M, Kd, generator=g) * 0.5).half().cuda()
+    W = (torch.randn(N, Kd, generator=g) * Kd ** -0.5).half().cuda()
+    b = torch.randn(N, generator=g).half().cuda()
+    res = torch.randn(M, N, generator=g).half().cuda()
+    gam = (1 + 0.1 * torch.randn(N, generator=g)).half().cuda()
+    bet = (0.1 * torch.randn(N, generator=g)).half().cuda()
+    xo, y = K.linear_splitk_ln(x, W, b, res, gam, bet, splitk=s)
+    xr = K.linear_splitk(x, W, b, aux=res, splitk=s)
+    yr = K.layernorm(xr, gam, bet)[0]
+    assert torch.equal(xo, xr) and torch.equal(y, yr)
