@@ -331,6 +331,13 @@ int mms2ut_splitk_epilogue_ln_f16(const float* slabs, int nsplit, int64_t slab, 
                                   mms2ut_half* xout, int64_t ldx, const mms2ut_half* gamma,
                                   const mms2ut_half* beta, float eps, mms2ut_half* y, int64_t ldy,
                                   hipStream_t stream);
+/* BeamSearch.step candidate selection: per sentence b, the top k (<= 32) of
+ * lprobs[b*beam + j][v] + prev_scores[(b*beam + j) * ld_prev] over j < beam (j = 0 only when
+ * first_step, prev_scores unused), v < V; descending, ties to the lower flat index j*V + v.
+ * Outputs [bsz][k]: score (fp32), token v, beam j (int64).                                   */
+int mms2ut_beam_topk(const float* lprobs, const float* prev_scores, int64_t ld_prev, int bsz, int beam, int V,
+                     int first_step, int k, float* out_score, int64_t* out_tok, int64_t* out_beam,
+                     hipStream_t stream);
 /* reorder_incremental_state: src [L][Nsrc][maxT][width], dst [L][N][maxT][width] (each decoder
  * layer's self-attention K|V rows); dst[l][n][0:rows] = src[l][idx[n]][0:rows], idx[n] < Nsrc.
  * width % 8 == 0, 16-B aligned.                                                              */

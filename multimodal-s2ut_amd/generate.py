@@ -157,6 +157,9 @@ class IncrementalDecoder:
         xl = h1                                      # the decoder's final LayerNorm
         K.gemm(xl, m.P("decoder.embed_tokens.weight"), self.logits, N, self.V, d, lda=d, ldb=d, ldc=self.Vp)
 
+    def beam_topk(self, lprobs, prev_col, bsz, beam, V, k, first_step):
+        return K.beam_topk(lprobs, prev_col, bsz, beam, V, k, first_step)
+
     def step(self, tokens_last, step, mode=MODE_NONE):
         """tokens_last [N] int64 (the token at position `step` of every hypothesis) -> lprobs [N, V]."""
         assert self.step_no == step and self.slot.shape[0] == self.N and step + 1 < self.maxT
@@ -214,15 +217,19 @@ class SequenceGenerator:
             mode = MODE_FORCE_EOS if step >= max_len else (MODE_NO_EOS if step < self.min_len else MODE_NONE)
             lprobs = decoder.step(tokens[:, step], step, mode)
             # BeamSearch.step
-            lp = lprobs.view(bsz, beam, V)
-            if step == 0:
-                lp = lp[:, ::beam, :].contiguous()
+            k = min(cand_size, (1 if step == 0 else beam) * V - 1)
+            if hasattr(decoder, "beam_topk"):     # HIP selection kernel (ties to the lower flat index)
+                cand_scores, cand_indices, cand_beams = decoder.beam_topk(
+                    lprobs, None if step == 0 else scores[:, step - 1], bsz, beam, V, k, step == 0)
             else:
-                lp = lp + scores.view(bsz, beam, -1)[:, :, step - 1].unsqueeze(-1)
-            flat = lp.view(bsz, -1)
-            cand_scores, idx = torch.topk(flat, k=min(cand_size, flat.size(1) - 1))
-            cand_beams = torch.div(idx, V, rounding_mode="trunc")
-            cand_indices = idx.fmod(V)
+                lp = lprobs.view(bsz, beam, V)
+                if step == 0:
+                    lp = lp[:, ::beam, :].contiguous()
+                else:
+                    lp = lp + scores.view(bsz, beam, -1)[:, :, step - 1].unsqueeze(-1)
+                cand_scores, idx = torch.topk(lp.view(bsz, -1), k=k)
+                cand_beams = torch.div(idx, V, rounding_mode="trunc")
+                cand_indices = idx.fmod(V)
             cand_bbsz_idx = cand_beams.add(bbsz_offsets)
             eos_mask = cand_indices.eq(eos) & cand_scores.ne(-math.inf)
             eos_mask[:, :beam][cands_to_ignore] = False

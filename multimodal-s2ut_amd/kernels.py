@@ -732,6 +732,19 @@ def linear_splitk_ln(x, W, bias, aux, g, b, eps=1e-5, *, splitk=4):
     return xo, y
 
 
+def beam_topk(lprobs, prev_col, bsz, beam, V, k, first_step):
+    """(scores [bsz,k] f32, tokens [bsz,k] i64, beams [bsz,k] i64): top-k of lprobs + prev_col per
+    sentence (prev_col: a strided fp32 column view [bsz*beam] of the cumulative scores)."""
+    dev = lprobs.device
+    sc = torch.empty(bsz, k, dtype=torch.float32, device=dev)
+    tok = torch.empty(bsz, k, dtype=torch.int64, device=dev)
+    bm = torch.empty(bsz, k, dtype=torch.int64, device=dev)
+    ld = prev_col.stride(0) if prev_col is not None else 0
+    call("mms2ut_beam_topk", lprobs.data_ptr(), _p(prev_col), ld, bsz, beam, V, int(first_step), k,
+         sc.data_ptr(), tok.data_ptr(), bm.data_ptr(), _s())
+    return sc, tok, bm
+
+
 def round_up(x, m):
     return (x + m - 1) // m * m
 

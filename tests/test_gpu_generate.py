@@ -228,3 +228,26 @@ def test_splitk_epilogue_ln_bit_identical(M, N, Kd, s):
     xr = K.linear_splitk(x, W, b, aux=res, splitk=s)
     yr = K.layernorm(xr, gam, bet)[0]
     assert torch.equal(xo, xr) and torch.equal(y, yr)
+
+
+@pytest.mark.parametrize("bsz,beam,V,k,first", [(16, 10, 1004, 20, False), (3, 10, 1004, 19, True),
+                                                (5, 4, 37, 8, False), (2, 2, 9, 4, True)])
+def test_beam_topk_matches_sorted_selection(bsz, beam, V, k, first):
+    """HIP candidate selection == stable sort of (lprobs + cumulative score) descending, ties to the
+    lower flat index; -inf candidates (pad) included when finite ones run out."""
+    K = pkg("kernels")
+    g = torch.Generator().manual_seed(V + k)
+    lp = torch.log_softmax(torch.randn(bsz * beam, V, generator=g) * 3, -1)
+    lp[:, 1] = -math.inf
+    lp[0, 5:9] = lp[0, 4]                       # exact ties
+    scores = torch.randn(bsz * beam, 7, generator=g)
+    col = scores[:, 3]
+    sc, tok, bm = K.beam_topk(lp.cuda(), None if first else scores.cuda()[:, 3], bsz, beam, V, k, first)
+    jm = 1 if first else beam
+    cand = lp.view(bsz, beam, V)[:, :jm] + (0 if first else col.view(bsz, beam, 1)[:, :jm])
+    flat = cand.reshape(bsz, -1)
+    for b in range(bsz):
+        order = sorted(range(flat.shape[1]), key=lambda i: (-float(flat[b, i]), i))[:k]
+        assert bm[b].cpu().tolist() == [i // V for i in order]
+        assert tok[b].cpu().tolist() == [i % V for i in order]
+        assert torch.equal(sc[b].cpu(), flat[b, order])
