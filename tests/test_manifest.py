@@ -154,3 +154,45 @@ def test_specaugment_oracle_known_answer():
     assert np.array_equal(y, ref)
     assert np.array_equal(RF.specaugment(x, [0, 0, 1, 0], 1, 1), x)   # zero widths mask nothing
     assert np.array_equal(RF.specaugment(x, [0, 3, 0, 0], 1, 1, mask_value=-1.0), np.full_like(x, -1.0))
+
+
+def test_wav_stereo_downmix_and_format_errors(tmp_path, M):
+    """Multi-channel 16-bit WAV -> channel mean (float32); 8-bit PCM and non-16 kHz rejected loudly."""
+    import wave
+    rng = np.random.default_rng(2)
+    st = rng.integers(-30000, 30000, (500, 2)).astype("<i2")
+    p = os.path.join(tmp_path, "st.wav")
+    with wave.open(p, "wb") as w:
+        w.setnchannels(2)
+        w.setsampwidth(2)
+        w.setframerate(16000)
+        w.writeframes(st.tobytes())
+    x, sr = M.read_wav(p)
+    assert sr == 16000 and np.array_equal(x, st.astype(np.float32).mean(axis=1, dtype=np.float32))
+    p8 = os.path.join(tmp_path, "u8.wav")
+    with wave.open(p8, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(1)
+        w.setframerate(16000)
+        w.writeframes(bytes(range(200)))
+    with pytest.raises(ValueError, match="16-bit"):
+        M.read_wav(p8)
+
+
+def test_non_16k_audio_and_short_utterance_rejected(tmp_path, M):
+    c = write_corpus(str(tmp_path), frames=(40, 50))
+    ds = M.MultiModalS2SManifest(str(tmp_path), "train", M.UnitDictionary.for_codes(1000))
+    wav0 = ds.audio_paths[0]
+    M.write_wav(wav0, c["waves"][0], sample_rate=8000)
+    with pytest.raises(ValueError, match="16 kHz"):
+        ds.item(0)
+    M.write_wav(wav0, np.zeros(300, np.float32))      # < 400 samples: no fbank frame
+    with pytest.raises(ValueError, match="shorter than one"):
+        ds.collate([0, 1])
+
+
+def test_specaugment_short_utterance_draws_no_time_mask():
+    fe = pkg("frontend")
+    sa = fe.SpecAugment(freq_mask_N=1, freq_mask_F=5, time_mask_N=2, time_mask_T=100, time_mask_p=0.2)
+    m = sa.draws([4, 3], 80, np.random.RandomState(0))     # floor(T * 0.2) < 1: no time masks
+    assert (m[:, 2:] == 0).all() and (m[:, 1] < 5).all()
