@@ -334,10 +334,11 @@ int mms2ut_splitk_epilogue_ln_f16(const float* slabs, int nsplit, int64_t slab, 
 /* BeamSearch.step candidate selection: per sentence b, the top k (<= 32) of
  * lprobs[b*beam + j][v] + prev_scores[(b*beam + j) * ld_prev] over j < beam (j = 0 only when
  * first_step, prev_scores unused), v < V; descending, ties to the lower flat index j*V + v.
- * Outputs [bsz][k]: score (fp32), token v, beam j (int64).                                   */
+ * Outputs [bsz][k]: score (fp32), token v, beam j (int64).  work: bsz*32*k uint64 scratch
+ * (two passes: 32 waves per sentence, then a merge).                                          */
 int mms2ut_beam_topk(const float* lprobs, const float* prev_scores, int64_t ld_prev, int bsz, int beam, int V,
                      int first_step, int k, float* out_score, int64_t* out_tok, int64_t* out_beam,
-                     hipStream_t stream);
+                     uint64_t* work, hipStream_t stream);
 /* reorder_incremental_state: src [L][Nsrc][maxT][width], dst [L][N][maxT][width] (each decoder
  * layer's self-attention K|V rows); dst[l][n][0:rows] = src[l][idx[n]][0:rows], idx[n] < Nsrc.
  * width % 8 == 0, 16-B aligned.                                                              */

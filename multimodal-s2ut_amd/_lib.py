@@ -111,7 +111,7 @@ SIGNATURES = {
     "mms2ut_decode_self_attn": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, vp, i64, i64, vp, i64, f32, vp]),
     "mms2ut_decode_embed": (i32, [vp, vp, vp, vp, i32, vp, i32, i32, f32, vp]),
     "mms2ut_splitk_epilogue_f16": (i32, [vp, i32, i64, i32, i32, vp, vp, i64, i32, vp, i64, vp]),
-    "mms2ut_beam_topk": (i32, [vp, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+    "mms2ut_beam_topk": (i32, [vp, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "mms2ut_splitk_epilogue_ln_f16": (i32, [vp, i32, i64, i32, i32, vp, vp, i64, vp, i64, vp, vp, f32, vp, i64,
                                             vp]),
 }

@@ -346,6 +346,87 @@ __global__ void __launch_bounds__(1024) beam_topk_kernel(const float* __restrict
   }
 }
 
+// Two-pass form of the same selection, spreading a sentence over BT_PARTS waves (the one-block
+// kernel keeps a sentence on one CU): pass 1 — each wave takes a contiguous share of the sentence's
+// candidates, keeps a per-lane register top-k and pops its own top k by k wave-max rounds into
+// part[b][p][k] (key 0 = empty); pass 2 — one wave per sentence merges the BT_PARTS*k keys the same
+// way and decodes them.  The keys are unique (flat index in the low word), so the result equals the
+// one-pass selection exactly.
+constexpr int BT_PARTS = 32;
+
+template <int KK>
+MMS_DEV void lane_insert(uint64_t (&top)[KK], uint64_t x) {
+  if (x > top[KK - 1]) {
+#pragma unroll
+    for (int t = 0; t < KK; ++t) {
+      const uint64_t hi = x > top[t] ? x : top[t], lo = x > top[t] ? top[t] : x;
+      top[t] = hi;
+      x = lo;
+    }
+  }
+}
+
+template <int KK>
+MMS_DEV uint64_t wave_pop(uint64_t (&top)[KK]) {
+  const uint64_t m = wave_max_u64(top[0]);
+  if (top[0] == m && m != 0) {
+#pragma unroll
+    for (int t = 0; t < KK - 1; ++t) top[t] = top[t + 1];
+    top[KK - 1] = 0;
+  }
+  return m;
+}
+
+template <int KK>
+__global__ void __launch_bounds__(256) beam_topk_part_kernel(const float* __restrict__ lprobs,
+                                                             const float* __restrict__ prev, long ld_prev, int beam,
+                                                             int V, int jmax, int k, int bsz,
+                                                             uint64_t* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= bsz * BT_PARTS) return;
+  const int b = gw / BT_PARTS, p = gw % BT_PARTS;
+  const int n = jmax * V, chunk = (n + BT_PARTS - 1) / BT_PARTS;
+  const int i0 = p * chunk, i1 = min(n, i0 + chunk);
+  uint64_t top[KK];
+#pragma unroll
+  for (int i = 0; i < KK; ++i) top[i] = 0;
+  for (int i = i0 + lane; i < i1; i += 64) {
+    const int j = i / V, v = i - j * V;
+    float sc = lprobs[((long)b * beam + j) * V + v];
+    if (prev) sc += prev[((long)b * beam + j) * ld_prev];
+    lane_insert<KK>(top, beam_key(sc, (uint32_t)i));
+  }
+  for (int r = 0; r < k; ++r) {
+    const uint64_t m = wave_pop<KK>(top);
+    if (lane == 0) part[((long)b * BT_PARTS + p) * k + r] = m;
+  }
+}
+
+template <int KK>
+__global__ void __launch_bounds__(64) beam_topk_merge_kernel(const uint64_t* __restrict__ part, int k, int V,
+                                                             float* __restrict__ out_score,
+                                                             int64_t* __restrict__ out_tok,
+                                                             int64_t* __restrict__ out_beam) {
+  const int lane = threadIdx.x, b = blockIdx.x;
+  uint64_t top[KK];
+#pragma unroll
+  for (int i = 0; i < KK; ++i) top[i] = 0;
+  const uint64_t* pb = part + (long)b * BT_PARTS * k;
+  for (int i = lane; i < BT_PARTS * k; i += 64) lane_insert<KK>(top, pb[i]);
+  for (int r = 0; r < k; ++r) {
+    const uint64_t best = wave_pop<KK>(top);
+    if (lane == 0) {
+      const uint32_t idx = 0xFFFFFFFFu - (uint32_t)best;
+      uint32_t u = (uint32_t)(best >> 32);
+      u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+      out_score[(long)b * k + r] = __uint_as_float(u);
+      out_tok[(long)b * k + r] = idx % V;
+      out_beam[(long)b * k + r] = idx / V;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int mms2ut_log_softmax_step(const h16* logits, int64_t ld, int64_t rows, int V, int pad_idx,
@@ -436,16 +517,31 @@ extern "C" int mms2ut_splitk_epilogue_ln_f16(const float* slabs, int nsplit, int
 
 extern "C" int mms2ut_beam_topk(const float* lprobs, const float* prev_scores, int64_t ld_prev, int bsz, int beam,
                                 int V, int first_step, int k, float* out_score, int64_t* out_tok,
-                                int64_t* out_beam, hipStream_t s) {
+                                int64_t* out_beam, uint64_t* work, hipStream_t s) {
   const int jmax = first_step ? 1 : beam;
   MMS_REQUIRE(k >= 1 && k <= 32 && k < jmax * V, "beam_topk: need 1 <= k <= 32 and k < candidates");
   MMS_REQUIRE((long)beam * V < 0x7FFFFFFFL, "beam_topk: beam * V too large");
   if (bsz == 0) return 0;
   const float* prev = first_step ? nullptr : prev_scores;
   const int kk = k <= 8 ? 8 : k <= 16 ? 16 : k <= 24 ? 24 : 32;
-  switch (kk) {
+  const char* e = getenv("MMS2UT_BEAM_TOPK_1PASS");
+  if (e && e[0] == '1') {
+    switch (kk) {
 #define CASE(KK) case KK: hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(bsz), dim3(1024), 0, s, lprobs, prev, \
                                              (long)ld_prev, beam, V, jmax, k, out_score, out_tok, out_beam); break;
+      CASE(8) CASE(16) CASE(24) CASE(32)
+#undef CASE
+    }
+    return mms::check_launch("beam_topk");
+  }
+  MMS_REQUIRE(work != nullptr, "beam_topk: work buffer (bsz * 32 * k uint64) required");
+  const dim3 g1((bsz * BT_PARTS + 3) / 4);
+  switch (kk) {
+#define CASE(KK) case KK: \
+    hipLaunchKernelGGL(beam_topk_part_kernel<KK>, g1, dim3(256), 0, s, lprobs, prev, (long)ld_prev, beam, V, jmax, \
+                       k, bsz, work); \
+    hipLaunchKernelGGL(beam_topk_merge_kernel<KK>, dim3(bsz), dim3(64), 0, s, work, k, V, out_score, out_tok, \
+                       out_beam); break;
     CASE(8) CASE(16) CASE(24) CASE(32)
 #undef CASE
   }

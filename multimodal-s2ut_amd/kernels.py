@@ -740,8 +740,9 @@ def beam_topk(lprobs, prev_col, bsz, beam, V, k, first_step):
     tok = torch.empty(bsz, k, dtype=torch.int64, device=dev)
     bm = torch.empty(bsz, k, dtype=torch.int64, device=dev)
     ld = prev_col.stride(0) if prev_col is not None else 0
+    work = torch.empty(bsz * 32 * k, dtype=torch.int64, device=dev)
     call("mms2ut_beam_topk", lprobs.data_ptr(), _p(prev_col), ld, bsz, beam, V, int(first_step), k,
-         sc.data_ptr(), tok.data_ptr(), bm.data_ptr(), _s())
+         sc.data_ptr(), tok.data_ptr(), bm.data_ptr(), work.data_ptr(), _s())
     return sc, tok, bm
 
 

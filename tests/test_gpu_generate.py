@@ -232,9 +232,12 @@ def test_splitk_epilogue_ln_bit_identical(M, N, Kd, s):
 
 @pytest.mark.parametrize("bsz,beam,V,k,first", [(16, 10, 1004, 20, False), (3, 10, 1004, 19, True),
                                                 (5, 4, 37, 8, False), (2, 2, 9, 4, True)])
-def test_beam_topk_matches_sorted_selection(bsz, beam, V, k, first):
-    """HIP candidate selection == stable sort of (lprobs + cumulative score) descending, ties to the
-    lower flat index; -inf candidates (pad) included when finite ones run out."""
+@pytest.mark.parametrize("one_pass", ["0", "1"])
+def test_beam_topk_matches_sorted_selection(bsz, beam, V, k, first, one_pass, monkeypatch):
+    """HIP candidate selection (two-pass default, one-block variant) == stable sort of
+    (lprobs + cumulative score) descending, ties to the lower flat index; -inf candidates (pad)
+    included when finite ones run out."""
+    monkeypatch.setenv("MMS2UT_BEAM_TOPK_1PASS", one_pass)
     K = pkg("kernels")
     g = torch.Generator().manual_seed(V + k)
     lp = torch.log_softmax(torch.randn(bsz * beam, V, generator=g) * 3, -1)
