@@ -5,11 +5,14 @@ Two parts:
 
 * ``IncrementalDecoder`` — fairseq ``TransformerDecoder`` with ``incremental_state``: one new
   token per hypothesis per step.  Every layer's self-attention K|V rows live in a cache
-  [L_d, slots, maxT, 2d] that the layer's K|V projection GEMM writes into directly (row stride
-  maxT·2d; hypothesis n writes row `step` of slot n).  Rows never move: a slot table
-  [N, maxT] int32 says which slot holds row t of hypothesis n, so ``reorder_incremental_state``
-  permutes N·step indices instead of copying every layer's K/V (fairseq's index_select of the
-  cache), and ``decode_self_attn`` reads K/V through the table (one wave per hypothesis·head).  Cross-attention K/V of all layers are one GEMM over the encoder output at the start
+  [L_d, slots, maxT, 2d]: the layer's one Q|K|V projection yields this step's K|V rows, and
+  ``decode_self_attn`` stores them as row `step` of slot n while it attends.  Rows never move:
+  a slot table [N, maxT] int32 says which slot holds row t of hypothesis n, so
+  ``reorder_incremental_state`` permutes N·step indices instead of copying every layer's K/V
+  (fairseq's index_select of the cache), and the attention reads K/V through the table (one
+  256-thread block per hypothesis·head).  The step reads its position from a device counter, so
+  it replays as one HIP graph.  Cross-attention K/V of all layers are one GEMM over the encoder
+  output at the start
   (the training path's batched slab); they stay per *sentence*: the beam hypotheses of sentence s
   are the query rows [s·beam, (s+1)·beam) of one attention problem (B = sentences, Tq = beam), so
   nothing is expanded by the beam (``reorder_encoder_out`` is the identity within a sentence and
@@ -135,11 +138,13 @@ class IncrementalDecoder:
                                m.P("decoder.layers.0.self_attn_layer_norm.bias"))
         for l in range(self.L):
             p = f"decoder.layers.{l}"
-            q = _lin(h1, m.P(p + ".self_attn.q_proj.weight"), m.P(p + ".self_attn.q_proj.bias"))
-            Wkv = m.params.span(p + ".self_attn.k_proj.weight", p + ".self_attn.v_proj.weight").view(2 * d, d)
-            bkv = m.params.span(p + ".self_attn.k_proj.bias", p + ".self_attn.v_proj.bias")
-            kvn = _lin(h1, Wkv, bkv)                 # this step's K|V rows, stored into the cache by the attention
-            O = K.decode_self_attn(q, self.cache[l], self.slot, N, H, hd, self.step_dev, kvn, hd ** -0.5)
+            # one Q|K|V projection (the weights are adjacent in the flat buffer); K|V are this step's
+            # cache rows, which the attention kernel stores
+            Wqkv = m.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
+            bqkv = m.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias")
+            qkv = _lin(h1, Wqkv, bqkv)
+            O = K.decode_self_attn(qkv[:, :d], self.cache[l], self.slot, N, H, hd, self.step_dev, qkv[:, d:],
+                                   hd ** -0.5)
             x2, h2 = _lin_ln(O, m.P(p + ".self_attn.out_proj.weight"), m.P(p + ".self_attn.out_proj.bias"), x,
                              m.P(p + ".encoder_attn_layer_norm.weight"), m.P(p + ".encoder_attn_layer_norm.bias"))
             q2 = _lin(h2, m.P(p + ".encoder_attn.q_proj.weight"), m.P(p + ".encoder_attn.q_proj.bias"))
