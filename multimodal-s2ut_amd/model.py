@@ -31,6 +31,11 @@ from .kernels import F16, round_up
 # ============================================================================ config
 
 
+# encoder backward: enqueue each dgrad (main stream, critical path) before the weight gradient
+# (side stream) that reads the same dy; MMS2UT_DGRAD_FIRST=0 restores wgrad-first (A/B)
+DGRAD_FIRST = os.environ.get("MMS2UT_DGRAD_FIRST", "1") != "0"
+
+
 def default_cfg(**over):
     """`s2ut_architecture_base` + textless/1_train.sh flags + shipped fusion YAML
     (mm_s2ut/config/multimodal_s2ut_transformer.yaml)."""
@@ -596,29 +601,45 @@ class MMS2UTModel:
         # fc2 / fc1
         if dy2 is None:
             dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
-        K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"),
-                       db=self.G(p + ".fc2.bias"))
+        # DGRAD_FIRST: the critical-path dgrad is enqueued before the side-stream weight gradient
+        # that reads the same dy, so its blocks are dispatched first
+        if not DGRAD_FIRST:
+            K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"), db=self.G(p + ".fc2.bias"))
         df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
-        K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"),
-                       db=self.G(p + ".fc1.bias"))
+        if DGRAD_FIRST:
+            K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"), db=self.G(p + ".fc2.bias"))
+        else:
+            K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"), db=self.G(p + ".fc1.bias"))
         dh2 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
+        if DGRAD_FIRST:
+            K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"), db=self.G(p + ".fc1.bias"))
         del df1
         dx2, dyo = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".final_layer_norm.weight"), c["m2"], c["r2"],
                                    self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
                                    dres=dx3, emit=(pd, c["drop1"]))
         # out proj (dyo = dropout(dx2) with the attention-branch mask, from the LN backward)
-        K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"),
-                       db=self.G(p + ".self_attn.out_proj.bias"))
+        if not DGRAD_FIRST:
+            K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"),
+                           db=self.G(p + ".self_attn.out_proj.bias"))
         dO = K.linear_dgrad(dyo, self.P(p + ".self_attn.out_proj.weight"))
+        if DGRAD_FIRST:
+            K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"),
+                           db=self.G(p + ".self_attn.out_proj.bias"))
         qkv = c["qkv"]
         dqkv = torch.empty_like(qkv)
         attn_backward(c["attn"], dO, d, c["O"], qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
                       B, H, T, T, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
                       p=pa, drop=c["drop_attn"])
         Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
-        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
-                       db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+
+        def qkv_wgrad():
+            K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
+                           db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+        if not DGRAD_FIRST:
+            qkv_wgrad()
         dh1 = K.linear_dgrad(dqkv, Wqkv)
+        if DGRAD_FIRST:
+            qkv_wgrad()
         if emit is None:
             dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
                                  self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
@@ -904,9 +925,15 @@ class MMS2UTModel:
                       Tt, Tt, hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pa,
                       drop=c["drop_sa"])
         Wqkv = self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight").view(3 * d, d)
-        K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
-                       db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+
+        def qkv_wgrad():
+            K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
+                           db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
+        if not DGRAD_FIRST:
+            qkv_wgrad()
         dh1 = K.linear_dgrad(dqkv, Wqkv)
+        if DGRAD_FIRST:
+            qkv_wgrad()
         if emit is None:
             dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
                                  self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
