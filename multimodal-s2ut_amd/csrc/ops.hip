@@ -772,11 +772,14 @@ extern "C" int mms2ut_layernorm_fwd_ex(const h16* x, const h16* gamma, const h16
   });
 }
 
-// row pairs per wave of ln_bwd16 (D % 256 == 0): MMS2UT_LN_NP in {1, 2, 4}, default 2
+// row pairs per wave of ln_bwd16 (D % 256 == 0): MMS2UT_LN_NP in {1, 2, 4}, default 1 — 8 rows per
+// block, twice the blocks of the 16-row layout: 18.95 vs 19.26 ms per training step over three
+// interleaved A/B pairs (scripts/ln_np_ab2.sh; the in-step LN backward shares the CUs with the
+// side-stream weight gradients, where the shorter blocks interleave better)
 static int ln16_np() {
   const char* e = getenv("MMS2UT_LN_NP");
-  const int v = e ? atoi(e) : 2;
-  return (v == 1 || v == 4) ? v : 2;
+  const int v = e ? atoi(e) : 1;
+  return (v == 2 || v == 4) ? v : 1;
 }
 
 static bool ln16_path(int D) {
