@@ -106,6 +106,26 @@ def gemm_pmc_traffic():
     return d.get("gemm_hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo) for the cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cycle_batches(steps, nbatches):
+    """Resident batch count for a K-step timed window: the largest divisor of K that is <= the
+    requested count, so the window is whole cycles of the resident set and the batch mix (hence
+    frames/s) does not depend on --steps beyond that choice."""
+    return max(d for d in range(1, max(1, min(steps, nbatches)) + 1) if steps % d == 0)
+
+
 def cpu_baseline(cfg, model, sample, budget_s=20.0):
     """The oracle (fp32 PyTorch-CPU restatement) timed on the host cores on a bounded sample of the
     same workload: a few utterances of one batch, full training step (fwd + bwd + Adam)."""
@@ -144,7 +164,7 @@ def cpu_baseline(cfg, model, sample, budget_s=20.0):
             break
     dt = time.time() - t0
     return {"value": frames * k / dt, "unit": "audio-frames/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "cpu": cpu_model(), "kind": "port",
             "sample": f"oracle fp32 training step (fwd+bwd+FP16Optimizer/Adam), {n} utterances / "
                       f"{frames} frames of the base config, {k} steps in {dt:.1f}s"}
 
@@ -247,7 +267,8 @@ def main():
     model = mm.MMS2UTModel(cfg, device=device).init_params(seed=1)
     tr = trainer_mod.Trainer(model, lr=5e-4, world_size=world, bucket_mb=args.bucket_mb)
     fe = frontend_mod.FbankFrontend(device)
-    batches = make_batches(cfg, rank, args.nbatches, args.max_tokens, device, fe, img_tokens=img_tokens)
+    nb = cycle_batches(args.steps, args.nbatches)
+    batches = make_batches(cfg, rank, nb, args.max_tokens, device, fe, img_tokens=img_tokens)
 
     def step(i):
         wb, batch = batches[i % len(batches)][:2]
@@ -268,12 +289,17 @@ def main():
         step(i)
     base = args.warmup   # the timed batch sequence does not depend on how many settling steps ran
     def timed(profile):
-        """K steps between barrier + synchronize on both sides -> (seconds, host issue seconds, GEMM stats)."""
+        """K steps between barrier + synchronize on both sides -> (seconds, host issue seconds, GEMM stats).
+        profile=True: the roofline pass — every GEMM launch bracketed by HIP events on its own
+        stream, with the weight-gradient side stream folded into the main stream so no two GEMMs
+        overlap and each event pair times exactly one kernel."""
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        side_was = kernels._Side.enabled
         if profile:
-            kernels.gemm_profile_begin(1000 * args.steps)
+            kernels._Side.enabled = False
+            kernels.gemm_profile_begin(2000 * args.steps)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -285,16 +311,33 @@ def main():
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
-        g = kernels.gemm_profile_end() if profile else (0.0, 0, 0.0, 0.0)
-        return t1 - t0, t_issue - t0, g
+        g = (0.0, 0, 0.0, 0.0)
+        launches = None
+        if profile:
+            g = kernels.gemm_profile_end()
+            launches = kernels.gemm_profile_launches(g[1])
+            kernels._Side.enabled = side_was
+        return t1 - t0, t_issue - t0, g, launches
 
     # the throughput region runs uninstrumented (per-launch HIP events cost ~5 % of the step);
-    # the same K steps are then re-run with the library's per-GEMM events for roofline.achieved
-    t_run, t_issue_run, _ = timed(False)
+    # the same K steps are then re-run serially with the library's per-GEMM events for the roofline
+    t_run, t_issue_run, _, _ = timed(False)
     t_prof = None
     gemm_ms, n_launch, launched_flops, gemm_bytes = 0.0, 0, 0.0, 0.0
+    classes = {}
     if not args.no_gemm_timing:
-        t_prof, _, (gemm_ms, n_launch, launched_flops, gemm_bytes) = timed(True)
+        t_prof, _, (gemm_ms, n_launch, launched_flops, gemm_bytes), (l_ms, l_fl, l_cls) = timed(True)
+        for ms_, fl_, c_ in zip(l_ms.tolist(), l_fl.tolist(), l_cls.tolist()):
+            if c_ & 256:
+                name = "batched (fusion attention QK^T / PV)"
+            elif not (c_ & 1) and not (c_ & 2):
+                name = "weight gradient (TN, fp32 split-K slabs)"
+            else:
+                name = "forward / dgrad (NT, fused epilogues)"
+            e = classes.setdefault(name, [0.0, 0.0, 0])
+            e[0] += ms_
+            e[1] += fl_
+            e[2] += 1
     t0, t1, t_issue = 0.0, t_run, t_issue_run
     elapsed = t1 - t0
     frames = sum(int(batches[(base + i) % len(batches)][1].n_src_frames) for i in range(args.steps))
@@ -320,6 +363,14 @@ def main():
         cpu = cpu_baseline(cfg, model, batches[0][2], args.cpu_budget)
     if rank == 0:
         achieved = (flops_all / (gemm_all / 1e3) / 1e12) if gemm_all > 0 else None
+        class_lines = {k: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[2] / args.steps,
+                           "launched_tflops": v[1] / max(v[0], 1e-9) / 1e9,
+                           "frac": v[1] / max(v[0], 1e-9) / 1e9 / MFMA_PEAK_F16}
+                       for k, v in classes.items()}
+        dominant = None
+        if class_lines:
+            dn = max(class_lines, key=lambda k: class_lines[k]["ms_per_step"])
+            dominant = dict(class_lines[dn], name=dn)
         line = {
             "metric": "audio-frames/sec/node, mm_s2ut_transformer fp16, max-tokens 40000, 1/2/4/8 GPUs",
             "value": frames_all / elapsed,
@@ -337,7 +388,7 @@ def main():
                        "parallelism": f"dp{world}", "front_end": "GPU fbank+CMVN in step",
                        "alg_flops_per_frame": total_flops_all / max(frames_all, 1),
                        "model_tflops_per_s": total_flops_all / elapsed / 1e12},
-            "roofline": {"bound": "mfma", "kernel": "mms2ut gemm_kernel (all GEMM launches)",
+            "roofline": {"bound": "mfma", "kernel": "mms2ut GEMM family (gemm_dma / gemm256p, all launches)",
                          "achieved": achieved, "peak": MFMA_PEAK_F16, "unit": "TFLOP/s",
                          "frac": (achieved / MFMA_PEAK_F16) if achieved else None, "traffic": traffic,
                          "traffic_source": traffic_src,
@@ -345,13 +396,16 @@ def main():
                          "gemm_ms_per_step": gemm_all / world / args.steps,
                          "gemm_launches_per_step": nl_all / world / args.steps,
                          "gemm_launched_tflops": launched_flops / max(gemm_ms, 1e-9) / 1e9,
+                         "dominant": dominant,
+                         "classes": class_lines,
                          "host_issue_ms_per_step": 1e3 * (t_issue - t0) / args.steps,
-                         "gemm_timed_pass_ms_per_step": (1e3 * t_prof / args.steps) if t_prof else None,
-                         "note": "achieved = SURVEY §8d algorithmic FLOPs (true lengths, 3x fwd) / summed "
-                                 "HIP-event durations of every GEMM launch (events on each launch's stream) "
-                                 "over a second timed pass of the same K steps; value comes from the "
-                                 "uninstrumented pass (weight-grad GEMMs overlap the dgrad chain on a side "
-                                 "stream, so contention inflates durations: a lower bound on the kernel's rate)"},
+                         "roofline_pass_ms_per_step": (1e3 * t_prof / args.steps) if t_prof else None,
+                         "note": "achieved = SURVEY §8d algorithmic GEMM FLOPs (true lengths, 3x fwd, "
+                                 "multi-head attention products excluded) / summed HIP-event durations of "
+                                 "every GEMM launch, measured on a second pass of the same K steps run "
+                                 "serially (side stream folded into the main one, so each event pair times "
+                                 "one kernel alone); value comes from the uninstrumented overlapped pass. "
+                                 "classes/dominant: launched (padded-shape) FLOPs per class / its kernel time"},
             "cpu_baseline": cpu,
             "optimizer": ost,
         }

@@ -84,6 +84,10 @@ int mms2ut_profile_end(float* total_ms, int* launches, double* flops);
 /* algorithmic HBM bytes of the GEMM launches of the last begin/end window (A and B read once, C
  * written once; fp32 split-K slabs, residual / accumulate / gate operands included)            */
 int mms2ut_profile_bytes(double* bytes);
+/* per-launch record of the last finished window (first n launches): kernel ms, launched FLOPs and
+ * a class word: bit0 A K-contiguous, bit1 B K-contiguous, bits 2-7 epilogue, bit8 batched,
+ * bit9 split-K.  Lets the bench split forward / dgrad (NT) from weight-gradient (TN) launches.   */
+int mms2ut_profile_launches(float* ms, double* flops, int* cls, int n);
 
 /* sum `nsplit` fp32 slabs [rows, cols] (slab stride `slab`) * alpha -> out, row stride ldo.
  * mode bit0: fp16 output (else fp32); bit1: accumulate into out (else overwrite)            */

@@ -1091,6 +1091,10 @@ struct GemmProfile {
   bool on = false;
   int cap = 0, n = 0;
   hipEvent_t* ev = nullptr;
+  // per launch (kept after end() for mms2ut_profile_launches): kernel ms, launched FLOPs, class
+  float* l_ms = nullptr;
+  double* l_flops = nullptr;
+  int* l_cls = nullptr;
   double flops = 0.0;
   double bytes = 0.0;  // algorithmic HBM bytes: A, B (and aux / accumulated C) read once, C written once
 } g_prof;
@@ -1101,6 +1105,11 @@ extern "C" int mms2ut_profile_begin(int max_launches) {
   MMS_REQUIRE(max_launches > 0, "profile_begin: max_launches must be > 0");
   g_prof.ev = (hipEvent_t*)calloc(2 * (size_t)max_launches, sizeof(hipEvent_t));
   MMS_REQUIRE(g_prof.ev != nullptr, "profile_begin: out of host memory");
+  free(g_prof.l_ms); free(g_prof.l_flops); free(g_prof.l_cls);
+  g_prof.l_ms = (float*)calloc((size_t)max_launches, sizeof(float));
+  g_prof.l_flops = (double*)calloc((size_t)max_launches, sizeof(double));
+  g_prof.l_cls = (int*)calloc((size_t)max_launches, sizeof(int));
+  MMS_REQUIRE(g_prof.l_ms && g_prof.l_flops && g_prof.l_cls, "profile_begin: out of host memory");
   for (int i = 0; i < 2 * max_launches; ++i)
     if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) { mms::set_error("profile_begin: hipEventCreate"); return 1; }
   g_prof.cap = max_launches;
@@ -1123,6 +1132,7 @@ extern "C" int mms2ut_profile_end(float* total_ms, int* launches, double* flops)
       return 1;
     }
     tot += ms;
+    g_prof.l_ms[i] = ms;
   }
   for (int i = 0; i < 2 * g_prof.cap; ++i) hipEventDestroy(g_prof.ev[i]);
   free(g_prof.ev);
@@ -1144,6 +1154,9 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (a) {
     const double nb = a->batch > 0 ? a->batch : 1;
     g_prof.flops += 2.0 * a->M * a->N * a->K * nb;
+    g_prof.l_flops[i] = 2.0 * a->M * a->N * a->K * nb;
+    g_prof.l_cls[i] = (a->a_kcontig ? 1 : 0) | (a->b_kcontig ? 2 : 0) | (a->epi << 2) | (nb > 1 ? 256 : 0) |
+                      ((a->splitk > 1 ? 1 : 0) << 9);
     const double c_bytes = (double)a->M * a->N * (a->epi == MMS_EPI_F32 ? 4.0 * (a->splitk > 0 ? a->splitk : 1) : 2.0);
     double extra = 0.0;
     if (a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_RELU_DROP_BWD || a->epi == MMS_EPI_F16_ACC) extra = 2.0 * a->M * a->N;
@@ -1151,6 +1164,17 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
     g_prof.bytes += nb * (2.0 * ((double)a->M * a->K + (double)a->N * a->K) + c_bytes + extra);
   }
   return rc;
+}
+
+extern "C" int mms2ut_profile_launches(float* ms, double* flops, int* cls, int n) {
+  MMS_REQUIRE(!g_prof.on && g_prof.l_ms != nullptr, "profile_launches: no finished profile window");
+  MMS_REQUIRE(n >= 0 && n <= g_prof.n, "profile_launches: n=%d > %d launches", n, g_prof.n);
+  for (int i = 0; i < n; ++i) {
+    if (ms) ms[i] = g_prof.l_ms[i];
+    if (flops) flops[i] = g_prof.l_flops[i];
+    if (cls) cls[i] = g_prof.l_cls[i];
+  }
+  return 0;
 }
 
 extern "C" int mms2ut_profile_bytes(double* bytes) {

@@ -98,6 +98,15 @@ def gemm_profile_end():
     return ms.value, n.value, fl.value, by.value
 
 
+def gemm_profile_launches(n):
+    """Per-launch (ms, launched FLOPs, class word) of the last gemm_profile window (numpy)."""
+    import numpy as np
+    ms, fl, cls = np.zeros(n, np.float32), np.zeros(n, np.float64), np.zeros(n, np.int32)
+    if n:
+        call("mms2ut_profile_launches", ms.ctypes.data, fl.ctypes.data, cls.ctypes.data, int(n))
+    return ms, fl, cls
+
+
 def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
            ldc=None, alpha=1.0):
     """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue)."""

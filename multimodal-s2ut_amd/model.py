@@ -993,12 +993,17 @@ class MMS2UTModel:
     def encoder_backward(self, ctx, denc):
         if ctx["fusion"] is not None:
             denc = self.fusion_bwd(ctx["fusion"], denc)
-            if ctx.get("audio_dropped"):
-                denc = torch.zeros_like(denc)
         last_fusion = [n for n, _ in self.params.specs if n.startswith(("encoder.gate", "encoder.multimodal",
                                                                          "encoder.selective", "encoder.image"))]
         if last_fusion:
             self._ready(last_fusion[-1])
+        if ctx.get("audio_dropped"):
+            # the reference replaces encoder_out by zeros_like(..., requires_grad=False)
+            # (mm_s2s_transformer.py:500): no gradient reaches the encoder, whose gradients stay
+            # at the step's zeros -- skip its whole backward, only flush the reducer
+            ctx["layers"] = None
+            self._ready(None)
+            return
         layers = ctx["layers"]
         L = self.cfg["encoder_layers"]
         emit = lambda l: (layers[l]["pd"], layers[l]["drop2"]) if l >= 0 else None  # noqa: E731

@@ -206,6 +206,37 @@ def test_attn_softmax(K, causal, extra):
     assert rel(dS.view(Bt, H, Tq, ldS)[..., :Tk], sf.grad.nan_to_num(0.0)) < 3e-3
 
 
+@pytest.mark.parametrize("Tk", [101, 578, 1031])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attn_softmax_fusion_widths(K, Tk, masked):
+    """The fusion attention's widths: DETR 100 + bias_kv (101), ViT 577 + bias_kv (578, the
+    3-chunks-per-lane instantiation) and one past it, with image key masks, the extra bias_kv key
+    and attention dropout 0.1 replayed from the HIP RNG."""
+    Z, Tq, p = 5, 37, 0.1
+    ldS = (Tk + 7) // 8 * 8
+    g = torch.Generator(device="cuda").manual_seed(Tk)
+    S = (3 * torch.randn(Z * Tq * ldS, device="cuda", generator=g)).half()
+    km = None
+    if masked:
+        km = torch.zeros(Z, ldS, dtype=torch.uint8, device="cuda")
+        for z in range(Z):
+            km[z, max(1, (Tk - 1) * (z + 1) // (Z + 1)):Tk - 1] = 1   # padded image keys; bias_kv column kept
+    P, Pd = K.attn_softmax(S, Z, 1, Tq, Tk, ldS, key_mask=km, extra_key=True, p=p, drop=(11, 512))
+    s = S.view(Z, Tq, ldS)[..., :Tk].float()
+    if km is not None:
+        s = s.masked_fill(km[:, None, :Tk].bool(), float("-inf"))
+    sf = s.clone().requires_grad_(True)
+    pr = torch.softmax(sf, -1)
+    m = K.dropout_mask(Z * Tq * Tk, p, 11, 512, "cuda").view(Z, Tq, Tk).float()
+    assert rel(P.view(Z, Tq, ldS)[..., :Tk], pr) < 2e-3
+    assert rel(Pd.view(Z, Tq, ldS)[..., :Tk], pr * m / (1 - p)) < 2e-3
+    dPd = torch.randn(Z * Tq * ldS, device="cuda", generator=g).half()
+    (pr * m / (1 - p)).backward(dPd.view(Z, Tq, ldS)[..., :Tk].float())
+    dS = K.attn_softmax_bwd(P, dPd.clone(), Z, 1, Tq, Tk, ldS, p=p, drop=(11, 512))
+    torch.cuda.synchronize()
+    assert rel(dS.view(Z, Tq, ldS)[..., :Tk], sf.grad.nan_to_num(0.0)) < 3e-3
+
+
 def test_attn_softmax_dropout_replay(K):
     Z, Tq, Tk = 4, 16, 30
     ldS = 32

@@ -3,7 +3,11 @@ own fusion golden vectors.  fp16 storage / fp32 accumulation vs fp32 (or fp64) o
   * logits: relative L2 error < 1e-2; unit-token argmax identical wherever the oracle's top-2
     margin exceeds 0.05 (the fp16 noise floor at these magnitudes);
   * loss / nll: relative error < 2e-3;
-  * every parameter gradient: relative L2 error < 5e-2 (fp16 gradients through 4+ layers).
+  * every parameter gradient: relative L2 error < 1e-2, with each FFN's ReLU activity pattern
+    replayed from the HIP forward (oracle/ref_model.py _relu; without it, units within fp16
+    rounding of zero switch sides and put ~1-2e-2 on the fc1 / FFN-LN gradients of small models,
+    scripts/grad_error_probe.py), at fairseq's dynamic loss scale.
+The full-size configurations (dropout on, masks replayed) are in test_gpu_model_full.py.
 """
 import numpy as np
 import pytest
@@ -11,8 +15,11 @@ import torch
 
 from conftest import golden_files, pkg
 from oracle import ref_model as R
+from parity_util import check_outputs, grad_errors, report, run_model_pair
 
 pytestmark = pytest.mark.gpu
+
+GRAD_TOL = 1e-2
 
 
 @pytest.fixture(scope="module")
@@ -32,54 +39,14 @@ def _round16(P):
 
 
 def _run_pair(mm, cfg, lengths, tlens, img_mask=False, with_images=True, seed=0):
-    cfg = R.no_dropout(cfg)
-    P = _round16(R.init_params(cfg, seed=seed + 5, include_unused=False))
-    model = mm.MMS2UTModel(mm.default_cfg(**cfg), device="cuda")
-    model.params.load_state_dict(P, strict=True)
-    sample = mm.data.make_sample(lengths, tlens, img_tokens=37, img_dim=cfg["image_feat_dim"],
-                                 with_images=with_images, img_mask=img_mask, seed=seed)
-    ni = sample["net_input"]
-    ni["src_tokens"] = ni["src_tokens"].half().float()
-    if ni["imgs_list"]:
-        ni["imgs_list"][0] = ni["imgs_list"][0].half().float()
-    batch = mm.runtime.prepare_batch(sample, model.cfg)
-    logits = mm.runtime.model_logits(model, batch)
-    V = cfg["vocab_size"]
-    loss, nll = mm.runtime.label_smoothed_ce(logits, batch.target, V, cfg["label_smoothing"], 1)
-    B, Tt = ni["prev_output_tokens"].shape
-    lg = logits[:, :V].float().cpu().view(B, Tt, V)
-    loss.backward()
-    torch.cuda.synchronize()
-    Pg = {k: v.clone().requires_grad_(True) for k, v in P.items()}
-    lo, nllo, lgo = R.model_forward(Pg, sample, cfg)
-    lo.backward()
-    return model, lg, lgo.detach(), loss.item(), lo.item(), nll.item(), nllo.item(), Pg, sample
+    return run_model_pair(mm, R.no_dropout(cfg), lengths, tlens, img_tokens=37, img_mask=img_mask,
+                          with_images=with_images, seed=seed, taps=False)
 
 
-def _check(model, lg, lgo, loss, lo, nll, nllo, Pg, sample, grad_tol=5e-2):
-    assert rel(lg, lgo) < 1e-2
-    keep = sample["target"] != 1
-    top2 = lgo.topk(2, -1).values
-    confident = keep & ((top2[..., 0] - top2[..., 1]) > 0.05)
-    assert torch.equal(lg.argmax(-1)[confident], lgo.argmax(-1)[confident])
-    assert abs(loss - lo) / abs(lo) < 2e-3
-    assert abs(nll - nllo) / abs(nllo) < 2e-3
-    bad = []
-    for k, v in Pg.items():
-        g = model.params.g[k].float().cpu()
-        if v.grad is None or v.grad.norm() == 0:
-            assert g.norm() == 0, k
-            continue
-        if k.endswith("k_proj.bias"):
-            # mathematically zero (softmax is shift-invariant along keys): fp rounding noise only;
-            # bound it by the matching value-bias gradient instead of a relative error
-            vb = Pg[k.replace("k_proj", "v_proj")].grad
-            assert g.norm() <= 1e-2 * vb.norm() + 1e-3, (k, g.norm(), vb.norm())
-            continue
-        e = rel(g, v.grad)
-        if e > grad_tol:
-            bad.append((k, e))
-    assert not bad, bad
+def _check(r, grad_tol=GRAD_TOL):
+    check_outputs(r)
+    bad = {k: e for k, e in grad_errors(r).items() if e > grad_tol}
+    assert not bad, report(r)
 
 
 def _tiny(**over):
@@ -87,42 +54,42 @@ def _tiny(**over):
 
 
 def test_model_parity_multimodal_attention(mm):
-    out = _run_pair(mm, _tiny(image_feat_dim=768), [93, 80, 61], [30, 25, 19])
-    _check(*out)
+    r = _run_pair(mm, _tiny(image_feat_dim=768), [93, 80, 61], [30, 25, 19])
+    _check(r)
 
 
 def test_model_parity_packed_inproj_imgmask(mm):
-    out = _run_pair(mm, _tiny(image_feat_dim=256), [77, 77, 40, 21], [21, 18, 30, 7], img_mask=True, seed=1)
-    _check(*out)
+    r = _run_pair(mm, _tiny(image_feat_dim=256), [77, 77, 40, 21], [21, 18, 30, 7], img_mask=True, seed=1)
+    _check(r)
 
 
 def test_model_parity_selective_attention(mm):
-    out = _run_pair(mm, _tiny(multimodal_attention_type="selective_attention", image_feat_dim=96),
+    r = _run_pair(mm, _tiny(multimodal_attention_type="selective_attention", image_feat_dim=96),
                     [64, 50], [12, 16], img_mask=True, seed=2)
-    _check(*out)
+    _check(r)
 
 
 def test_model_parity_no_gate(mm):
-    out = _run_pair(mm, _tiny(use_selective_gate=False), [70, 33], [9, 14], seed=3)
-    _check(*out)
+    r = _run_pair(mm, _tiny(use_selective_gate=False), [70, 33], [9, 14], seed=3)
+    _check(r)
 
 
 def test_model_parity_audio_only(mm):
-    out = _run_pair(mm, _tiny(fusion=False), [90, 45, 45], [20, 11, 11], with_images=False, seed=4)
-    _check(*out)
+    r = _run_pair(mm, _tiny(fusion=False), [90, 45, 45], [20, 11, 11], with_images=False, seed=4)
+    _check(r)
 
 
 def test_model_parity_no_padding_q1(mm):
     # B=1: fairseq returns encoder_padding_mask=[] -> reference IndexError;
     # defined semantics: all-False mask
-    out = _run_pair(mm, _tiny(), [50], [13], seed=6)
-    _check(*out)
+    r = _run_pair(mm, _tiny(), [50], [13], seed=6)
+    _check(r)
 
 
 def test_model_parity_base_dims(mm):
     cfg = R.base_config(encoder_layers=2, decoder_layers=1)
-    out = _run_pair(mm, cfg, [120, 97], [37, 29], seed=7)
-    _check(*out)
+    r = _run_pair(mm, cfg, [120, 97], [37, 29], seed=7)
+    _check(r)
 
 # ------------------------------------------------------------------ reference golden vectors
 
