@@ -284,7 +284,8 @@ int mms2ut_ls_xent_bwd(const mms2ut_half* logits, int64_t ld, const int64_t* tar
 enum {
   MMS_OST_MULT = 0, MMS_OST_GNORM = 1, MMS_OST_OVERFLOW = 2, MMS_OST_STEP = 3,
   MMS_OST_STEP_SIZE = 4, MMS_OST_LOSS_SCALE = 5, MMS_OST_ITER = 6, MMS_OST_LAST_OVERFLOW = 7,
-  MMS_OST_LAST_RESCALE = 8, MMS_OST_CLIP_COEF = 9, MMS_OST_FATAL = 10, MMS_OST_LR = 11, MMS_OST_SIZE = 16
+  MMS_OST_LAST_RESCALE = 8, MMS_OST_CLIP_COEF = 9, MMS_OST_FATAL = 10, MMS_OST_LR = 11,
+  MMS_OST_INCONSISTENT = 12, MMS_OST_SIZE = 16
 };
 int mms2ut_grad_sqnorm(const mms2ut_half* grad, int64_t n, float* part, int nparts,
                        hipStream_t stream);
@@ -295,6 +296,16 @@ int mms2ut_grad_norm_finalize(const float* part, int nparts, float* ost, const f
 int mms2ut_optim_prepare(float* ost, float lr, float warmup_init_lr, float warmup_updates, float beta1,
                          float beta2, float clip_norm, float scale_window, float min_loss_scale,
                          hipStream_t stream);
+/* fairseq Trainer._check_grad_norms on device.  stage 0: buf[0..world) = 0 except
+ * buf[rank] = ost[MMS_OST_GNORM]; the caller SUM-all-reduces buf; stage 1: ost[MMS_OST_INCONSISTENT]
+ * = 1 when the norms are finite and max|n_r - n_0| / (n_0 + 1e-6) >= 1e-6 — optim_prepare then
+ * sets MMS_OST_FATAL and no rank updates (the host raises FloatingPointError at its next read). */
+int mms2ut_grad_norm_check(float* buf, int world, int rank, float* ost, int stage, hipStream_t stream);
+/* x *= alpha in place (fp16, n % 8 == 0): the data-parallel gradient pre-division by world size
+ * (torch DDP's allreduce hook divides each bucket before its SUM all-reduce)                    */
+int mms2ut_scale_f16(mms2ut_half* x, int64_t n, float alpha, hipStream_t stream);
+/* acc (fp32) += x (fp16), n % 8 == 0: gradient accumulation over --update-freq micro-batches    */
+int mms2ut_accum_f16_f32(float* acc, const mms2ut_half* x, int64_t n, hipStream_t stream);
 int mms2ut_adam_fp16_master(mms2ut_half* param, const mms2ut_half* grad, float* master,
                             float* exp_avg, float* exp_avg_sq, int64_t n, const float* ost,
                             float beta1, float beta2, float eps, float weight_decay, hipStream_t stream);

@@ -30,8 +30,8 @@ def main(argv=None):
     args = build_parser().parse_args(argv)
     if not args.fp16:
         raise SystemExit("mms2ut-train: only --fp16 training is implemented (the reference's setting)")
-    if args.update_freq != 1:
-        raise SystemExit("mms2ut-train: --update-freq 1 only (BASELINE configs)")
+    if args.update_freq < 1:
+        raise SystemExit("mms2ut-train: --update-freq must be >= 1")
     for kind, name in (("task", args.task), ("arch", args.arch), ("criterion", args.criterion)):
         if name not in REGISTRY[kind]:
             raise SystemExit(f"mms2ut-train: unknown {kind} {name!r}; have {sorted(REGISTRY[kind])}")
@@ -46,32 +46,75 @@ def main(argv=None):
     betas = tuple(ast.literal_eval(args.adam_betas))
     tr = Trainer(net, lr=args.lr, betas=betas, clip_norm=args.clip_norm,
                  warmup_updates=args.warmup_updates, warmup_init_lr=args.warmup_init_lr,
-                 init_scale=float(args.fp16_init_scale), world_size=world)
+                 init_scale=float(args.fp16_init_scale), world_size=world, update_freq=args.update_freq)
+    start = _restore(args, tr, dev)
     fus = task.multimodal_translation_config
     if not args.synthetic:
-        return _train_manifest(args, task, cfg, tr, fus, rank, world, dev)
-    ds = SyntheticSpeechMulti30K(n_utts=max(64, 2 * args.max_tokens // 400), seed=args.seed,
+        rc = _train_manifest(args, task, cfg, tr, fus, rank, world, dev, start)
+        _save(args, tr, rank)
+        return rc
+    # enough utterances that every rank gets at least one update of update_freq micro-batches
+    need = max(64, 2 * args.max_tokens // 400) * world * args.update_freq
+    ds = SyntheticSpeechMulti30K(n_utts=need, seed=args.seed,
                                  vocab=cfg["vocab_size"], img_dim=cfg["image_feat_dim"],
                                  with_images=bool(fus is not None and cfg["fusion"]))
     batches = ds.batches(args.max_tokens)
     g = torch.Generator().manual_seed(args.seed)
-    upd, t0, ntok = 0, time.time(), 0.0
+    upd, t0, ntok = start, time.time(), 0.0
     while upd < args.max_update:
         order = torch.randperm(len(batches), generator=g).tolist()
         # equal batch count per rank (fairseq pads the last shard with dummy batches)
         order = order[: len(order) // world * world]
-        for bi in order[rank::world]:
-            sample = ds.sample(batches[bi])
-            batch = runtime.prepare_batch(sample, cfg, dev)
-            log = tr.train_step(batch)
-            ntok += batch.ntokens * world  # rank-local count scaled (no per-step host sync)
+        mine = order[rank::world]
+        mine = mine[: len(mine) // args.update_freq * args.update_freq]
+        if not mine:
+            raise SystemExit(f"mms2ut-train: {len(batches)} synthetic batches cannot feed {world} ranks x "
+                             f"update-freq {args.update_freq}")
+        for j in range(0, len(mine), args.update_freq):
+            micro = [runtime.prepare_batch(ds.sample(batches[bi]), cfg, dev) for bi in mine[j:j + args.update_freq]]
+            log = tr.train_step(micro)
+            ntok += sum(b.ntokens for b in micro) * world  # rank-local count scaled (no per-step host sync)
             upd += 1
             if upd % args.log_interval == 0 or upd == args.max_update:
                 _log(args, upd, log, tr, ntok, t0, rank)
+            if args.save_interval_updates and upd % args.save_interval_updates == 0:
+                _save(args, tr, rank)
             if upd >= args.max_update:
                 break
     torch.cuda.synchronize(dev)
+    _save(args, tr, rank)
     return 0
+
+
+def _save(args, tr, rank):
+    """--save-dir: fairseq-layout checkpoint_last.pt (model keys of MM_S2UTTransformerModel, the
+    fp32 master / Adam state, num_updates), written by rank 0 (fairseq's checkpoint_utils)."""
+    import os
+    if not args.save_dir:
+        return
+    state = tr.state_dict()          # every rank syncs; only rank 0 writes
+    if rank != 0:
+        return
+    os.makedirs(args.save_dir, exist_ok=True)
+    state["args"] = {k: v for k, v in vars(args).items() if isinstance(v, (int, float, str, bool, type(None)))}
+    path = os.path.join(args.save_dir, "checkpoint_last.pt")
+    torch.save(state, path + ".tmp")
+    os.replace(path + ".tmp", path)
+
+
+def _restore(args, tr, dev):
+    """--restore-file (default checkpoint_last.pt in --save-dir, as fairseq): returns num_updates."""
+    import os
+    path = args.restore_file
+    if path and not os.path.isabs(path) and args.save_dir:
+        path = os.path.join(args.save_dir, path)
+    if not path or not os.path.exists(path):
+        if args.restore_file and args.restore_file != "checkpoint_last.pt":
+            raise SystemExit(f"mms2ut-train: --restore-file {args.restore_file} not found")
+        return 0
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    tr.load_state_dict(ckpt)
+    return int(ckpt.get("extra_state", {}).get("num_updates", 0))
 
 
 def _log(args, upd, log, tr, ntok, t0, rank):
@@ -79,6 +122,9 @@ def _log(args, upd, log, tr, ntok, t0, rank):
         return
     lg = log.tolist()
     st = tr.opt.stats()
+    if st["inconsistent"]:
+        raise FloatingPointError("Fatal error: gradients are inconsistent between workers "
+                                 "(fairseq Trainer._check_grad_norms)")
     el = time.time() - t0
     ln2 = math.log(2)
     rec = {"num_updates": upd, "loss": lg[0] / lg[2] / ln2, "nll_loss": lg[1] / lg[2] / ln2,
@@ -87,7 +133,7 @@ def _log(args, upd, log, tr, ntok, t0, rank):
     print(json.dumps(rec), flush=True)
 
 
-def _train_manifest(args, task, cfg, tr, fus, rank, world, dev):
+def _train_manifest(args, task, cfg, tr, fus, rank, world, dev, start=0):
     """On-disk data: ``{data}/{train_subset}.tsv`` + ``{data}/{config_yaml}``,
     image features from the fusion YAML's ``image_feat_path``; per epoch the length-ordered batches
     are shuffled with (seed, epoch) and dealt round-robin to ranks (fairseq ShardedIterator)."""
@@ -104,20 +150,29 @@ def _train_manifest(args, task, cfg, tr, fus, rank, world, dev):
                                  data_cfg=data_cfg, image_feat_path=feat,
                                  max_source_positions=cfg.get("max_source_positions", 6000),
                                  max_target_positions=cfg.get("max_target_positions", 1024))
-    upd, t0, ntok, epoch = 0, time.time(), 0.0, 1
+    upd, t0, ntok, epoch = start, time.time(), 0.0, 1
+    uf = args.update_freq
     while upd < args.max_update:
         batches = ds.batches(args.max_tokens, seed=args.seed, epoch=epoch, skip_invalid=True)
         order = np.random.RandomState((args.seed + epoch) % 2 ** 32).permutation(len(batches)).tolist()
         order = order[: len(order) // world * world]
         mine = [batches[i] for i in order[rank::world]]
+        mine = mine[: len(mine) // uf * uf]
         if not mine:
-            raise SystemExit(f"mms2ut-train: {len(batches)} batches cannot feed {world} ranks")
+            raise SystemExit(f"mms2ut-train: {len(batches)} batches cannot feed {world} ranks x update-freq {uf}")
+        micro = []
         for batch, _ in M.DeviceLoader(ds, mine, cfg, dev, seed=args.seed + rank, epoch=epoch):
-            log = tr.train_step(batch)
-            ntok += batch.ntokens * world
+            micro.append(batch)
+            if len(micro) < uf:
+                continue
+            log = tr.train_step(micro)
+            ntok += sum(b.ntokens for b in micro) * world
+            micro = []
             upd += 1
             if upd % args.log_interval == 0 or upd == args.max_update:
                 _log(args, upd, log, tr, ntok, t0, rank)
+            if args.save_interval_updates and upd % args.save_interval_updates == 0:
+                _save(args, tr, rank)
             if upd >= args.max_update:
                 break
         epoch += 1

@@ -137,6 +137,11 @@ __global__ void grad_norm_finalize_kernel(const float* __restrict__ part, int np
 __global__ void optim_prepare_kernel(float* ost, float lr_peak, float warmup_init_lr, float warmup_updates,
                                      float b1, float b2, float clip, float scale_window, float min_scale) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (ost[MMS_OST_INCONSISTENT] != 0.f) {
+    // fairseq Trainer._check_grad_norms raised: no update, the run is dead (FATAL for the host)
+    ost[MMS_OST_FATAL] = 1.f;
+    return;
+  }
   const bool overflow = ost[MMS_OST_OVERFLOW] != 0.f;
   float it = ost[MMS_OST_ITER];
   if (overflow) {
@@ -178,7 +183,8 @@ __global__ void optim_prepare_kernel(float* ost, float lr_peak, float warmup_ini
 __global__ void adam_kernel(h16* __restrict__ param, const h16* __restrict__ grad, float* __restrict__ master,
                             float* __restrict__ m, float* __restrict__ v, long n, const float* __restrict__ ost,
                             float b1, float b2, float eps, float wd) {
-  if (ost[MMS_OST_OVERFLOW] != 0.f) return;  // overflow: skip (FP16Optimizer OverflowError path)
+  // overflow: skip (FP16Optimizer OverflowError path); inconsistent grads across ranks: no update
+  if (ost[MMS_OST_OVERFLOW] != 0.f || ost[MMS_OST_INCONSISTENT] != 0.f) return;
   const float lr = ost[MMS_OST_LR];
   const float mult = ost[MMS_OST_MULT] * ost[MMS_OST_CLIP_COEF];
   const float step_size = ost[MMS_OST_STEP_SIZE];
@@ -193,6 +199,48 @@ __global__ void adam_kernel(h16* __restrict__ param, const h16* __restrict__ gra
     p -= step_size * mi / (sqrtf(vi) + eps);
     master[i] = p;
     param[i] = (h16)p;
+  }
+}
+
+// fairseq Trainer._check_grad_norms, on device: every rank writes its grad norm into its slot of
+// a zeroed [world] buffer (stage 0), the buffer is SUM-all-reduced, and stage 1 flags the step
+// when the norms are finite and differ: max|n_r - n_0| / (n_0 + 1e-6) >= 1e-6.
+__global__ void grad_norm_check_kernel(float* buf, int world, int rank, float* ost, int stage) {
+  const int i = threadIdx.x;
+  if (stage == 0) {
+    for (int r = i; r < world; r += blockDim.x) buf[r] = (r == rank) ? ost[MMS_OST_GNORM] : 0.f;
+    return;
+  }
+  if (i != 0) return;
+  bool finite = true;
+  float dmax = 0.f;
+  for (int r = 0; r < world; ++r) {
+    finite = finite && isfinite(buf[r]);
+    dmax = fmaxf(dmax, fabsf(buf[r] - buf[0]));
+  }
+  ost[MMS_OST_INCONSISTENT] = (finite && dmax / (buf[0] + 1e-6f) >= 1e-6f) ? 1.f : 0.f;
+}
+
+// x *= alpha (fp16, in place): DDP's pre-division of a gradient bucket by the world size
+__global__ void scale_f16_kernel(h16* __restrict__ x, long n8, float alpha) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    h16x8 v = *reinterpret_cast<const h16x8*>(x + i * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (h16)((float)v[e] * alpha);
+    *reinterpret_cast<h16x8*>(x + i * 8) = v;
+  }
+}
+
+// acc (fp32) += x (fp16): gradient accumulation across --update-freq micro-batches
+__global__ void accum_f16_f32_kernel(float* __restrict__ acc, const h16* __restrict__ x, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const h16x8 v = *reinterpret_cast<const h16x8*>(x + i * 8);
+    f32x4 a = *reinterpret_cast<const f32x4*>(acc + i * 8);
+    f32x4 b = *reinterpret_cast<const f32x4*>(acc + i * 8 + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { a[e] += (float)v[e]; b[e] += (float)v[e + 4]; }
+    *reinterpret_cast<f32x4*>(acc + i * 8) = a;
+    *reinterpret_cast<f32x4*>(acc + i * 8 + 4) = b;
   }
 }
 
@@ -266,4 +314,30 @@ extern "C" int mms2ut_adam_fp16_master(h16* param, const h16* grad, float* maste
   hipLaunchKernelGGL(adam_kernel, dim3((int)g), dim3(256), 0, s, param, grad, master, exp_avg, exp_avg_sq,
                      (long)n, ost, beta1, beta2, eps, weight_decay);
   return mms::check_launch("adam");
+}
+
+extern "C" int mms2ut_grad_norm_check(float* buf, int world, int rank, float* ost, int stage, hipStream_t s) {
+  MMS_REQUIRE(world >= 1 && rank >= 0 && rank < world && (stage == 0 || stage == 1),
+              "grad_norm_check: world=%d rank=%d stage=%d", world, rank, stage);
+  hipLaunchKernelGGL(grad_norm_check_kernel, dim3(1), dim3(64), 0, s, buf, world, rank, ost, stage);
+  return mms::check_launch("grad_norm_check");
+}
+
+extern "C" int mms2ut_scale_f16(h16* x, int64_t n, float alpha, hipStream_t s) {
+  MMS_REQUIRE(n % 8 == 0 && ((uintptr_t)x & 15) == 0, "scale_f16: n %% 8 == 0 and 16-B alignment");
+  if (n == 0) return 0;
+  const long n8 = n / 8;
+  const long nb = std::min<long>((n8 + 255) / 256, 4096);
+  hipLaunchKernelGGL(scale_f16_kernel, dim3(nb), dim3(256), 0, s, x, n8, alpha);
+  return mms::check_launch("scale_f16");
+}
+
+extern "C" int mms2ut_accum_f16_f32(float* acc, const h16* x, int64_t n, hipStream_t s) {
+  MMS_REQUIRE(n % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)acc & 15) == 0,
+              "accum_f16_f32: n %% 8 == 0 and 16-B alignment");
+  if (n == 0) return 0;
+  const long n8 = n / 8;
+  const long nb = std::min<long>((n8 + 255) / 256, 4096);
+  hipLaunchKernelGGL(accum_f16_f32_kernel, dim3(nb), dim3(256), 0, s, acc, x, n8);
+  return mms::check_launch("accum_f16_f32");
 }

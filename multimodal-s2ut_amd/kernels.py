@@ -621,7 +621,7 @@ def ls_xent_bwd(logits, ld, target, rows, V, eps, pad, lse, grad, out):
 
 
 OST_MULT, OST_GNORM, OST_OVERFLOW, OST_STEP, OST_STEP_SIZE, OST_LOSS_SCALE, OST_ITER, \
-    OST_LAST_OVERFLOW, OST_LAST_RESCALE, OST_CLIP_COEF, OST_FATAL, OST_LR = range(12)
+    OST_LAST_OVERFLOW, OST_LAST_RESCALE, OST_CLIP_COEF, OST_FATAL, OST_LR, OST_INCONSISTENT = range(13)
 OST_SIZE = 16
 
 
@@ -629,6 +629,21 @@ def grad_norm(grad, ost, sample_size=None, nparts=1024):
     part = torch.empty(nparts, dtype=torch.float32, device=grad.device)
     call("mms2ut_grad_sqnorm", grad.data_ptr(), grad.numel(), part.data_ptr(), nparts, _s())
     call("mms2ut_grad_norm_finalize", part.data_ptr(), nparts, ost.data_ptr(), _p(sample_size), _s())
+
+
+def grad_norm_check(buf, world, rank, ost, stage):
+    call("mms2ut_grad_norm_check", buf.data_ptr(), int(world), int(rank), ost.data_ptr(), int(stage), _s())
+
+
+def scale_f16(x, alpha):
+    call("mms2ut_scale_f16", x.data_ptr(), x.numel(), float(alpha), _s())
+    return x
+
+
+def accum_f16_f32(acc, x):
+    assert acc.dtype == torch.float32 and x.dtype == F16 and acc.numel() == x.numel()
+    call("mms2ut_accum_f16_f32", acc.data_ptr(), x.data_ptr(), x.numel(), _s())
+    return acc
 
 
 def optim_prepare(ost, lr, warmup_init_lr, warmup_updates, beta1, beta2, clip, scale_window, min_scale):

@@ -55,7 +55,7 @@ class FP16Adam:
         wu = max(self.warmup_updates, 1)
         return self.lr * math.sqrt(wu) * max(self.num_updates, 1) ** -0.5
 
-    def step(self, sample_size):
+    def step(self, sample_size, check=None):
         """sample_size: device fp32 tensor [1] (all-reduced ntokens).
 
         The global part (grad norm, clip factor, overflow / loss-scale logic) runs on the current
@@ -67,6 +67,8 @@ class FP16Adam:
         launch in stream order instead."""
         b1, b2 = self.betas
         K.grad_norm(self.params.grad, self.ost, sample_size)
+        if check is not None:
+            check(self.ost)      # parallel.GradNormCheck: cross-rank grad-norm consistency
         K.optim_prepare(self.ost, self.lr, self.warmup_init_lr, self.warmup_updates, b1, b2, self.clip,
                         self.scale_window, self.min_loss_scale)
         ps = self.params
@@ -99,4 +101,5 @@ class FP16Adam:
         o = self.ost.cpu()
         return {"gnorm": float(o[K.OST_GNORM]), "overflow": bool(o[K.OST_OVERFLOW]),
                 "loss_scale": float(o[K.OST_LOSS_SCALE]), "step": int(o[K.OST_STEP]),
-                "fatal": bool(o[K.OST_FATAL]), "lr": float(o[K.OST_LR])}
+                "fatal": bool(o[K.OST_FATAL]), "lr": float(o[K.OST_LR]),
+                "inconsistent": bool(o[K.OST_INCONSISTENT])}

@@ -42,9 +42,20 @@ def init_from_env(backend=None):
 
 
 class GradAllReducer:
-    """Bucketed, backward-overlapped SUM all-reduce of a flat gradient buffer."""
+    """Bucketed, backward-overlapped all-reduce of a flat gradient buffer with torch DDP's
+    arithmetic: each bucket is divided by the world size in place, then SUM-all-reduced, so the
+    fp16 gradient magnitudes (hence overflow and the loss-scale trajectory) are those of fairseq's
+    DDP-averaged gradients; the optimizer's multiply factor carries world/sample_size as fairseq's
+    ``multiply_grads(world / sample_size)`` does.  ``acc`` (fp32, optional): gradients accumulated
+    over earlier --update-freq micro-batches, added into each bucket right before it is reduced."""
 
-    def __init__(self, grad_flat, bucket_mb=64.0, group=None):
+    def __init__(self, grad_flat, bucket_mb=64.0, group=None, prescale=None, merge=None):
+        """prescale(bucket, alpha) / merge(bucket, acc_bucket): in-place bucket arithmetic, the HIP
+        kernels by default (kernels.scale_f16 / add_f32_to_f16); host-tensor rehearsals of the
+        bookkeeping (tests/test_plugins.py, gloo on CPU) pass their own."""
+        from . import kernels as K
+        self.prescale = prescale or K.scale_f16
+        self.merge = merge or (lambda g, a: K.add_f32_to_f16(g, a, g))
         self.grad = grad_flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -52,6 +63,7 @@ class GradAllReducer:
         per = max(1, int(bucket_mb * 2 ** 20 // grad_flat.element_size()))
         per = (per + 7) // 8 * 8
         self.bounds = [(a, min(n, a + per)) for a in range(0, n, per)]
+        self.acc = None
         self.reset()
 
     def reset(self):
@@ -74,8 +86,12 @@ class GradAllReducer:
         with (ctx or K._NULLCTX):
             while self.next < len(self.bounds) and self.bounds[self.next][1] <= upto:
                 a, b = self.bounds[self.next]
-                self.handles.append(dist.all_reduce(self.grad[a:b], op=dist.ReduceOp.SUM,
-                                                    group=self.group, async_op=True))
+                g = self.grad[a:b]
+                if self.acc is not None:
+                    self.merge(g, self.acc[a:b])
+                self.prescale(g, 1.0 / self.world)
+                self.handles.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group,
+                                                    async_op=True))
                 self.next += 1
 
     def finish(self):
@@ -85,6 +101,26 @@ class GradAllReducer:
         for h in self.handles:
             h.wait()
         self.reset()
+
+
+class GradNormCheck:
+    """fairseq Trainer._check_grad_norms: after the gradient all-reduce every rank's grad norm
+    must agree (relative 1e-6).  Runs on device (kernels.grad_norm_check + one [world] fp32
+    all-reduce); an inconsistent step is not applied and the optimizer state turns FATAL, which
+    the host raises as FloatingPointError at its next read (FP16Adam.stats)."""
+
+    def __init__(self, device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.buf = torch.zeros(max(self.world, 1), dtype=torch.float32, device=device)
+
+    def __call__(self, ost):
+        from . import kernels as K
+        K.grad_norm_check(self.buf, self.world, self.rank, ost, 0)
+        if self.world > 1:
+            dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
+        K.grad_norm_check(self.buf, self.world, self.rank, ost, 1)
 
 
 def all_reduce_scalars(t, group=None):

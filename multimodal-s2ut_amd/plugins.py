@@ -254,6 +254,134 @@ class UnitSequenceGenerator:
 # ------------------------------------------------------------------------------------ model
 
 
+def _padding_mask(len32, Te):
+    """bool [B, Te] (True = pad) from subsampled lengths (fairseq lengths_to_padding_mask)."""
+    return torch.arange(Te, device=len32.device)[None, :] >= len32.long()[:, None]
+
+
+def encoder_out_dict(net, enc, len32, Te, ctx=None, return_all_hiddens=False):
+    """fairseq S2TTransformerEncoder's output contract over the HIP encoder's
+    batch-major buffers, as zero-copy time-major views: encoder_out [Te, B, C]; encoder_padding_mask
+    [B, Te] or [] when nothing is padded (fairseq's idiom); encoder_states: the L_e
+    layer outputs before the final LayerNorm when return_all_hiddens (else [])."""
+    d = net.cfg["encoder_embed_dim"]
+    B = len32.shape[0]
+    tm = lambda x: x.view(B, Te, d).transpose(0, 1)  # noqa: E731
+    mask = _padding_mask(len32, Te)
+    states = []
+    if return_all_hiddens and ctx is not None:
+        layers = ctx["layers"]
+        states = [tm(layers[l + 1]["x"]) for l in range(len(layers) - 1)] + ([tm(ctx["lx"])] if layers else [])
+    return {"encoder_out": [tm(enc)], "encoder_padding_mask": [mask] if bool(mask.any()) else [],
+            "encoder_embedding": [], "encoder_states": states, "src_tokens": [], "src_lengths": []}
+
+
+def reorder_encoder_out(encoder_out, new_order):
+    """fairseq S2TTransformerEncoder.reorder_encoder_out: select batch entries (beam expansion /
+    finished sentences leaving the batch) in every field of the encoder-out dict."""
+    sel = lambda xs, dim: [x.index_select(dim, new_order) for x in xs]  # noqa: E731
+    return {"encoder_out": sel(encoder_out["encoder_out"], 1),
+            "encoder_padding_mask": sel(encoder_out["encoder_padding_mask"], 0),
+            "encoder_embedding": sel(encoder_out.get("encoder_embedding", []), 0),
+            "encoder_states": sel(encoder_out.get("encoder_states", []), 1),
+            "src_tokens": [], "src_lengths": []}
+
+
+def _enc_from_dict(net, encoder_out):
+    """encoder-out dict -> (batch-major fp16 [B*Te, d], subsampled lengths int32 [B], Te)."""
+    x = encoder_out["encoder_out"][0]
+    Te, B, d = x.shape
+    enc = x.transpose(0, 1).to(torch.float16).contiguous().view(B * Te, d)
+    pm = encoder_out.get("encoder_padding_mask") or []
+    if len(pm) > 0:
+        len32 = (~pm[0]).sum(1).to(torch.int32)
+    else:
+        len32 = torch.full((B,), Te, dtype=torch.int32, device=x.device)
+    return enc, len32.contiguous(), Te
+
+
+class EncoderAdapter:
+    """``model.encoder`` as fairseq's generator drives it: forward / forward_torchscript /
+    reorder_encoder_out / max_positions (MM_S2STransformerEncoder, mm_s2s_transformer.py:378-562)."""
+
+    def __init__(self, owner):
+        self.owner = owner
+
+    def forward(self, src_tokens, src_lengths, src_audio_path=None, img_path=None, img_tensor=None,
+                imgs_list=(), img_masks_list=(), tgt_speaker=None, return_all_hiddens=False, **kw):
+        return self.owner.forward_encoder(src_tokens, src_lengths, src_audio_path, img_path, img_tensor,
+                                          imgs_list, img_masks_list, tgt_speaker, return_all_hiddens)
+
+    __call__ = forward
+
+    def forward_torchscript(self, net_input):
+        return self.forward(**{k: v for k, v in net_input.items() if k != "prev_output_tokens"})
+
+    def reorder_encoder_out(self, encoder_out, new_order):
+        return reorder_encoder_out(encoder_out, new_order)
+
+    def max_positions(self):
+        return self.owner.cfg["max_source_positions"]
+
+
+class DecoderAdapter:
+    """``model.decoder`` with fairseq's incremental-decoder interface (TransformerUnitDecoder):
+    forward(prev_output_tokens, encoder_out, incremental_state) -> (logits [B, T, V], extra),
+    reorder_incremental_state(_scripting), get_normalized_probs, max_positions.  Without an
+    incremental_state the whole prefix is decoded (teacher forcing); with one, the HIP incremental
+    decoder (generate.IncrementalDecoder: KV cache + slot table) decodes the last position."""
+
+    KEY = "_mms2ut_incremental_decoder"
+
+    def __init__(self, owner):
+        self.owner = owner
+
+    def forward(self, prev_output_tokens, encoder_out=None, incremental_state=None, features_only=False, **kw):
+        net = self.owner.net
+        if features_only:
+            raise NotImplementedError("features_only decoder outputs")
+        if torch.is_grad_enabled() and net.training:
+            raise NotImplementedError("decoder adapter is inference-only: training runs the fused model "
+                                      "forward (its backward is hand-written end to end)")
+        V = self.owner.cfg["vocab_size"]
+        enc, len32, Te = _enc_from_dict(net, encoder_out)
+        tok = prev_output_tokens.to(enc.device)
+        B, T = tok.shape
+        if incremental_state is None:
+            batch = runtime.decoder_batch(tok, self.owner.cfg)
+            with torch.no_grad():
+                logits, _ = net.decoder_forward(batch, enc, len32, Te)
+            return logits.view(B, T, -1)[:, :, :V].float(), {"attn": [None], "inner_states": None}
+        from . import generate as G
+        inc = incremental_state.get(self.KEY)
+        if inc is None:
+            if T != 1:
+                raise NotImplementedError("incremental decoding must start from the first position")
+            maxlen = int(os.environ.get("MMS2UT_INC_MAXLEN", min(1024, self.owner.cfg["max_target_positions"])))
+            inc = G.IncrementalDecoder(net, enc, len32, Te, B, 1, maxlen)
+            incremental_state[self.KEY] = inc
+        with torch.no_grad():
+            inc.step(tok[:, -1].contiguous(), T - 1)
+        return inc.logits[:, :V].float().view(B, 1, V), {"attn": [None], "inner_states": None}
+
+    __call__ = forward
+
+    def reorder_incremental_state(self, incremental_state, new_order):
+        inc = incremental_state.get(self.KEY) if incremental_state is not None else None
+        if inc is not None:
+            # beam = 1 inside: every hypothesis owns its encoder rows, gathered with it
+            inc.reorder(new_order.to(inc.dev), batch_idxs=new_order.to(inc.dev))
+
+    reorder_incremental_state_scripting = reorder_incremental_state
+
+    def get_normalized_probs(self, net_output, log_probs, sample=None):
+        logits = net_output[0].float()
+        return torch.log_softmax(logits, -1) if log_probs else torch.softmax(logits, -1)
+
+    def max_positions(self):
+        return self.owner.cfg["max_target_positions"]
+
+
 @register_model("mm_s2ut_transformer")
 class MM_S2UTTransformerModel:
     """mm_s2s_transformer.py:625-700 over the HIP model (module tree / state-dict keys kept)."""
@@ -261,6 +389,8 @@ class MM_S2UTTransformerModel:
     def __init__(self, cfg, device="cuda", seed=1):
         self.net = MMS2UTModel(cfg, device=device, seed=seed).init_params(seed)
         self.cfg = self.net.cfg
+        self.encoder = EncoderAdapter(self)
+        self.decoder = DecoderAdapter(self)
 
     @classmethod
     def build_model(cls, args, task, device="cuda"):
@@ -281,24 +411,68 @@ class MM_S2UTTransformerModel:
         sd = {k: v for k, v in sd.items() if k != "decoder.output_projection.weight"}
         return self.net.params.load_state_dict(sd, strict=strict)
 
+    def max_positions(self):
+        return (self.cfg["max_source_positions"], self.cfg["max_target_positions"])
+
+    def max_decoder_positions(self):
+        return self.cfg["max_target_positions"]
+
+    def _batch(self, src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target=None):
+        sample = {"net_input": {"src_tokens": src_tokens, "src_lengths": src_lengths,
+                                "prev_output_tokens": prev_output_tokens, "imgs_list": list(imgs_list or []),
+                                "img_masks_list": list(img_masks_list or [])},
+                  "target": target if target is not None else prev_output_tokens,
+                  "ntokens": int(prev_output_tokens.ne(self.cfg["padding_idx"]).sum())}
+        return runtime.prepare_batch(sample, self.cfg, self.net.device)
+
+    def forward_encoder(self, src_tokens, src_lengths, src_audio_path=None, img_path=None, img_tensor=None,
+                        imgs_list=(), img_masks_list=(), tgt_speaker=None, return_all_hiddens=False, **kw):
+        """mm_s2s_transformer.py:643-665 -> fairseq's encoder-out dict (encoder_out_dict).  The
+        encoder runs without a tape (inference / generation); training gradients flow through
+        ``forward``, whose backward is hand-written across the whole model."""
+        if tgt_speaker is not None:
+            raise NotImplementedError("target speaker embeddings (spk_emb_proj) are out of scope")
+        B = src_tokens.shape[0]
+        prev = torch.full((B, 1), 2, dtype=torch.long)
+        batch = self._batch(src_tokens, src_lengths, prev, imgs_list, img_masks_list)
+        with torch.no_grad():
+            enc, len32, Te, ctx = self.net.encoder_forward(batch)
+        return encoder_out_dict(self.net, enc, len32, Te, ctx, return_all_hiddens)
+
+    def reorder_encoder_out(self, encoder_out, new_order):
+        return reorder_encoder_out(encoder_out, new_order)
+
+    def reorder_incremental_state(self, incremental_state, new_order):
+        self.decoder.reorder_incremental_state(incremental_state, new_order)
+
+    def get_normalized_probs(self, net_output, log_probs, sample=None):
+        return self.decoder.get_normalized_probs(net_output, log_probs, sample)
+
     def forward(self, src_tokens, src_lengths, prev_output_tokens, src_audio_path=None, img_path=None,
                 img_tensor=None, imgs_list=(), img_masks_list=(), tgt_speaker=None,
                 return_all_hiddens=False, target=None, **kwargs):
         """Reference signature (mm_s2s_transformer.py:667-680) -> (logits [B, Tt, V], extra).
-        The logits are autograd-connected to the hand-written backward."""
+        The logits are autograd-connected to the hand-written backward.  return_all_hiddens adds
+        ``encoder_states`` (L_e layer outputs, [Te, B, C]) and ``encoder_padding_mask`` to extra
+        as the reference does (:697-699)."""
         if tgt_speaker is not None:
             raise NotImplementedError("target speaker embeddings (spk_emb_proj) are out of scope")
-        sample = {"net_input": {"src_tokens": src_tokens, "src_lengths": src_lengths,
-                                "prev_output_tokens": prev_output_tokens, "imgs_list": list(imgs_list),
-                                "img_masks_list": list(img_masks_list)},
-                  "target": target if target is not None else prev_output_tokens,
-                  "ntokens": int(prev_output_tokens.ne(self.cfg["padding_idx"]).sum())}
-        batch = runtime.prepare_batch(sample, self.cfg, self.net.device)
-        logits = runtime.model_logits(self.net, batch)
+        batch = self._batch(src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target)
+        stash = {}
+        if return_all_hiddens:
+            self.net.encoder_hook = stash.__setitem__
+        try:
+            logits = runtime.model_logits(self.net, batch)
+        finally:
+            self.net.encoder_hook = None
         B, Tt = prev_output_tokens.shape
         V = self.cfg["vocab_size"]
         out = logits.view(B, Tt, -1)[:, :, :V]
         extra = {"attn": [None], "inner_states": None, "_batch": batch, "_logits_padded": logits}
+        if return_all_hiddens:
+            eo = encoder_out_dict(self.net, stash["enc"], batch.enc_len32, batch.Te, stash["ctx"], True)
+            extra["encoder_states"] = eo["encoder_states"]
+            extra["encoder_padding_mask"] = eo["encoder_padding_mask"]
         return out, extra
 
     __call__ = forward
@@ -375,6 +549,8 @@ def build_parser():
     p.add_argument("--num-workers", type=int, default=0)
     p.add_argument("--user-dir", default=None)
     p.add_argument("--save-dir", default=None)
+    p.add_argument("--restore-file", default="checkpoint_last.pt")
+    p.add_argument("--save-interval-updates", type=int, default=0)
     p.add_argument("--log-interval", type=int, default=10)
     # accepted for command-line compatibility with 1_train.sh (no effect on the training step)
     p.add_argument("--distributed-world-size", type=int, default=None)

@@ -56,17 +56,7 @@ def prepare_batch(sample, cfg, device="cuda", src_override=None):
     enc_len = subsampled_lengths(lens, nl).astype(np.int32)
     prev_cpu = ni["prev_output_tokens"].cpu()
     B, Tt = prev_cpu.shape
-    pad = cfg["padding_idx"]
-    padm = prev_cpu.eq(pad)
-    tgt_mask = None
-    if bool(padm.any()):
-        tm = torch.zeros(B, round_up(Tt, 8), dtype=torch.uint8)
-        tm[:, :Tt] = padm.to(torch.uint8)
-        tgt_mask = tm.to(dev, non_blocking=True)
-    # fairseq collate_tokens(left_pad=False): padding is a suffix -> it is a key length
-    nonpad = (~padm).sum(1)
-    right_padded = bool(torch.all(padm == (torch.arange(Tt)[None, :] >= nonpad[:, None])))
-    tgt_len32 = nonpad.to(torch.int32).to(dev, non_blocking=True) if right_padded else None
+    tgt_mask, tgt_len32 = _target_masks(prev_cpu, cfg["padding_idx"], dev)
     imgs = img_keymask = None
     imgs_list = ni.get("imgs_list") or []
     if cfg["fusion"] and len(imgs_list) > 0:
@@ -88,10 +78,44 @@ def prepare_batch(sample, cfg, device="cuda", src_override=None):
         nsentences=int(sample.get("nsentences", B)), n_src_frames=int(lens.sum()))
 
 
+def _target_masks(prev_cpu, pad, dev):
+    """(uint8 [B, round8(Tt)] key mask or None, int32 [B] key lengths when right-padded or None)."""
+    B, Tt = prev_cpu.shape
+    padm = prev_cpu.eq(pad)
+    tgt_mask = None
+    if bool(padm.any()):
+        tm = torch.zeros(B, round_up(Tt, 8), dtype=torch.uint8)
+        tm[:, :Tt] = padm.to(torch.uint8)
+        tgt_mask = tm.to(dev, non_blocking=True)
+    # fairseq collate_tokens(left_pad=False): padding is a suffix -> it is a key length
+    nonpad = (~padm).sum(1)
+    right_padded = bool(torch.all(padm == (torch.arange(Tt)[None, :] >= nonpad[:, None])))
+    tgt_len32 = nonpad.to(torch.int32).to(dev, non_blocking=True) if right_padded else None
+    return tgt_mask, tgt_len32
+
+
+@dataclass
+class DecoderBatch:
+    prev: torch.Tensor
+    tgt_mask: Optional[torch.Tensor]
+    tgt_len32: Optional[torch.Tensor]
+
+
+def decoder_batch(prev_output_tokens, cfg):
+    """The decoder-side fields of a DeviceBatch for a [B, T] prefix already on the device."""
+    cpu = prev_output_tokens.cpu()
+    dev = prev_output_tokens.device
+    tm, tl = _target_masks(cpu, cfg["padding_idx"], dev)
+    return DecoderBatch(prev=prev_output_tokens.contiguous(), tgt_mask=tm, tgt_len32=tl)
+
+
 class _ModelFn(torch.autograd.Function):
     @staticmethod
     def forward(fctx, anchor, model, batch):
         enc, len32, Te, ectx = model.encoder_forward(batch)
+        if getattr(model, "encoder_hook", None) is not None:   # return_all_hiddens (plugins.py)
+            model.encoder_hook("enc", enc)
+            model.encoder_hook("ctx", ectx)
         logits, dctx = model.decoder_forward(batch, enc, len32, Te)
         fctx.model = model
         fctx.saved = (ectx, dctx, enc, batch)

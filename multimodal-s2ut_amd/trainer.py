@@ -1,11 +1,21 @@
-"""Trainer: one optimizer update per batch (update-freq 1), fairseq Trainer.train_step semantics.
+"""Trainer: one optimizer update per ``update_freq`` micro-batches, fairseq Trainer.train_step
+semantics.
 
-  zero grads -> fwd (model + LS-CE) -> loss.backward(loss_scale) [hand-written bwd, bucketed RCCL
-  all-reduce overlapped] -> sample_size all-reduce -> FP16Optimizer/Adam (device-side overflow skip
-  + loss-scale update) -> lr schedule.
+  per micro-batch: fwd (model + LS-CE) -> loss.backward(loss_scale) [hand-written bwd]
+  gradients of micro-batches 1..n-1 accumulate into an fp32 buffer; the last micro-batch's
+  backward adds it bucket by bucket just before the bucketed RCCL all-reduce (overlapped with the
+  backward) -> scalar all-reduce (loss, nll, ntokens, ...) -> grad norm -> cross-rank grad-norm
+  consistency check -> FP16Optimizer/Adam (device-side overflow skip + loss-scale update) -> lr.
 
-fairseq reference: Trainer.train_step (multiply_grads(world/sample_size) after DDP's averaging
-== SUM all-reduce then 1/sample_size), FP16Optimizer.clip_grad_norm(10), DynamicLossScaler.
+fairseq reference: Trainer.train_step (DDP no_sync on all but the last micro-batch; DDP averages
+gradients, then multiply_grads(world/sample_size) with sample_size summed over micro-batches and
+ranks), FP16Optimizer.clip_grad_norm(10), DynamicLossScaler (scale window 2^14/world/update_freq),
+Trainer._check_grad_norms.
+
+Buffer access: the Adam update and the gradient zeroing run deferred on the side stream
+(optim.FP16Adam.step).  Call ``trainer.sync()`` (or ``model.params.await_all()``) before reading
+``params.flat`` / ``params.grad`` / ``opt.master`` directly after a step; ``state_dict``,
+``opt.stats`` and the next forward wait by themselves.
 """
 import os
 
@@ -14,20 +24,28 @@ import torch
 from . import kernels as K
 from . import runtime
 from .optim import FP16Adam
-from .parallel import GradAllReducer, all_reduce_scalars
+from .parallel import GradAllReducer, GradNormCheck, all_reduce_scalars
+
+# log slots (all-reduced SUM over ranks every step)
+LOG_LOSS, LOG_NLL, LOG_NTOKENS, LOG_NSENT, LOG_SS_OVER_WORLD = range(5)
 
 
 class Trainer:
     def __init__(self, model, lr=5e-4, betas=(0.9, 0.98), clip_norm=10.0, warmup_updates=10000,
-                 warmup_init_lr=1e-7, init_scale=128.0, bucket_mb=64.0, world_size=1):
+                 warmup_init_lr=1e-7, init_scale=128.0, bucket_mb=64.0, world_size=1, update_freq=1):
         self.model = model
         self.cfg = model.cfg
+        self.update_freq = int(update_freq)
+        if self.update_freq < 1:
+            raise ValueError("update_freq must be >= 1")
         self.opt = FP16Adam(model.params, lr=lr, betas=betas, clip_norm=clip_norm, init_scale=init_scale,
-                            world_size=world_size, warmup_updates=warmup_updates,
-                            warmup_init_lr=warmup_init_lr)
+                            world_size=world_size, update_freq=self.update_freq,
+                            warmup_updates=warmup_updates, warmup_init_lr=warmup_init_lr)
         self.reducer = GradAllReducer(model.params.grad, bucket_mb) if world_size > 1 else None
+        self.norm_check = GradNormCheck(model.params.flat.device) if world_size > 1 else None
         self.world = world_size
-        self.log = torch.zeros(4, dtype=torch.float32, device=model.params.flat.device)
+        self.acc = None   # fp32 gradient accumulator (update_freq > 1), allocated on first use
+        self.log = torch.zeros(5, dtype=torch.float32, device=model.params.flat.device)
         # The step's critical path (forward, dgrad chain, optimizer) runs on a high-priority stream
         # so the hardware dispatcher prefers its workgroups over the weight-gradient side stream's
         # (lowest priority), which only fills the CUs the critical path leaves idle.
@@ -38,45 +56,75 @@ class Trainer:
                 K._Side.stream = K.make_side_stream(model.params.flat.device)
                 K._Side.ptr = K._Side.stream.cuda_stream
 
-    def train_step(self, batch):
+    def sync(self):
+        """Wait (on the current stream) for every deferred optimizer chunk of the last step."""
+        self.model.params.await_all()
+
+    def train_step(self, batches):
+        """batches: one runtime.DeviceBatch or a list of ``update_freq`` micro-batches (fairseq's
+        ``samples``).  Returns the device log [loss, nll, ntokens, nsentences, ntokens/world]
+        summed over micro-batches and ranks."""
+        if not isinstance(batches, (list, tuple)):
+            batches = [batches]
+        if len(batches) != self.update_freq:
+            raise ValueError(f"train_step: {len(batches)} micro-batches for update_freq {self.update_freq}")
         if self.stream is None:
-            return self._train_step(batch)
+            return self._train_step(batches)
         cur = torch.cuda.current_stream()
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
-            log = self._train_step(batch)
+            log = self._train_step(batches)
         cur.wait_stream(self.stream)
         return log
 
-    def _train_step(self, batch):
+    def _train_step(self, batches):
         cfg = self.cfg
         m = self.model
         m.train()
-        if self.reducer is not None:
-            self.reducer.reset()
-            m.grad_ready_hook = self.reducer.ready
-        logits = runtime.model_logits(m, batch)
-        # zeroed after the forward: by then every deferred optimizer chunk of the previous step
-        # (which reads the gradients) has been waited for (ParamStore.await_group)
-        m.params.await_all()
-        if not getattr(m.params, "grad_zeroed", False):
-            m.params.grad.zero_()
-        m.params.grad_zeroed = False
-        loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
-                                              cfg["label_smoothing"], cfg["padding_idx"])
-        del logits
-        loss.backward(self.opt.loss_scale())
-        m.grad_ready_hook = None
+        n = len(batches)
+        if n > 1 and self.acc is None:
+            self.acc = torch.zeros(m.params.numel, dtype=torch.float32, device=m.params.flat.device)
+        self.log.zero_()
+        ntok = sum(int(b.ntokens) for b in batches)
+        for i, batch in enumerate(batches):
+            last = i == n - 1
+            if self.reducer is not None and last:
+                self.reducer.reset()
+                self.reducer.acc = self.acc if n > 1 else None
+                m.grad_ready_hook = self.reducer.ready
+            logits = runtime.model_logits(m, batch)
+            # zeroed after the forward: by then every deferred optimizer chunk of the previous step
+            # (which reads the gradients) has been waited for (ParamStore.await_group).  Every
+            # micro-batch starts from zero (a backward writes, not adds, most of its gradients).
+            m.params.await_all()
+            if i > 0 or not getattr(m.params, "grad_zeroed", False):
+                m.params.grad.zero_()
+            m.params.grad_zeroed = False
+            loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
+                                                  cfg["label_smoothing"], cfg["padding_idx"])
+            del logits
+            loss.backward(self.opt.loss_scale())
+            m.grad_ready_hook = None
+            if n > 1:
+                if i == 0:
+                    self.acc.zero_()
+                if not last:
+                    K.accum_f16_f32(self.acc, m.params.grad)
+                elif self.reducer is None:
+                    K.add_f32_to_f16(m.params.grad, self.acc, m.params.grad)
+            self.log[LOG_LOSS] += loss.detach()
+            self.log[LOG_NLL] += nll.detach()
         if self.reducer is not None:
             self.reducer.finish()
-        # logging / sample-size sync: [loss, nll, ntokens, nsentences] summed over ranks
-        self.log[0] = loss.detach()
-        self.log[1] = nll.detach()
-        # fill_ takes the scalar as a kernel argument (item assignment would be a blocking H2D copy)
-        self.log[2].fill_(float(batch.ntokens))
-        self.log[3].fill_(float(batch.nsentences))
+            self.reducer.acc = None
+        # logging / sample-size sync: fixed scalars summed over ranks (fill_ takes the scalar as a
+        # kernel argument; item assignment would be a blocking H2D copy)
+        self.log[LOG_NTOKENS].fill_(float(ntok))
+        self.log[LOG_NSENT].fill_(float(sum(int(b.nsentences) for b in batches)))
+        self.log[LOG_SS_OVER_WORLD].fill_(float(ntok) / self.world)
         all_reduce_scalars(self.log)
-        self.opt.step(self.log[2:3])
+        # DDP-averaged gradients (sum / world): multiply factor world / (scale * sample_size)
+        self.opt.step(self.log[LOG_SS_OVER_WORLD:LOG_SS_OVER_WORLD + 1], check=self.norm_check)
         return self.log
 
     def valid_step(self, batch):
@@ -88,3 +136,25 @@ class Trainer:
                                                   self.cfg["label_smoothing"], self.cfg["padding_idx"])
         m.train()
         return loss, nll
+
+    # ------------------------------------------------------------------ checkpoints
+    def state_dict(self):
+        """fairseq checkpoint layout (checkpoint_utils.save_checkpoint): model (fairseq keys),
+        last_optimizer_state (fp32 master / Adam moments / device optimizer state vector)."""
+        self.sync()
+        o = self.opt
+        return {"model": {k: v.detach().cpu() for k, v in self.model.params.state_dict().items()},
+                "last_optimizer_state": {"master": o.master.cpu(), "exp_avg": o.exp_avg.cpu(),
+                                         "exp_avg_sq": o.exp_avg_sq.cpu(), "ost": o.ost.cpu()},
+                "extra_state": {"num_updates": int(o.ost[K.OST_STEP].item())}}
+
+    def load_state_dict(self, ckpt):
+        self.sync()
+        self.model.params.load_state_dict({k: v for k, v in ckpt["model"].items()
+                                           if k != "decoder.output_projection.weight"})
+        o, s = self.opt, ckpt.get("last_optimizer_state")
+        if s is None:
+            o.resync_master()
+            return
+        for name in ("master", "exp_avg", "exp_avg_sq", "ost"):
+            getattr(o, name).copy_(s[name])

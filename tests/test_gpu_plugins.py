@@ -105,3 +105,151 @@ def test_cli_trains_on_manifest(tmp_path, capsys):
     recs = [json.loads(l) for l in capsys.readouterr().out.splitlines() if l.startswith("{")]
     assert [r["num_updates"] for r in recs] == [5]
     assert recs[0]["loss"] > 0 and recs[0]["wps"] > 0
+
+
+def _tiny_model(tmp_path, seed=11):
+    P = pkg("plugins")
+    a = _args(tmp_path)
+    task = P.REGISTRY["task"][a.task].setup_task(a)
+    model = task.build_model(a)
+    ocfg = R.no_dropout(R.tiny_config())
+    Pp = {k: v.half().float() for k, v in R.init_params(ocfg, seed=seed, include_unused=False).items()}
+    model.load_state_dict(Pp, strict=True)
+    return P, model, ocfg, Pp
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_return_all_hiddens_and_encoder_out_contract(tmp_path):
+    """mm_s2s_transformer.py:643-665 / :697-699: forward(return_all_hiddens=True) puts the L_e
+    per-layer encoder states and the padding mask in extra; forward_encoder returns fairseq's
+    encoder-out dict; reorder_encoder_out selects batch entries in every field."""
+    P, model, ocfg, Pp = _tiny_model(tmp_path)
+    mm = pkg()
+    sample = mm.data.make_sample([300, 211, 160], [91, 64, 49], img_tokens=37, img_dim=768, seed=3)
+    ni = sample["net_input"]
+    ni["src_tokens"] = ni["src_tokens"].half().float()
+    ni["imgs_list"][0] = ni["imgs_list"][0].half().float()
+    model.train()
+    logits, extra = model(**ni, return_all_hiddens=True, target=sample["target"])
+    enc_o, pad_o, states_o = R.encoder_forward(Pp, ni["src_tokens"], ni["src_lengths"], ocfg,
+                                               imgs=ni["imgs_list"][0], return_all_hiddens=True)
+    assert len(extra["encoder_states"]) == ocfg["encoder_layers"] == len(states_o)
+    for s, so in zip(extra["encoder_states"], states_o):
+        assert s.shape == so.shape and _rel(s, so) < 1e-2
+    assert torch.equal(extra["encoder_padding_mask"][0].cpu(), pad_o)
+    logits.sum().backward()                 # the states do not break the fused backward
+    torch.cuda.synchronize()
+    model.eval()
+    eo = model.forward_encoder(ni["src_tokens"], ni["src_lengths"], imgs_list=ni["imgs_list"],
+                               img_masks_list=ni["img_masks_list"], return_all_hiddens=True)
+    assert set(eo) == {"encoder_out", "encoder_padding_mask", "encoder_embedding", "encoder_states",
+                       "src_tokens", "src_lengths"}
+    assert eo["encoder_out"][0].shape == enc_o.shape and _rel(eo["encoder_out"][0], enc_o) < 1e-2
+    assert torch.equal(eo["encoder_padding_mask"][0].cpu(), pad_o)
+    order = torch.tensor([2, 0, 0, 1], device="cuda")
+    ro = model.reorder_encoder_out(eo, order)
+    assert torch.equal(ro["encoder_out"][0], eo["encoder_out"][0].index_select(1, order))
+    assert torch.equal(ro["encoder_padding_mask"][0], eo["encoder_padding_mask"][0][order])
+    assert len(ro["encoder_states"]) == 2 and ro["encoder_states"][1].shape[1] == 4
+    # a batch without padding: fairseq's [] mask (SURVEY Q1)
+    one = model.forward_encoder(ni["src_tokens"][:1, :300], ni["src_lengths"][:1],
+                                imgs_list=[ni["imgs_list"][0][:1]], img_masks_list=[None])
+    assert one["encoder_padding_mask"] == [] and one["encoder_states"] == []
+
+
+def test_decoder_adapter_incremental_matches_full_prefix(tmp_path):
+    """fairseq's incremental-decoder protocol through model.decoder: per-step logits with an
+    incremental_state (HIP KV-cache decoder) equal the full-prefix decode at the last position,
+    across a reorder_incremental_state that permutes and drops hypotheses."""
+    P, model, ocfg, Pp = _tiny_model(tmp_path, seed=12)
+    mm = pkg()
+    sample = mm.data.make_sample([160, 120, 97], [5, 5, 5], img_tokens=37, img_dim=768, seed=4)
+    ni = sample["net_input"]
+    model.eval()
+    with torch.no_grad():
+        eo = model.encoder.forward_torchscript(ni)
+        beam = 2
+        eo = model.encoder.reorder_encoder_out(eo, torch.arange(3, device="cuda").repeat_interleave(beam))
+        g = torch.Generator().manual_seed(0)
+        toks = torch.randint(4, 1004, (6, 12), generator=g).cuda()
+        toks[:, 0] = 2
+        inc = {}
+        order_full = torch.arange(6, device="cuda")
+        for t in range(12):
+            if t == 5:   # hypotheses permuted within sentences and one sentence leaving the batch
+                new = torch.tensor([1, 0, 5, 4], device="cuda")
+                model.reorder_incremental_state(inc, new)
+                eo = model.reorder_encoder_out(eo, new)
+                toks = toks[new]
+            lg_inc, _ = model.decoder(toks[:, :t + 1], encoder_out=eo, incremental_state=inc)
+            lg_full, _ = model.decoder(toks[:, :t + 1], encoder_out=eo)
+            assert lg_inc.shape == (toks.shape[0], 1, 1004)
+            assert _rel(lg_inc[:, 0], lg_full[:, -1]) < 1e-2, t
+            lp = model.get_normalized_probs((lg_inc, None), log_probs=True)
+            assert torch.allclose(lp.exp().sum(-1), torch.ones_like(lp[..., 0]), atol=1e-4)
+    del order_full
+
+
+def test_update_freq_accumulation_matches_union(tmp_path):
+    """--update-freq 2: one update from two micro-batches; the gradient equals the union batch's
+    gradient.  The union pads the second batch to a longer length, so GEMM accumulation order and
+    fp16 rounding differ and FFN units within rounding of 0 switch ReLU sides:
+    1e-2, the model-parity gradient tolerance.  Same-shape equality (accumulated vs DP-reduced)
+    is checked at 1e-3 in test_gpu_dp.py."""
+    mm = pkg()
+    cfg = mm.default_cfg(**R.no_dropout(R.tiny_config(conv_channels=256)))
+    samples = [mm.data.make_sample(L, T, img_tokens=37, img_dim=768, seed=s)
+               for s, (L, T) in enumerate((([120, 90], [30, 22]), ([100, 77, 60], [25, 20, 15])))]
+    grads = {}
+    for name, uf in (("accum", 2), ("union", 1)):
+        os_env = __import__("os").environ
+        os_env["MMS2UT_DEFER_ADAM"] = "0"
+        try:
+            model = mm.MMS2UTModel(cfg, device="cuda").init_params(seed=5)
+            tr = mm.trainer.Trainer(model, lr=1e-4, update_freq=uf, init_scale=8.0)
+        finally:
+            os_env.pop("MMS2UT_DEFER_ADAM")
+        if uf == 2:
+            bs = [mm.runtime.prepare_batch(s, cfg, "cuda") for s in samples]
+        else:
+            items = []
+            for s in samples:
+                ni = s["net_input"]
+                for b in range(ni["src_tokens"].shape[0]):
+                    L = int(ni["src_lengths"][b])
+                    items.append({"index": len(items), "source": ni["src_tokens"][b, :L], "target": s["target"][b][s["target"][b] != 1],
+                                  "img": ni["imgs_list"][0][b]})
+            bs = [mm.runtime.prepare_batch(mm.data.collater(items), cfg, "cuda")]
+        log = tr.train_step(bs)
+        torch.cuda.synchronize()
+        assert not tr.opt.stats()["overflow"]
+        grads[name] = (model.params.grad.float().cpu(), float(log[2]))
+    assert grads["accum"][1] == grads["union"][1]
+    assert _rel(grads["accum"][0], grads["union"][0]) < 1e-2
+
+
+def test_cli_save_dir_checkpoint_and_restore(tmp_path, capsys):
+    """--save-dir writes checkpoint_last.pt (fairseq keys, optimizer state, num_updates);
+    a second run restores it and continues the update count (fairseq --restore-file)."""
+    a = _args(tmp_path)
+    y = a.multimodal_translation_config_yaml
+    sd = tmp_path / "ckpt"
+    base = (f"/d --task multimodal_speech_to_speech --arch mm_s2ut_transformer --criterion speech_to_unit "
+            f"--target-is-code --target-code-size 1000 --share-decoder-input-output-embed --fp16 "
+            f"--multimodal-translation-config-yaml {y} {TINY} --max-tokens 6000 --log-interval 2 "
+            f"--warmup-updates 4 --lr 1e-3 --synthetic --save-dir {sd} --update-freq 2")
+    assert pkg("cli").main((base + " --max-update 2").split()) == 0
+    ck = torch.load(sd / "checkpoint_last.pt", map_location="cpu", weights_only=True)
+    assert "encoder.transformer_layers.0.fc1.weight" in ck["model"]
+    assert set(ck["last_optimizer_state"]) == {"master", "exp_avg", "exp_avg_sq", "ost"}
+    n1 = ck["extra_state"]["num_updates"]
+    assert 1 <= n1 <= 2
+    assert pkg("cli").main((base + " --max-update 4").split()) == 0
+    recs = [json.loads(l) for l in capsys.readouterr().out.splitlines() if l.startswith("{")]
+    assert recs[-1]["num_updates"] == 4
+    ck2 = torch.load(sd / "checkpoint_last.pt", map_location="cpu", weights_only=True)
+    assert ck2["extra_state"]["num_updates"] > n1

@@ -190,7 +190,8 @@ def _reducer_worker(rank, world, port, q):
         r, w, _ = par.init_from_env(backend="gloo")
         n = 1000
         g = torch.arange(n, dtype=torch.float32) * (r + 1)
-        red = par.GradAllReducer(g, bucket_mb=256 * 4 / 2 ** 20)  # 256-element buckets
+        # 256-element buckets; host tensors: the DDP pre-division by world as a host op
+        red = par.GradAllReducer(g, bucket_mb=256 * 4 / 2 ** 20, prescale=lambda b, a: b.mul_(a))
         assert len(red.bounds) == 4
         for upto in (100, 300, 600, 1000):  # layer completion offsets
             red.ready(upto)
@@ -198,7 +199,7 @@ def _reducer_worker(rank, world, port, q):
         red.finish()
         s = torch.tensor([1.0 + r, 10.0 * (r + 1)])
         par.all_reduce_scalars(s)
-        q.put((r, launched_before_finish, torch.equal(g, torch.arange(n, dtype=torch.float32) * 3),
+        q.put((r, launched_before_finish, torch.equal(g, torch.arange(n, dtype=torch.float32) * 1.5),
                s.tolist()))
     except Exception as e:  # pragma: no cover
         q.put((rank, "error", repr(e), None))
