@@ -327,6 +327,10 @@ def main():
     classes = {}
     if not args.no_gemm_timing:
         t_prof, _, (gemm_ms, n_launch, launched_flops, gemm_bytes), (l_ms, l_fl, l_cls) = timed(True)
+        if os.environ.get("MMS2UT_GEMM_DUMP"):
+            # per-launch table of the roofline pass (scripts/gemm_table.py summarises it)
+            np.savez(os.environ["MMS2UT_GEMM_DUMP"], ms=l_ms, flops=l_fl, cls=l_cls,
+                     mnk=kernels.gemm_profile_shapes(int(n_launch)), steps=args.steps)
         for ms_, fl_, c_ in zip(l_ms.tolist(), l_fl.tolist(), l_cls.tolist()):
             if c_ & 256:
                 name = "batched (fusion attention QK^T / PV)"

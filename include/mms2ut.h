@@ -88,6 +88,8 @@ int mms2ut_profile_bytes(double* bytes);
  * a class word: bit0 A K-contiguous, bit1 B K-contiguous, bits 2-7 epilogue, bit8 batched,
  * bit9 split-K.  Lets the bench split forward / dgrad (NT) from weight-gradient (TN) launches.   */
 int mms2ut_profile_launches(float* ms, double* flops, int* cls, int n);
+/* the same window's shapes: mnk[4i..4i+3] = M, N, K, batch * splitk of launch i                  */
+int mms2ut_profile_shapes(int* mnk, int n);
 
 /* sum `nsplit` fp32 slabs [rows, cols] (slab stride `slab`) * alpha -> out, row stride ldo.
  * mode bit0: fp16 output (else fp32); bit1: accumulate into out (else overwrite)            */
@@ -296,6 +298,21 @@ int mms2ut_grad_norm_finalize(const float* part, int nparts, float* ost, const f
 int mms2ut_optim_prepare(float* ost, float lr, float warmup_init_lr, float warmup_updates, float beta1,
                          float beta2, float clip_norm, float scale_window, float min_loss_scale,
                          hipStream_t stream);
+/* CTC loss of a multitask CTC head (fairseq CtcCriterion: F.ctc_loss on log_softmax(logits.float()),
+ * reduction "sum").  logits: fp16 batch-major rows b*T + t, leading dim ld >= V; targets int64
+ * [B, tgt_ld] (first tgt_len[b] used, max_tgt_len = max tgt_len); in_len / tgt_len int32 [B];
+ * work: fp32 scratch of mms2ut_ctc_workspace_floats(B, T, max_tgt_len) elements, kept from fwd to
+ * bwd.  fwd ADDS the summed loss to *loss_sum (zero_infinity: infinite per-utterance losses count
+ * 0).  bwd writes dlogits (ldd >= V, padded rows/columns 0) = grad_scale[0] * d loss / d logits;
+ * impossible alignments get a zero gradient.                                                     */
+int mms2ut_ctc_workspace_floats(int B, int T, int max_tgt_len, int64_t* n);
+int mms2ut_ctc_loss_fwd(const mms2ut_half* logits, int64_t ld, int B, int T, int V, const int64_t* targets,
+                        int64_t tgt_ld, int max_tgt_len, const int* in_len, const int* tgt_len, int blank,
+                        int zero_infinity, float* work, float* loss_sum, hipStream_t stream);
+int mms2ut_ctc_loss_bwd(const mms2ut_half* logits, int64_t ld, int B, int T, int V, const int64_t* targets,
+                        int64_t tgt_ld, int max_tgt_len, const int* in_len, const int* tgt_len, int blank,
+                        const float* work, const float* grad_scale, mms2ut_half* dlogits, int64_t ldd,
+                        hipStream_t stream);
 /* fairseq Trainer._check_grad_norms on device.  stage 0: buf[0..world) = 0 except
  * buf[rank] = ost[MMS_OST_GNORM]; the caller SUM-all-reduces buf; stage 1: ost[MMS_OST_INCONSISTENT]
  * = 1 when the norms are finite and max|n_r - n_0| / (n_0 + 1e-6) >= 1e-6 — optim_prepare then

@@ -10,7 +10,7 @@ Plugin names (same as the reference): task ``multimodal_speech_to_speech``, mode
 ``mm_s2ut_transformer``, criterion ``speech_to_unit`` (aliases ``speech_to_speech``,
 ``speech_to_unit_v2``).
 """
-from . import _lib, data, frontend, generate, kernels, manifest, model, optim, parallel, plugins, runtime, trainer  # noqa: F401
+from . import _lib, data, frontend, generate, kernels, manifest, model, multitask, optim, parallel, plugins, runtime, trainer  # noqa: F401
 from .model import MMS2UTModel, default_cfg, param_specs  # noqa: F401
 from .plugins import REGISTRY  # noqa: F401
 

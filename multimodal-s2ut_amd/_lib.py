@@ -60,7 +60,11 @@ SIGNATURES = {
     "mms2ut_profile_end": (i32, [C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "mms2ut_profile_bytes": (i32, [C.POINTER(C.c_double)]),
     "mms2ut_profile_launches": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, i32]),
+    "mms2ut_profile_shapes": (i32, [C.c_void_p, i32]),
     "mms2ut_grad_norm_check": (i32, [vp, i32, i32, vp, i32, vp]),
+    "mms2ut_ctc_workspace_floats": (i32, [i32, i32, i32, C.POINTER(C.c_int64)]),
+    "mms2ut_ctc_loss_fwd": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp, vp, i32, i32, vp, vp, vp]),
+    "mms2ut_ctc_loss_bwd": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp, vp, i32, vp, vp, vp, i64, vp]),
     "mms2ut_scale_f16": (i32, [vp, i64, f32, vp]),
     "mms2ut_accum_f16_f32": (i32, [vp, vp, i64, vp]),
     "mms2ut_splitk_reduce": (i32, [vp, i32, i64, i32, i32, vp, i64, i32, f32, vp]),

@@ -49,6 +49,8 @@ def main(argv=None):
                  init_scale=float(args.fp16_init_scale), world_size=world, update_freq=args.update_freq)
     start = _restore(args, tr, dev)
     fus = task.multimodal_translation_config
+    if args.synthetic and cfg.get("multitask"):
+        raise SystemExit("mms2ut-train: --multitask-config-yaml needs the on-disk data (text targets per task)")
     if not args.synthetic:
         rc = _train_manifest(args, task, cfg, tr, fus, rank, world, dev, start)
         _save(args, tr, rank)
@@ -149,7 +151,8 @@ def _train_manifest(args, task, cfg, tr, fus, rank, world, dev, start=0):
     ds = M.MultiModalS2SManifest(args.data, args.train_subset, M.UnitDictionary.for_codes(args.target_code_size),
                                  data_cfg=data_cfg, image_feat_path=feat,
                                  max_source_positions=cfg.get("max_source_positions", 6000),
-                                 max_target_positions=cfg.get("max_target_positions", 1024))
+                                 max_target_positions=cfg.get("max_target_positions", 1024),
+                                 multitask=getattr(task, "multitask_tasks", None))
     upd, t0, ntok, epoch = start, time.time(), 0.0, 1
     uf = args.update_freq
     while upd < args.max_update:

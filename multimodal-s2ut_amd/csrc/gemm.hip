@@ -1095,6 +1095,7 @@ struct GemmProfile {
   float* l_ms = nullptr;
   double* l_flops = nullptr;
   int* l_cls = nullptr;
+  int* l_mnk = nullptr;   // M, N, K, batch*splitk per launch
   double flops = 0.0;
   double bytes = 0.0;  // algorithmic HBM bytes: A, B (and aux / accumulated C) read once, C written once
 } g_prof;
@@ -1105,7 +1106,8 @@ extern "C" int mms2ut_profile_begin(int max_launches) {
   MMS_REQUIRE(max_launches > 0, "profile_begin: max_launches must be > 0");
   g_prof.ev = (hipEvent_t*)calloc(2 * (size_t)max_launches, sizeof(hipEvent_t));
   MMS_REQUIRE(g_prof.ev != nullptr, "profile_begin: out of host memory");
-  free(g_prof.l_ms); free(g_prof.l_flops); free(g_prof.l_cls);
+  free(g_prof.l_ms); free(g_prof.l_flops); free(g_prof.l_cls); free(g_prof.l_mnk);
+  g_prof.l_mnk = (int*)calloc(4 * (size_t)max_launches, sizeof(int));
   g_prof.l_ms = (float*)calloc((size_t)max_launches, sizeof(float));
   g_prof.l_flops = (double*)calloc((size_t)max_launches, sizeof(double));
   g_prof.l_cls = (int*)calloc((size_t)max_launches, sizeof(int));
@@ -1155,6 +1157,8 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
     const double nb = a->batch > 0 ? a->batch : 1;
     g_prof.flops += 2.0 * a->M * a->N * a->K * nb;
     g_prof.l_flops[i] = 2.0 * a->M * a->N * a->K * nb;
+    g_prof.l_mnk[4 * i] = a->M; g_prof.l_mnk[4 * i + 1] = a->N; g_prof.l_mnk[4 * i + 2] = a->K;
+    g_prof.l_mnk[4 * i + 3] = (a->batch > 0 ? a->batch : 1) * (a->splitk > 0 ? a->splitk : 1);
     g_prof.l_cls[i] = (a->a_kcontig ? 1 : 0) | (a->b_kcontig ? 2 : 0) | (a->epi << 2) | (nb > 1 ? 256 : 0) |
                       ((a->splitk > 1 ? 1 : 0) << 9);
     const double c_bytes = (double)a->M * a->N * (a->epi == MMS_EPI_F32 ? 4.0 * (a->splitk > 0 ? a->splitk : 1) : 2.0);
@@ -1174,6 +1178,13 @@ extern "C" int mms2ut_profile_launches(float* ms, double* flops, int* cls, int n
     if (flops) flops[i] = g_prof.l_flops[i];
     if (cls) cls[i] = g_prof.l_cls[i];
   }
+  return 0;
+}
+
+extern "C" int mms2ut_profile_shapes(int* mnk, int n) {
+  MMS_REQUIRE(!g_prof.on && g_prof.l_mnk != nullptr, "profile_shapes: no finished profile window");
+  MMS_REQUIRE(n >= 0 && n <= g_prof.n, "profile_shapes: n=%d > %d launches", n, g_prof.n);
+  for (int i = 0; i < 4 * n; ++i) mnk[i] = g_prof.l_mnk[i];
   return 0;
 }
 

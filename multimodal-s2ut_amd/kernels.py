@@ -107,6 +107,15 @@ def gemm_profile_launches(n):
     return ms, fl, cls
 
 
+def gemm_profile_shapes(n):
+    """[n, 4] int32 (M, N, K, batch * splitk) of the last gemm_profile window's launches."""
+    import numpy as np
+    mnk = np.zeros((max(n, 0), 4), np.int32)
+    if n:
+        call("mms2ut_profile_shapes", mnk.ctypes.data, int(n))
+    return mnk
+
+
 def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
            ldc=None, alpha=1.0):
     """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue)."""
@@ -629,6 +638,27 @@ def grad_norm(grad, ost, sample_size=None, nparts=1024):
     part = torch.empty(nparts, dtype=torch.float32, device=grad.device)
     call("mms2ut_grad_sqnorm", grad.data_ptr(), grad.numel(), part.data_ptr(), nparts, _s())
     call("mms2ut_grad_norm_finalize", part.data_ptr(), nparts, ost.data_ptr(), _p(sample_size), _s())
+
+
+def ctc_loss_fwd(logits, B, T, V, targets, in_len32, tgt_len32, max_tgt_len, blank, zero_infinity, loss_sum):
+    """Adds the summed CTC loss to loss_sum (fp32 [1]); returns the workspace for ctc_loss_bwd."""
+    import ctypes
+    n = ctypes.c_int64()
+    call("mms2ut_ctc_workspace_floats", int(B), int(T), int(max_tgt_len), ctypes.byref(n))
+    work = torch.empty(max(n.value, 1), dtype=torch.float32, device=logits.device)
+    assert targets.dtype == torch.int64 and in_len32.dtype == torch.int32 and tgt_len32.dtype == torch.int32
+    call("mms2ut_ctc_loss_fwd", logits.data_ptr(), logits.stride(0), int(B), int(T), int(V), targets.data_ptr(),
+         targets.stride(0), int(max_tgt_len), in_len32.data_ptr(), tgt_len32.data_ptr(), int(blank),
+         int(zero_infinity), work.data_ptr(), loss_sum.data_ptr(), _s())
+    return work
+
+
+def ctc_loss_bwd(logits, B, T, V, targets, in_len32, tgt_len32, max_tgt_len, blank, work, grad_scale, out=None):
+    out = torch.empty_like(logits) if out is None else out
+    call("mms2ut_ctc_loss_bwd", logits.data_ptr(), logits.stride(0), int(B), int(T), int(V), targets.data_ptr(),
+         targets.stride(0), int(max_tgt_len), in_len32.data_ptr(), tgt_len32.data_ptr(), int(blank), work.data_ptr(),
+         grad_scale.data_ptr(), out.data_ptr(), out.stride(0), _s())
+    return out
 
 
 def grad_norm_check(buf, world, rank, ost, stage):

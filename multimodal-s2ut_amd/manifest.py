@@ -165,8 +165,17 @@ class MultiModalS2SManifest:
     """One split of the on-disk corpus (``MultiModalSpeechToSpeechDatasetCreator._from_list``)."""
 
     def __init__(self, root, split, tgt_dict, data_cfg=None, image_feat_path=None, is_train=None,
-                 max_source_positions=6000, max_target_positions=1024):
+                 max_source_positions=6000, max_target_positions=1024, multitask=None):
+        """multitask: {task: (raw config, multitask.Dictionary)} (--multitask-config-yaml): each
+        task's text targets (``{data}/{split}.tsv``) join every collated batch as
+        sample["multitask"] (speech_to_speech_dataset.py:474-521)."""
         self.root, self.split = root, split
+        self.multitask = {}
+        if multitask:
+            from . import multitask as MT
+            for name, (raw, dct) in multitask.items():
+                self.multitask[name] = MT.TextTargetMultitaskData(raw["data"], split, dct,
+                                                                   raw.get("decoder_type", "transformer"))
         self.data_cfg = data_cfg or load_data_config(os.path.join(root, "config.yaml"))
         self.is_train = split.startswith("train") if is_train is None else is_train
         samples = load_samples_from_tsv(root, split)
@@ -252,6 +261,12 @@ class MultiModalS2SManifest:
         sample = D.collater(items)
         by_index = {it["index"]: it for it in items}
         waves = [by_index[int(i)]["wave"] for i in sample["id"].tolist()]
+        if self.multitask:
+            from . import multitask as MT
+            pos = {int(i): k for k, i in enumerate(indices)}
+            order = torch.tensor([pos[int(i)] for i in sample["id"].tolist()], dtype=torch.long)
+            sample["multitask"] = MT.sample_multitask(
+                {n: (d, [d.get(self.ids[int(i)]) for i in indices]) for n, d in self.multitask.items()}, order)
         return sample, waves
 
 

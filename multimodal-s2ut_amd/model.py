@@ -53,6 +53,66 @@ def default_cfg(**over):
     cfg.update(over)
     return cfg
 
+# ============================================================================ decoder specs
+
+
+class DecoderSpec:
+    """One fairseq TransformerDecoder (pre-LN, sinusoidal positions, tied output projection) over
+    the flat parameter buffer: the unit decoder (prefix "decoder") or a multitask auxiliary
+    transformer decoder (prefix "{task}_decoder", fairseq S2STransformerMultitaskModelBase;
+    base_multitask_text_transformer_decoder_arch dims).  kdim: the encoder dim it cross-attends."""
+
+    def __init__(self, prefix, d, H, F, L, V, kdim, dropout, attention_dropout, activation_dropout,
+                 pad=1, no_scale_embedding=False, max_target_positions=3000):
+        self.prefix, self.d, self.H, self.F, self.L, self.V, self.kdim = prefix, d, H, F, L, V, kdim
+        self.pd, self.pa, self.pact = dropout, attention_dropout, activation_dropout
+        self.pad, self.no_scale_embedding, self.max_target_positions = pad, no_scale_embedding, max_target_positions
+
+    @classmethod
+    def main(cls, cfg):
+        return cls("decoder", cfg["decoder_embed_dim"], cfg["decoder_attention_heads"], cfg["decoder_ffn_embed_dim"],
+                   cfg["decoder_layers"], cfg["vocab_size"], cfg["encoder_embed_dim"], cfg["dropout"],
+                   cfg["attention_dropout"], cfg["activation_dropout"], cfg["padding_idx"],
+                   cfg["no_scale_embedding"], cfg["max_target_positions"])
+
+    @classmethod
+    def aux(cls, cfg, t):
+        """A multitask task dict (multitask.task_model_cfg) of decoder_type transformer."""
+        return cls(f"{t['name']}_decoder", t["d"], t["H"], t["F"], t["L"], t["V"], cfg["encoder_embed_dim"],
+                   t["dropout"], t["attention_dropout"], t["activation_dropout"], t["pad"],
+                   t.get("no_scale_embedding", False), t.get("max_target_positions", 1024))
+
+
+def aux_tasks(cfg):
+    return list(cfg.get("multitask") or [])
+
+
+def _decoder_param_specs(S, spec, mha, ln):
+    """Backward-completion order of one decoder: final LN, layers L-1..0, the layer-major
+    cross-attention K/V slab, the (tied) token embedding."""
+    p0, dd, Fd = spec.prefix, spec.d, spec.F
+    ln(f"{p0}.layer_norm", dd)
+    for l in reversed(range(spec.L)):
+        p = f"{p0}.layers.{l}"
+        S.extend([(f"{p}.fc2.weight", (dd, Fd)), (f"{p}.fc2.bias", (dd,)),
+                  (f"{p}.fc1.weight", (Fd, dd)), (f"{p}.fc1.bias", (Fd,))])
+        ln(p + ".final_layer_norm", dd)
+        mha(p + ".encoder_attn", dd, spec.kdim, kv=False)
+        ln(p + ".encoder_attn_layer_norm", dd)
+        mha(p + ".self_attn", dd, dd)
+        ln(p + ".self_attn_layer_norm", dd)
+    # Every layer's cross-attention K/V projection reads the same encoder output, so their
+    # weights sit layer-major in one [L*2*dd, kdim] slab (and biases in one [L*2*dd] vector): one
+    # forward GEMM, one dgrad and one wgrad for all layers.  Their gradients complete after the
+    # whole decoder backward, hence the block's place after the layers.
+    for l in range(spec.L):
+        p = f"{p0}.layers.{l}.encoder_attn"
+        S.extend([(f"{p}.k_proj.weight", (dd, spec.kdim)), (f"{p}.v_proj.weight", (dd, spec.kdim))])
+    for l in range(spec.L):
+        p = f"{p0}.layers.{l}.encoder_attn"
+        S.extend([(f"{p}.k_proj.bias", (dd,)), (f"{p}.v_proj.bias", (dd,))])
+    S.append((f"{p0}.embed_tokens.weight", (spec.V, dd)))
+
 # ============================================================================ parameter layout
 
 
@@ -78,27 +138,18 @@ def param_specs(cfg):
     def ln(p, n):
         S.extend([(f"{p}.weight", (n,)), (f"{p}.bias", (n,))])
 
-    ln("decoder.layer_norm", dd)
-    for l in reversed(range(cfg["decoder_layers"])):
-        p = f"decoder.layers.{l}"
-        S.extend([(f"{p}.fc2.weight", (dd, Fd)), (f"{p}.fc2.bias", (dd,)),
-                  (f"{p}.fc1.weight", (Fd, dd)), (f"{p}.fc1.bias", (Fd,))])
-        ln(p + ".final_layer_norm", dd)
-        mha(p + ".encoder_attn", dd, d, kv=False)
-        ln(p + ".encoder_attn_layer_norm", dd)
-        mha(p + ".self_attn", dd, dd)
-        ln(p + ".self_attn_layer_norm", dd)
-    # Every decoder layer's cross-attention K/V projection reads the same encoder output, so their
-    # weights sit layer-major in one [L_d*2*dd, d] slab (and biases in one [L_d*2*dd] vector): one
-    # forward GEMM, one dgrad and one wgrad for all layers.  Their gradients complete after the whole
-    # decoder backward, hence the block's place after the decoder layers.
-    for l in range(cfg["decoder_layers"]):
-        p = f"decoder.layers.{l}.encoder_attn"
-        S.extend([(f"{p}.k_proj.weight", (dd, d)), (f"{p}.v_proj.weight", (dd, d))])
-    for l in range(cfg["decoder_layers"]):
-        p = f"decoder.layers.{l}.encoder_attn"
-        S.extend([(f"{p}.k_proj.bias", (dd,)), (f"{p}.v_proj.bias", (dd,))])
-    S.append(("decoder.embed_tokens.weight", (V, dd)))
+    tasks = aux_tasks(cfg)
+    # multitask heads on the unit decoder's inner states complete their backward first, then the
+    # unit decoder, then the heads on encoder states, then the encoder (runtime._ModelFn.backward)
+    for t in tasks:
+        if t["type"] == "ctc" and t["input_from"] == "decoder":
+            S.extend([(f"{t['name']}_decoder.proj.weight", (t["V"], dd)), (f"{t['name']}_decoder.proj.bias", (t["V"],))])
+    _decoder_param_specs(S, DecoderSpec.main(cfg), mha, ln)
+    for t in tasks:
+        if t["type"] == "transformer":
+            _decoder_param_specs(S, DecoderSpec.aux(cfg, t), mha, ln)
+        elif t["input_from"] == "encoder":
+            S.extend([(f"{t['name']}_decoder.proj.weight", (t["V"], d)), (f"{t['name']}_decoder.proj.bias", (t["V"],))])
     if cfg["fusion"]:
         Di = cfg["image_feat_dim"]
         S.extend([("encoder.gate_denses.0.weight", (d, 2 * d)), ("encoder.gate_denses.0.bias", (d,))])
@@ -185,6 +236,9 @@ class ParamStore:
             return f"dec{m.group(1)}"
         if name.startswith("decoder.embed_tokens"):
             return "dec_emb"
+        m = re.match(r"(\w+)_decoder\.", name)
+        if m:
+            return f"aux_{m.group(1)}"     # a multitask head (one contiguous group per task)
         return "dec_ln"
 
     def _forward_groups(self):
@@ -362,6 +416,9 @@ class MMS2UTModel:
         d, dd = cfg["encoder_embed_dim"], cfg["decoder_embed_dim"]
         self.enc_pos = sinusoidal_table(cfg["max_source_positions"] + 2, d).to(self.device, F16)
         self.dec_pos = sinusoidal_table(cfg["max_target_positions"] + 2, dd).to(self.device, F16)
+        self.dspec = DecoderSpec.main(cfg)
+        self.aux_specs = {t["name"]: DecoderSpec.aux(cfg, t) for t in aux_tasks(cfg) if t["type"] == "transformer"}
+        self._pos = {}   # sinusoidal tables of other widths (multitask decoders)
         self.np_rng = np.random  # modality-dropout draws use the global numpy stream (reference)
         # autograd anchor: the model's output is connected to the graph through this leaf
         self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
@@ -381,11 +438,12 @@ class MMS2UTModel:
 
         for l in range(cfg["encoder_layers"]):
             layer(f"encoder.transformer_layers.{l}", d)
-        for l in range(cfg["decoder_layers"]):
-            p = f"decoder.layers.{l}"
-            layer(p, dd)
-            mats.extend([P(p + ".encoder_attn.out_proj.weight"), P(p + ".encoder_attn.q_proj.weight")])
-        mats.append(self.cross_kv()[0])
+        for sp in [self.dspec] + list(self.aux_specs.values()):
+            for l in range(sp.L):
+                p = f"{sp.prefix}.layers.{l}"
+                layer(p, sp.d)
+                mats.extend([P(p + ".encoder_attn.out_proj.weight"), P(p + ".encoder_attn.q_proj.weight")])
+            mats.append(self.cross_kv(spec=sp)[0])
         for i in range(1, len(cfg["conv_kernel_sizes"])):
             W = P(f"encoder.subsample.conv_layers.{i}.weight")
             mats.append(W.view(W.shape[0], -1))
@@ -429,7 +487,7 @@ class MMS2UTModel:
                 t = torch.ones(shape)
             elif name.endswith(".bias") and ("layer_norm" in name or "out_proj" in name or "image_pre_norm" in name):
                 t = torch.zeros(shape)
-            elif name == "decoder.embed_tokens.weight":
+            elif name.endswith("embed_tokens.weight"):
                 t = torch.randn(shape, generator=g) * shape[1] ** -0.5
                 t[self.cfg["padding_idx"]] = 0
             elif len(shape) >= 2:
@@ -469,10 +527,11 @@ class MMS2UTModel:
             off, _, n = self.params.offsets[last_param]
             self.grad_ready_hook(off + n)
 
-    def cross_kv(self, grad=False):
+    def cross_kv(self, grad=False, spec=None):
         """(W [L_d*2d, de], b [L_d*2d]) of all decoder layers' cross-attention K/V projections."""
-        L = self.cfg["decoder_layers"]
-        f, t = "decoder.layers.0.encoder_attn", f"decoder.layers.{L - 1}.encoder_attn"
+        spec = spec or self.dspec
+        L = spec.L
+        f, t = f"{spec.prefix}.layers.0.encoder_attn", f"{spec.prefix}.layers.{L - 1}.encoder_attn"
         W = self.params.span(f + ".k_proj.weight", t + ".v_proj.weight", grad=grad)
         b = self.params.span(f + ".k_proj.bias", t + ".v_proj.bias", grad=grad)
         return W.view(b.numel(), -1), b
@@ -490,6 +549,12 @@ class MMS2UTModel:
         return self.drop.take(n) if p > 0 else None
 
     def _ensure_pos(self, T, which):
+        if isinstance(which, int):       # a decoder width other than the unit decoder's
+            tab = self._pos.get(which)
+            if tab is None or T + 2 > tab.shape[0]:
+                tab = sinusoidal_table(max(T + 2, 1026), which).to(self.device, F16)
+                self._pos[which] = tab
+            return tab
         tab = self.enc_pos if which == "enc" else self.dec_pos
         if T + 2 > tab.shape[0]:
             dim = tab.shape[1]
@@ -822,13 +887,16 @@ class MMS2UTModel:
         return dtext_total
 
     # -------------------------------------------------------------- decoder layer
-    def dec_layer_fwd(self, l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None):
-        cfg = self.cfg
-        p = f"decoder.layers.{l}"
-        d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
+    def _sp(self, p):
+        return p if self.training else 0.0
+
+    def dec_layer_fwd(self, l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None, spec=None):
+        spec = spec or self.dspec
+        p = f"{spec.prefix}.layers.{l}"
+        d, H = spec.d, spec.H
         hd = d // H
         R = B * Tt
-        pd, pa, pact = self._p("dropout"), self._p("attention_dropout"), self._p("activation_dropout")
+        pd, pa, pact = self._sp(spec.pd), self._sp(spec.pa), self._sp(spec.pact)
         c = {"x": x, "B": B, "Tt": Tt, "Te": Te, "pd": pd, "pa": pa, "pact": pact}
         # self attention (causal + target padding)
         h1, c["m1"], c["r1"] = K.layernorm(x, self.P(p + ".self_attn_layer_norm.weight"), self.P(p + ".self_attn_layer_norm.bias"))
@@ -868,7 +936,7 @@ class MMS2UTModel:
         # FFN
         h3, c["m3"], c["r3"] = K.layernorm(x3, self.P(p + ".final_layer_norm.weight"), self.P(p + ".final_layer_norm.bias"))
         c["h3"] = h3
-        c["drop_act"] = self._drop(pact, R * cfg["decoder_ffn_embed_dim"])
+        c["drop_act"] = self._drop(pact, R * spec.F)
         f1 = K.linear(h3, self.P(p + ".fc1.weight"), self.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP, p=pact,
                       drop=c["drop_act"])
         c["f1"] = f1
@@ -877,13 +945,13 @@ class MMS2UTModel:
                       p=pd, drop=c["drop3"])
         return x4, c
 
-    def dec_layer_bwd(self, l, c, dx4, dkv_all, dy3=None, emit=None):
+    def dec_layer_bwd(self, l, c, dx4, dkv_all, dy3=None, emit=None, spec=None):
         """Returns (dx, masked dx for the layer below or None); writes this layer's cross-attention
         K/V gradient into its columns of dkv_all [B*Te, L_d*2d] (the K/V projection's dgrad and
         wgrad run once for all layers, decoder_backward).  dy3/emit as enc_layer_bwd's dy2/emit."""
-        cfg = self.cfg
-        p = f"decoder.layers.{l}"
-        d, H = cfg["decoder_embed_dim"], cfg["decoder_attention_heads"]
+        spec = spec or self.dspec
+        p = f"{spec.prefix}.layers.{l}"
+        d, H = spec.d, spec.H
         hd = d // H
         B, Tt, Te = c["B"], c["Tt"], c["Te"]
         pd, pa, pact = c["pd"], c["pa"], c["pact"]
@@ -990,75 +1058,117 @@ class MMS2UTModel:
         ctx["B"], ctx["Te"] = B, Te
         return out, lens32, Te, ctx
 
-    def encoder_backward(self, ctx, denc):
+    def encoder_backward(self, ctx, denc, dstates=None):
+        """dstates: {l: gradient of encoder_states[l]} (layer l's output, fairseq's
+        ``encoder_states`` with return_all_hiddens) from multitask heads."""
+        dstates = dstates or {}
         if ctx["fusion"] is not None:
             denc = self.fusion_bwd(ctx["fusion"], denc)
         last_fusion = [n for n, _ in self.params.specs if n.startswith(("encoder.gate", "encoder.multimodal",
                                                                          "encoder.selective", "encoder.image"))]
         if last_fusion:
             self._ready(last_fusion[-1])
-        if ctx.get("audio_dropped"):
+        if ctx.get("audio_dropped") and not dstates:
             # the reference replaces encoder_out by zeros_like(..., requires_grad=False)
             # (mm_s2s_transformer.py:500): no gradient reaches the encoder, whose gradients stay
             # at the step's zeros -- skip its whole backward, only flush the reducer
             ctx["layers"] = None
             self._ready(None)
             return
+        if ctx.get("audio_dropped"):
+            denc = torch.zeros_like(denc)   # only the multitask heads' state gradients remain
         layers = ctx["layers"]
         L = self.cfg["encoder_layers"]
         emit = lambda l: (layers[l]["pd"], layers[l]["drop2"]) if l >= 0 else None  # noqa: E731
-        dx, dmask = K.layernorm_bwd(denc, ctx["lx"], self.P("encoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
-                                    self.params.span("encoder.layer_norm.weight", "encoder.layer_norm.bias", grad=True),
-                                    emit=emit(L - 1))
+        gln = self.params.span("encoder.layer_norm.weight", "encoder.layer_norm.bias", grad=True)
+        if (L - 1) in dstates:     # encoder_states[L-1] = the final LayerNorm's input
+            dx = K.layernorm_bwd(denc, ctx["lx"], self.P("encoder.layer_norm.weight"), ctx["lm"], ctx["lr"], gln,
+                                 dres=dstates[L - 1])
+            dmask = None
+        else:
+            dx, dmask = K.layernorm_bwd(denc, ctx["lx"], self.P("encoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
+                                        gln, emit=emit(L - 1))
         self._ready("encoder.layer_norm.bias")
         for l in reversed(range(L)):
-            dx, dmask = self.enc_layer_bwd(l, layers[l], dx, dy2=dmask, emit=emit(l - 1))
+            em = None if (l - 1) in dstates else emit(l - 1)
+            dx, dmask = self.enc_layer_bwd(l, layers[l], dx, dy2=dmask, emit=em)
             layers[l] = None
+            if (l - 1) in dstates:      # encoder_states[l-1] = this layer's input
+                dx = K.add_f16(dx, dstates[l - 1])
+                dmask = None
             self._ready(f"encoder.transformer_layers.{l}.self_attn_layer_norm.bias")
         scale, pd = ctx["emb"]
         dh = K.scale_dropout_bwd(dx, scale, pd, ctx["drop_emb"])
         self.subsample_bwd(ctx["sub"], dh)
         self._ready(None)
 
-    def decoder_forward(self, batch, enc, enc_len32, Te):
-        cfg = self.cfg
-        d, V, pad = cfg["decoder_embed_dim"], cfg["vocab_size"], cfg["padding_idx"]
+    def decoder_forward(self, batch, enc, enc_len32, Te, spec=None):
+        """fairseq TransformerDecoder (pre-LN, tied output projection) of `spec` (the unit decoder
+        by default).  batch: .prev [B, Tt] int64, .tgt_mask, .tgt_len32 (runtime.prepare_batch /
+        decoder_batch).  Returns (padded logits [B*Tt, round64(V)], ctx)."""
+        spec = spec or self.dspec
+        d, V, pad = spec.d, spec.V, spec.pad
         tok = batch.prev
         B, Tt = tok.shape
-        ctx = {"B": B, "Tt": Tt}
-        pos = self._ensure_pos(Tt, "dec")
-        scale = 1.0 if cfg["no_scale_embedding"] else math.sqrt(d)
-        pd = self._p("dropout")
+        ctx = {"B": B, "Tt": Tt, "spec": spec}
+        main = spec is self.dspec
+        pos = self._ensure_pos(Tt, "dec" if main else d)
+        scale = 1.0 if spec.no_scale_embedding else math.sqrt(d)
+        pd = self._sp(spec.pd)
         ctx["drop_emb"] = self._drop(pd, B * Tt * d)
         ctx["tok"] = tok
-        self.params.await_group("dec_emb")
-        x = K.token_embed(tok, self.P("decoder.embed_tokens.weight"), pos, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
+        self.params.await_group("dec_emb" if main else f"aux_{spec.prefix[:-len('_decoder')]}")
+        x = K.token_embed(tok, self.P(f"{spec.prefix}.embed_tokens.weight"), pos, B, Tt, d, pad, scale, pd,
+                          ctx["drop_emb"])
         ctx["emb"] = (scale, pd)
         tgt_mask = batch.tgt_mask  # uint8 [B, round8(Tt)] or None (no target padding in the batch)
         ctx["layers"] = []
-        self.params.await_group("cross_kv")
-        Wkv, bkv = self.cross_kv()
+        if main:
+            self.params.await_group("cross_kv")
+        Wkv, bkv = self.cross_kv(spec=spec)
         kv_all = K.linear(enc, Wkv, bkv)   # [B*Te, L_d*2d]: every layer's cross-attention K | V
         ctx["kv_all"] = kv_all
-        for l in range(cfg["decoder_layers"]):
-            self.params.await_group(f"dec{l}")
-            x, c = self.dec_layer_fwd(l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, batch.tgt_len32)
+        for l in range(spec.L):
+            if main:
+                self.params.await_group(f"dec{l}")
+            x, c = self.dec_layer_fwd(l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, batch.tgt_len32, spec=spec)
             ctx["layers"].append(c)
-        self.params.await_all()   # "dec_ln" and anything not consumed above
-        xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("decoder.layer_norm.weight"), self.P("decoder.layer_norm.bias"))
+        if main:
+            self.params.await_all()   # "dec_ln" and anything not consumed above
+        xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P(f"{spec.prefix}.layer_norm.weight"),
+                                               self.P(f"{spec.prefix}.layer_norm.bias"))
         ctx["lx"], ctx["xl"] = x, xl
         Vp = round_up(V, 64)  # whole k-tiles for the tied-embedding dgrad (pad columns of dlogits are 0)
         logits = torch.empty(B * Tt, Vp, dtype=F16, device=x.device)
-        E = self.P("decoder.embed_tokens.weight")
+        E = self.P(f"{spec.prefix}.embed_tokens.weight")
         K.gemm(xl, E, logits, B * Tt, V, d, lda=d, ldb=d, ldc=Vp)
         ctx["Vp"] = Vp
         return logits, ctx
 
-    def decoder_backward(self, ctx, dlogits, enc, denc):
-        cfg = self.cfg
-        d, V, pad = cfg["decoder_embed_dim"], cfg["vocab_size"], cfg["padding_idx"]
+    @staticmethod
+    def encoder_states(ctx):
+        """fairseq ``encoder_states`` (return_all_hiddens) as batch-major [B*Te, d] buffers: every
+        encoder layer's output (the last = the final LayerNorm's input)."""
+        layers = ctx["layers"]
+        return [layers[l + 1]["x"] for l in range(len(layers) - 1)] + ([ctx["lx"]] if layers else [])
+
+    @staticmethod
+    def inner_states(ctx):
+        """fairseq TransformerDecoder ``inner_states`` as batch-major [B*Tt, d] buffers: the
+        embedding output (after dropout), then every layer's output (the last = the final
+        LayerNorm's input)."""
+        return [c["x"] for c in ctx["layers"]] + [ctx["lx"]]
+
+    def decoder_backward(self, ctx, dlogits, enc, denc, dinner=None, denc_accumulate=False):
+        """Hand-written backward of decoder_forward.  denc [B*Te, de] receives the encoder-output
+        gradient (added to its contents with denc_accumulate).  dinner: {j: gradient of
+        inner_states[j]} from multitask heads reading the decoder's hidden states."""
+        spec = ctx["spec"]
+        main = spec is self.dspec
+        d, V, pad = spec.d, spec.V, spec.pad
         B, Tt = ctx["B"], ctx["Tt"]
-        E = self.P("decoder.embed_tokens.weight")
+        dinner = dinner or {}
+        E = self.P(f"{spec.prefix}.embed_tokens.weight")
         dE32 = torch.zeros(V, d, dtype=torch.float32, device=E.device)
         # tied output projection: dE += dlogits^T xl ; dxl = dlogits E.  Both halves of the tied
         # embedding gradient (this wgrad and the token scatter below) run on the side stream, in
@@ -1068,35 +1178,45 @@ class MMS2UTModel:
         # dxl = dlogits E over K = Vp: E zero-padded to Vp rows (refreshed per step), so the GEMM
         # runs on the LDS-DMA path (K % 64 == 0) instead of the predicated one
         Vp = ctx["Vp"]
-        Ep = self._wpad.get("embed")
+        key = ("embed", spec.prefix)
+        Ep = self._wpad.get(key)
         if Ep is None or Ep.shape != (Vp, d):
             Ep = torch.zeros(Vp, d, dtype=F16, device=E.device)
-            self._wpad["embed"] = Ep
+            self._wpad[key] = Ep
         K.copy2d(E, Ep, V, d)
         K.gemm(dlogits, Ep, dxl, B * Tt, d, Vp, a_kc=True, b_kc=False, lda=Vp, ldb=d, ldc=d)
         layers = ctx["layers"]
-        L = cfg["decoder_layers"]
+        L = spec.L
         emit = lambda l: (layers[l]["pd"], layers[l]["drop3"]) if l >= 0 else None  # noqa: E731
-        dx, dmask = K.layernorm_bwd(dxl, ctx["lx"], self.P("decoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
-                                    self.params.span("decoder.layer_norm.weight", "decoder.layer_norm.bias", grad=True),
-                                    emit=emit(L - 1))
-        self._ready("decoder.layer_norm.bias")
+        gln = self.params.span(f"{spec.prefix}.layer_norm.weight", f"{spec.prefix}.layer_norm.bias", grad=True)
+        if L in dinner:      # inner_states[L] = the final LayerNorm's input
+            dx = K.layernorm_bwd(dxl, ctx["lx"], self.P(f"{spec.prefix}.layer_norm.weight"), ctx["lm"], ctx["lr"],
+                                 gln, dres=dinner[L])
+            dmask = None
+        else:
+            dx, dmask = K.layernorm_bwd(dxl, ctx["lx"], self.P(f"{spec.prefix}.layer_norm.weight"), ctx["lm"],
+                                        ctx["lr"], gln, emit=emit(L - 1))
+        self._ready(f"{spec.prefix}.layer_norm.bias")
         dkv_all = torch.empty_like(ctx["kv_all"])
         for l in reversed(range(L)):
-            dx, dmask = self.dec_layer_bwd(l, layers[l], dx, dkv_all, dy3=dmask, emit=emit(l - 1))
+            em = None if l in dinner else emit(l - 1)     # inner_states[l] = this layer's input
+            dx, dmask = self.dec_layer_bwd(l, layers[l], dx, dkv_all, dy3=dmask, emit=em, spec=spec)
             layers[l] = None
-            self._ready(f"decoder.layers.{l}.self_attn_layer_norm.bias")
+            if l in dinner:
+                dx = K.add_f16(dx, dinner[l])
+                dmask = None      # the layer below recomputes its masked gradient from dx
+            self._ready(f"{spec.prefix}.layers.{l}.self_attn_layer_norm.bias")
         # cross-attention K/V projections of all layers: one wgrad (+ bias) and one dgrad (K = L_d*2d)
-        Wkv, _ = self.cross_kv()
-        gWkv, gbkv = self.cross_kv(grad=True)
+        Wkv, _ = self.cross_kv(spec=spec)
+        gWkv, gbkv = self.cross_kv(grad=True, spec=spec)
         K.linear_wgrad(dkv_all, enc, gWkv, db=gbkv)
-        K.linear_dgrad(dkv_all, Wkv, out=denc)   # the encoder output's only gradient source
+        K.linear_dgrad(dkv_all, Wkv, out=denc, accumulate=denc_accumulate)   # the encoder output's gradient
         del dkv_all
-        self._ready(f"decoder.layers.{L - 1}.encoder_attn.v_proj.bias")
+        self._ready(f"{spec.prefix}.layers.{L - 1}.encoder_attn.v_proj.bias")
         scale, pd = ctx["emb"]
-        gE = self.G("decoder.embed_tokens.weight")
+        gE = self.G(f"{spec.prefix}.embed_tokens.weight")
         with (K.side_begin(dx, ctx["tok"], dE32) or K._NULLCTX):
             K.token_embed_bwd(ctx["tok"], dx, dE32, B, Tt, d, pad, scale, pd, ctx["drop_emb"])
             K.call("mms2ut_splitk_reduce", dE32.data_ptr(), 1, dE32.numel(), V, d, gE.data_ptr(), d, 1, 1.0,
                    K._s())
-        self._ready("decoder.embed_tokens.weight")
+        self._ready(f"{spec.prefix}.embed_tokens.weight")

@@ -186,6 +186,17 @@ class MultiModalSpeechToSpeechTask:
         code_size = getattr(args, "target_code_size", None) or 1000
         self.vocab_size = code_size + 4  # <s> <pad> </s> <unk> + units (fairseq Dictionary)
         self.padding_idx, self.eos = 1, 2
+        # fairseq SpeechToSpeechTask: --multitask-config-yaml -> one auxiliary task per entry
+        # (dictionary + text targets), SURVEY §8f row 3 (multitask.py)
+        self.multitask_tasks = {}
+        if getattr(args, "multitask_config_yaml", None):
+            from . import multitask as MT
+            path = args.multitask_config_yaml
+            if not os.path.isabs(path) and getattr(args, "data", None):
+                path = os.path.join(args.data, path)
+            for name, raw in MT.load_multitask_config(path).items():
+                dct = MT.Dictionary.load(raw["dict"])
+                self.multitask_tasks[name] = (raw, dct)
 
     @classmethod
     def setup_task(cls, args, **kw):
@@ -193,6 +204,16 @@ class MultiModalSpeechToSpeechTask:
 
     def build_model(self, args, device="cuda"):
         return MM_S2UTTransformerModel.build_model(args, self, device=device)
+
+    def multitask_model_cfg(self, cfg):
+        """Model-side configs of the tasks with a non-zero loss weight (fairseq skips the others)."""
+        from . import multitask as MT
+        out = []
+        for name, (raw, dct) in self.multitask_tasks.items():
+            t = MT.task_model_cfg(name, raw, dct, cfg)
+            if t["weight"] != 0:
+                out.append(t)
+        return out
 
     def build_criterion(self, args):
         return SpeechToUnitCriterion(self, getattr(args, "label_smoothing", 0.2))
@@ -395,6 +416,8 @@ class MM_S2UTTransformerModel:
     @classmethod
     def build_model(cls, args, task, device="cuda"):
         cfg = cfg_from_args(args, task.multimodal_translation_config, task.vocab_size)
+        if getattr(task, "multitask_tasks", None):
+            cfg["multitask"] = task.multitask_model_cfg(cfg)
         return cls(cfg, device=device, seed=getattr(args, "seed", 1))
 
     def train(self, mode=True):
@@ -417,13 +440,19 @@ class MM_S2UTTransformerModel:
     def max_decoder_positions(self):
         return self.cfg["max_target_positions"]
 
-    def _batch(self, src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target=None):
+    def _batch(self, src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target=None,
+               multitask=None):
         sample = {"net_input": {"src_tokens": src_tokens, "src_lengths": src_lengths,
                                 "prev_output_tokens": prev_output_tokens, "imgs_list": list(imgs_list or []),
                                 "img_masks_list": list(img_masks_list or [])},
                   "target": target if target is not None else prev_output_tokens,
                   "ntokens": int(prev_output_tokens.ne(self.cfg["padding_idx"]).sum())}
-        return runtime.prepare_batch(sample, self.cfg, self.net.device)
+        cfg = self.cfg
+        if multitask is not None:
+            sample["multitask"] = multitask
+        elif cfg.get("multitask"):
+            cfg = dict(cfg, multitask=None)    # inference / no multitask targets: heads unused
+        return runtime.prepare_batch(sample, cfg, self.net.device)
 
     def forward_encoder(self, src_tokens, src_lengths, src_audio_path=None, img_path=None, img_tensor=None,
                         imgs_list=(), img_masks_list=(), tgt_speaker=None, return_all_hiddens=False, **kw):
@@ -450,25 +479,26 @@ class MM_S2UTTransformerModel:
 
     def forward(self, src_tokens, src_lengths, prev_output_tokens, src_audio_path=None, img_path=None,
                 img_tensor=None, imgs_list=(), img_masks_list=(), tgt_speaker=None,
-                return_all_hiddens=False, target=None, **kwargs):
+                return_all_hiddens=False, target=None, multitask=None, **kwargs):
         """Reference signature (mm_s2s_transformer.py:667-680) -> (logits [B, Tt, V], extra).
         The logits are autograd-connected to the hand-written backward.  return_all_hiddens adds
         ``encoder_states`` (L_e layer outputs, [Te, B, C]) and ``encoder_padding_mask`` to extra
         as the reference does (:697-699)."""
         if tgt_speaker is not None:
             raise NotImplementedError("target speaker embeddings (spk_emb_proj) are out of scope")
-        batch = self._batch(src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target)
+        batch = self._batch(src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target,
+                            multitask)
         stash = {}
         if return_all_hiddens:
             self.net.encoder_hook = stash.__setitem__
         try:
-            logits = runtime.model_logits(self.net, batch)
+            logits, aux = runtime.model_outputs(self.net, batch)
         finally:
             self.net.encoder_hook = None
         B, Tt = prev_output_tokens.shape
         V = self.cfg["vocab_size"]
         out = logits.view(B, Tt, -1)[:, :, :V]
-        extra = {"attn": [None], "inner_states": None, "_batch": batch, "_logits_padded": logits}
+        extra = {"attn": [None], "inner_states": None, "_batch": batch, "_logits_padded": logits, "_aux_loss": aux}
         if return_all_hiddens:
             eo = encoder_out_dict(self.net, stash["enc"], batch.enc_len32, batch.Te, stash["ctx"], True)
             extra["encoder_states"] = eo["encoder_states"]
@@ -495,13 +525,20 @@ class SpeechToUnitCriterion:
 
     def forward(self, model, sample, reduce=True):
         ni = dict(sample["net_input"])
-        _, extra = model(**ni, target=sample["target"])
+        _, extra = model(**ni, target=sample["target"], multitask=sample.get("multitask"))
         batch, logits = extra["_batch"], extra["_logits_padded"]
         loss, nll = runtime.label_smoothed_ce(logits, batch.target, model.cfg["vocab_size"], self.eps,
                                               self.padding_idx)
         sample_size = sample["target"].size(0) if self.sentence_avg else sample["ntokens"]
         logging_output = {"loss": loss.detach(), "nll_loss": nll.detach(), "ntokens": sample["ntokens"],
                           "nsentences": sample["target"].size(0), "sample_size": sample_size}
+        if model.cfg.get("multitask"):
+            # fairseq SpeechToUnitMultitaskTaskCriterion: loss += sum_t weight_t * loss_t; the logged
+            # "loss" is the main one, the heads are logged under "multitask"
+            loss = loss + extra["_aux_loss"]
+            logging_output["multitask"] = {k: {"loss": v.detach(), "loss_weight": w}
+                                           for (k, v), w in zip(model.net.last_aux_losses.items(),
+                                                                [t["weight"] for t in model.cfg["multitask"]])}
         return loss, sample_size, logging_output
 
     @staticmethod

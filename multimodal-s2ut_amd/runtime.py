@@ -30,6 +30,8 @@ class DeviceBatch:
     ntokens: int
     nsentences: int
     n_src_frames: int                 # sum of src lengths (the benchmark's unit of work)
+    tgt_lengths32: Optional[torch.Tensor] = None   # [B] int32 (device) target lengths (multitask CTC on decoder states)
+    mt: Optional[dict] = None         # {task: multitask.MTBatch} (--multitask-config-yaml)
 
 
 def subsampled_lengths(lengths, n_layers=2):
@@ -69,7 +71,18 @@ def prepare_batch(sample, cfg, device="cuda", src_override=None):
             km = torch.zeros(B, round_up(Ti + 1, 8), dtype=torch.uint8)
             km[:, :Ti] = masks[0].cpu().to(torch.uint8)
             img_keymask = km.to(dev, non_blocking=True)
+    tasks = [t for t in (cfg.get("multitask") or []) if t["weight"] != 0]
+    mt = None
+    if tasks:
+        from . import multitask as MT
+        if "multitask" not in sample:
+            raise ValueError("the model has multitask heads but the sample carries no 'multitask' targets")
+        mt = MT.prepare_multitask(sample["multitask"], tasks, dev)
+    tl = sample.get("target_lengths")
+    if tl is None:
+        tl = (~prev_cpu.eq(cfg["padding_idx"])).sum(1)
     return DeviceBatch(
+        tgt_lengths32=tl.to(torch.int32).to(dev, non_blocking=True), mt=mt,
         src=src.contiguous(), src_lengths=torch.as_tensor(lens), Te=Te,
         enc_len32=torch.from_numpy(enc_len).to(dev, non_blocking=True),
         prev=prev_cpu.to(dev, non_blocking=True).contiguous(), tgt_mask=tgt_mask, tgt_len32=tgt_len32,
@@ -110,34 +123,56 @@ def decoder_batch(prev_output_tokens, cfg):
 
 
 class _ModelFn(torch.autograd.Function):
+    """Outputs (padded logits, weighted multitask loss fp32 [1]); the backward is hand-written:
+    multitask heads on decoder states -> unit decoder -> heads on encoder states -> encoder."""
+
     @staticmethod
     def forward(fctx, anchor, model, batch):
+        from . import multitask as MT
         enc, len32, Te, ectx = model.encoder_forward(batch)
         if getattr(model, "encoder_hook", None) is not None:   # return_all_hiddens (plugins.py)
             model.encoder_hook("enc", enc)
             model.encoder_hook("ctx", ectx)
         logits, dctx = model.decoder_forward(batch, enc, len32, Te)
+        aux, actx, alog = MT.aux_forward(model, batch, ectx, dctx, len32, Te)
+        model.last_aux_losses = alog
         fctx.model = model
-        fctx.saved = (ectx, dctx, enc, batch)
-        return logits
+        fctx.saved = (ectx, dctx, enc, batch, actx, Te)
+        if aux is None:
+            aux = torch.zeros(1, dtype=torch.float32, device=logits.device)
+        return logits, aux.reshape(())
 
     @staticmethod
-    def backward(fctx, dlogits):
+    def backward(fctx, dlogits, daux):
+        from . import multitask as MT
         model = fctx.model
-        ectx, dctx, enc, batch = fctx.saved
+        ectx, dctx, enc, batch, actx, Te = fctx.saved
         fctx.saved = None
         d = model.cfg["encoder_embed_dim"]
         denc = torch.empty(enc.shape[0], d, dtype=F16, device=enc.device)  # written by decoder_backward
-        model.decoder_backward(dctx, dlogits.contiguous(), enc, denc)
+        use_aux = bool(actx) and daux is not None
+        if use_aux:
+            daux = daux.reshape(1).to(torch.float32).contiguous()
+        dinner = MT.aux_backward_decoder_heads(model, actx, daux) if use_aux else None
+        if dlogits is None:    # only the multitask losses were differentiated
+            dlogits = torch.zeros(dctx["B"] * dctx["Tt"], dctx["Vp"], dtype=F16, device=enc.device)
+        model.decoder_backward(dctx, dlogits.contiguous(), enc, denc, dinner=dinner)
         del dctx
-        model.encoder_backward(ectx, denc)
+        dstates = MT.aux_backward_encoder_heads(model, actx, daux, batch.prev.shape[0], Te) if use_aux else None
+        model.encoder_backward(ectx, denc, dstates)
         K.side_join()  # weight gradients (side stream) complete before anyone reads them
         return None, None, None
 
 
+def model_outputs(model, batch):
+    """(padded logits [B*Tt, round64(V)] fp16, weighted multitask loss fp32 0-dim) — both
+    autograd-connected through the hand-written backward."""
+    return _ModelFn.apply(model.anchor, model, batch)
+
+
 def model_logits(model, batch):
     """Padded logits [B*Tt, round64(V)] fp16 (autograd-connected through the hand-written bwd)."""
-    return _ModelFn.apply(model.anchor, model, batch)
+    return _ModelFn.apply(model.anchor, model, batch)[0]
 
 
 class _LSXentFn(torch.autograd.Function):

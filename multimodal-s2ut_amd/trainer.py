@@ -92,7 +92,7 @@ class Trainer:
                 self.reducer.reset()
                 self.reducer.acc = self.acc if n > 1 else None
                 m.grad_ready_hook = self.reducer.ready
-            logits = runtime.model_logits(m, batch)
+            logits, aux = runtime.model_outputs(m, batch)
             # zeroed after the forward: by then every deferred optimizer chunk of the previous step
             # (which reads the gradients) has been waited for (ParamStore.await_group).  Every
             # micro-batch starts from zero (a backward writes, not adds, most of its gradients).
@@ -103,7 +103,9 @@ class Trainer:
             loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
                                                   cfg["label_smoothing"], cfg["padding_idx"])
             del logits
-            loss.backward(self.opt.loss_scale())
+            # multitask heads: loss + sum_t weight_t * loss_t (fairseq MultitaskCriterion); the
+            # logged loss stays the main one (fairseq logs multitask losses separately)
+            (loss + aux if m.cfg.get("multitask") else loss).backward(self.opt.loss_scale())
             m.grad_ready_hook = None
             if n > 1:
                 if i == 0:
@@ -131,7 +133,7 @@ class Trainer:
         m = self.model
         m.eval()
         with torch.no_grad():
-            logits = runtime.model_logits(m, batch)
+            logits, aux = runtime.model_outputs(m, batch)
             loss, nll = runtime.label_smoothed_ce(logits, batch.target, self.cfg["vocab_size"],
                                                   self.cfg["label_smoothing"], self.cfg["padding_idx"])
         m.train()

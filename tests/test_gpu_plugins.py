@@ -253,3 +253,43 @@ def test_cli_save_dir_checkpoint_and_restore(tmp_path, capsys):
     assert recs[-1]["num_updates"] == 4
     ck2 = torch.load(sd / "checkpoint_last.pt", map_location="cpu", weights_only=True)
     assert ck2["extra_state"]["num_updates"] > n1
+
+
+def test_cli_trains_on_manifest_with_multitask(tmp_path, capsys):
+    """The reference recipe's --multitask-config-yaml (textless/1_train.sh:119): per-task dict.txt +
+    {split}.tsv text targets, a transformer head on an encoder layer and CTC heads on encoder and
+    decoder states, trained with the on-disk manifest path; the model's state carries the heads
+    under fairseq's ``{task}_decoder.*`` names."""
+    from manifest_corpus import write_corpus
+    d = tmp_path / "data"
+    d.mkdir()
+    c = write_corpus(str(d), frames=(150, 97, 200, 61, 88, 131, 45, 170), di=768, ti=12)
+    letters = "abcdefghij"
+    mtd = tmp_path / "letters"
+    mtd.mkdir()
+    (mtd / "dict.txt").write_text("".join(f"{ch} 1\n" for ch in letters))
+    rng = __import__("numpy").random.default_rng(0)
+    rows = ["id\ttgt_text"] + [f"utt{k}\t{' '.join(rng.choice(list(letters), max(2, T // 20)))}"
+                               for k, T in enumerate(c["frames"])]
+    (mtd / "train.tsv").write_text("\n".join(rows) + "\n")
+    mt = tmp_path / "config_multitask.yaml"
+    mt.write_text(f"source_letter:\n  decoder_type: transformer\n  dict: {mtd}/dict.txt\n  data: {mtd}\n"
+                  f"  encoder_layer: 2\n  loss_weight: 8.0\n  decoder_args:\n    decoder_layers: 1\n"
+                  f"target_ctc:\n  decoder_type: ctc\n  dict: {mtd}/dict.txt\n  data: {mtd}\n  encoder_layer: 1\n"
+                  f"  loss_weight: 1.0\ndecoder_ctc:\n  decoder_type: ctc\n  dict: {mtd}/dict.txt\n  data: {mtd}\n"
+                  f"  decoder_layer: 2\n  loss_weight: 1.6\n")
+    y = tmp_path / "mm.yaml"
+    y.write_text(FUSION_YAML.replace('["/feats/vit_base_patch16_384"]', f'["{c["feat_dir"]}"]'))
+    sd = tmp_path / "ck"
+    argv = (f"{d} --task multimodal_speech_to_speech --arch mm_s2ut_transformer --criterion speech_to_unit "
+            f"--config-yaml config.yaml --target-is-code --target-code-size 1000 --multitask-config-yaml {mt} "
+            f"--share-decoder-input-output-embed --fp16 --multimodal-translation-config-yaml {y} {TINY} "
+            f"--max-update 4 --max-tokens 600 --log-interval 4 --warmup-updates 4 --lr 1e-3 --save-dir {sd}").split()
+    assert pkg("cli").main(argv) == 0
+    recs = [json.loads(l) for l in capsys.readouterr().out.splitlines() if l.startswith("{")]
+    assert [r["num_updates"] for r in recs] == [4] and recs[0]["loss"] > 0
+    ck = torch.load(sd / "checkpoint_last.pt", map_location="cpu", weights_only=True)
+    for k in ("source_letter_decoder.layers.0.encoder_attn.k_proj.weight", "source_letter_decoder.embed_tokens.weight",
+              "target_ctc_decoder.proj.weight", "decoder_ctc_decoder.proj.bias"):
+        assert k in ck["model"], k
+    assert tuple(ck["model"]["source_letter_decoder.layers.0.encoder_attn.k_proj.weight"].shape) == (256, 256)

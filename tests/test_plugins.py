@@ -50,7 +50,10 @@ def _plugins():
 def _args(tmp_path, extra=""):
     y = tmp_path / "mm.yaml"
     y.write_text(FUSION_YAML)
-    return _plugins().build_parser().parse_args((CANONICAL.format(yaml=y) + extra).split())
+    mt = tmp_path / "config_multitask.yaml"     # the recipe's multitask config, here with no tasks
+    mt.write_text("{}\n")
+    cmd = CANONICAL.format(yaml=y).replace("config_multitask.yaml", str(mt))
+    return _plugins().build_parser().parse_args((cmd + extra).split())
 
 
 def test_registry_names():
@@ -227,3 +230,42 @@ def test_grad_allreducer_gloo_world2():
         assert launched == 4, (r, launched, ok)  # every bucket launched during the "backward"
         assert ok is True
         assert scal == [3.0, 30.0]
+
+
+def test_multitask_config_and_text_targets(tmp_path):
+    """fairseq MultitaskConfig / TextTargetMultitaskData restatement: input_from / input_layer,
+    defaults, dict.txt, eos appended except for CTC, collater (eos-first prev_output_tokens)."""
+    MT = pkg("multitask")
+    d = tmp_path / "letters"
+    d.mkdir()
+    (d / "dict.txt").write_text("a 10\nb 7\nc 3\n")
+    (d / "train.tsv").write_text("id\ttgt_text\nu1\ta b c\nu2\tc a\n")
+    y = tmp_path / "mt.yaml"
+    y.write_text(f"src_letter:\n  decoder_type: transformer\n  dict: {d}/dict.txt\n  data: {d}\n  encoder_layer: 6\n"
+                 f"  loss_weight: 8.0\nctc_tgt:\n  decoder_type: ctc\n  dict: {d}/dict.txt\n  data: {d}\n"
+                 f"  decoder_layer: 3\n  loss_weight: 1.6\n")
+    raw = MT.load_multitask_config(str(y))
+    assert list(raw) == ["src_letter", "ctc_tgt"]
+    assert MT.input_spec(raw["src_letter"]) == ("encoder", 5)
+    assert MT.input_spec(raw["ctc_tgt"]) == ("decoder", 2)
+    assert MT.input_spec({"decoder_type": "ctc"}) == ("encoder", -1)
+    dct = MT.Dictionary.load(raw["src_letter"]["dict"])
+    assert len(dct) == 7 and dct.index["a"] == 4
+    cfg = pkg().default_cfg()
+    t = MT.task_model_cfg("src_letter", raw["src_letter"], dct, cfg)
+    assert (t["d"], t["H"], t["F"], t["L"], t["dropout"], t["layer"]) == (256, 4, 2048, 2, 0.3, 5)
+    c = MT.task_model_cfg("ctc_tgt", raw["ctc_tgt"], dct, cfg)
+    assert c["blank"] == 0 and c["zero_infinity"] and c["layer"] == 2
+    tx = MT.TextTargetMultitaskData(str(d), "train", dct, "transformer")
+    assert tx.get("u1").tolist() == [4, 5, 6, 2]
+    assert MT.TextTargetMultitaskData(str(d), "train", dct, "ctc").get("u2").tolist() == [6, 4]
+    col = tx.collater([tx.get("u1"), tx.get("u2")])
+    assert col["target"].tolist() == [[4, 5, 6, 2], [6, 4, 2, 1]]
+    assert col["prev_output_tokens"].tolist() == [[2, 4, 5, 6], [2, 6, 4, 1]]
+    assert col["target_lengths"].tolist() == [4, 3] and col["ntokens"] == 7
+    # the heads enter the flat layout with fairseq's key names
+    cfg["multitask"] = [t, c]
+    names = [n for n, _ in pkg("model").param_specs(cfg)[0]]
+    assert "src_letter_decoder.layers.1.encoder_attn.k_proj.weight" in names
+    assert names.index("ctc_tgt_decoder.proj.weight") < names.index("decoder.layer_norm.weight")
+    assert names.index("src_letter_decoder.embed_tokens.weight") < names.index("encoder.layer_norm.weight")
