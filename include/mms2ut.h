@@ -43,7 +43,9 @@ enum {
   MMS_EPI_F32 = 3,          /* C(fp32) = alpha*acc                        (split-K slabs) */
   MMS_EPI_GATE = 4,         /* g = sigmoid(acc+bias); C = t + g*(o-t); out2 = g; o = aux[:, :N], t = aux[:, N:2N] */
   MMS_EPI_RELU_DROP_BWD = 5,/* C = aux>0 ? alpha*acc/(1-p) : 0            (fc2 dgrad -> fc1 pre-act) */
-  MMS_EPI_F16_ACC = 6       /* C += alpha*acc                                               */
+  MMS_EPI_F16_ACC = 6,      /* C += alpha*acc                                               */
+  MMS_EPI_GELU_DROP = 7,    /* z = alpha*acc + bias; out2 = z; C = dropout(gelu(z))  (torch F.gelu, erf form) */
+  MMS_EPI_GELU_DROP_BWD = 8 /* z = aux: C = keep ? alpha*acc/(1-p) * gelu'(z) : 0 (mask regenerated from seed/offset) */
 };
 
 typedef struct mms2ut_gemm_args {

@@ -10,7 +10,8 @@ LIB_PATH = os.environ.get("MMS2UT_LIB") or os.path.join(HERE, "lib", "libmms2ut_
 
 vp, i32, i64, u64, f32 = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_float
 
-EPI_F16, EPI_RELU_DROP, EPI_DROP_RESID, EPI_F32, EPI_GATE, EPI_RELU_DROP_BWD, EPI_F16_ACC = range(7)
+EPI_F16, EPI_RELU_DROP, EPI_DROP_RESID, EPI_F32, EPI_GATE, EPI_RELU_DROP_BWD, EPI_F16_ACC, EPI_GELU_DROP, \
+    EPI_GELU_DROP_BWD = range(9)
 
 
 class GemmArgs(C.Structure):

@@ -132,6 +132,11 @@ MMS_DEV h16x8 read_frag(const char* lds, int sub, int kk, int lane) {
 }
 
 MMS_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// torch F.gelu (approximate='none'): 0.5 z (1 + erf(z / sqrt 2)) and its derivative
+MMS_DEV float gelu_(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+MMS_DEV float gelu_grad_(float z) {
+  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+}
 
 template <int EPI>
 MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, int n, f32x4 v) {
@@ -148,7 +153,7 @@ MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, in
     return;
   }
   const bool full = n + 3 < N;
-  if (P.bias && EPI != MMS_EPI_RELU_DROP_BWD) {
+  if (P.bias && EPI != MMS_EPI_RELU_DROP_BWD && EPI != MMS_EPI_GELU_DROP_BWD) {
     if (full) {
       const h16x4 bv = *reinterpret_cast<const h16x4*>(P.bias + n);
 #pragma unroll
@@ -171,7 +176,8 @@ MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, in
     }
   };
   bool keep[4] = {true, true, true, true};
-  if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID) && P.thresh)
+  if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GELU_DROP ||
+       EPI == MMS_EPI_GELU_DROP_BWD) && P.thresh)
     mms_keep4(P.seed, P.offset + (uint64_t)m * P.ld_rng + n, P.thresh, keep);
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
   float o[4];
@@ -209,6 +215,24 @@ MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, in
     ld4(C, n, c);
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[r] = c[r] + x[r];
+  } else if (EPI == MMS_EPI_GELU_DROP) {
+    h16 zh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      zh[r] = (h16)x[r];
+      o[r] = keep[r] ? gelu_((float)zh[r]) * dscale : 0.f;
+    }
+    h16* z_row = P.out2 + (long)m * P.ldo2;
+    if (full) {
+      *reinterpret_cast<h16x4*>(z_row + n) = h16x4{zh[0], zh[1], zh[2], zh[3]};
+    } else {
+      for (int r = 0; r < 4; ++r) if (n + r < N) z_row[n + r] = zh[r];
+    }
+  } else if (EPI == MMS_EPI_GELU_DROP_BWD) {
+    float z[4];
+    ld4(auxz + (long)m * P.ldaux, n, z);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = keep[r] ? x[r] * dscale * gelu_grad_(z[r]) : 0.f;
   } else {
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[r] = x[r];
@@ -244,7 +268,7 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
   float x[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) x[r] = v[r] * P.alpha;
-  if (P.bias && EPI != MMS_EPI_RELU_DROP_BWD) {
+  if (P.bias && EPI != MMS_EPI_RELU_DROP_BWD && EPI != MMS_EPI_GELU_DROP_BWD) {
     const h16x8 bv = *reinterpret_cast<const h16x8*>(P.bias + n);
 #pragma unroll
     for (int r = 0; r < 8; ++r) x[r] += (float)bv[r];
@@ -256,7 +280,8 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
     for (int r = 0; r < 8; ++r) o[r] = (float)t[r];
   };
   bool keep[8] = {true, true, true, true, true, true, true, true};
-  if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID) && P.thresh) {
+  if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GELU_DROP ||
+       EPI == MMS_EPI_GELU_DROP_BWD) && P.thresh) {
     const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
     bool k0[4], k1[4];
     mms_keep4(P.seed, c0, P.thresh, k0);
@@ -297,6 +322,19 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
     ld8(C + n, c);
 #pragma unroll
     for (int r = 0; r < 8; ++r) o[r] = c[r] + x[r];
+  } else if (EPI == MMS_EPI_GELU_DROP) {
+    h16x8 zv;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      zv[r] = (h16)x[r];
+      o[r] = keep[r] ? gelu_((float)zv[r]) * dscale : 0.f;
+    }
+    *reinterpret_cast<h16x8*>(P.out2 + (long)m * P.ldo2 + n) = zv;
+  } else if (EPI == MMS_EPI_GELU_DROP_BWD) {
+    float z[8];
+    ld8(auxz + (long)m * P.ldaux + n, z);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) o[r] = keep[r] ? x[r] * dscale * gelu_grad_(z[r]) : 0.f;
   } else {
 #pragma unroll
     for (int r = 0; r < 8; ++r) o[r] = x[r];
@@ -354,7 +392,7 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
     v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
   };
   constexpr bool LOADS = EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GATE || EPI == MMS_EPI_RELU_DROP_BWD ||
-                         EPI == MMS_EPI_F16_ACC;
+                         EPI == MMS_EPI_F16_ACC || EPI == MMS_EPI_GELU_DROP_BWD;
   if (EPI == MMS_EPI_F32 || !(P.vec16 && n + 7 < P.N)) {
 #pragma unroll 2
     for (int pass = 0; pass < 8; ++pass) {
@@ -371,7 +409,7 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
   // serialised the epilogue into 8 dependent global round trips.
   const int m0 = bm + wm * 64 + (lane >> 3);
   float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (EPI != MMS_EPI_RELU_DROP_BWD && P.bias) {
+  if (EPI != MMS_EPI_RELU_DROP_BWD && EPI != MMS_EPI_GELU_DROP_BWD && P.bias) {
     const h16x8 b8 = *reinterpret_cast<const h16x8*>(P.bias + n);
 #pragma unroll
     for (int e = 0; e < 8; ++e) bv[e] = (float)b8[e];
@@ -403,7 +441,8 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] = x[e] * P.alpha + bv[e];
     bool keep[8] = {true, true, true, true, true, true, true, true};
-    if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID) && P.thresh) {
+    if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GELU_DROP ||
+         EPI == MMS_EPI_GELU_DROP_BWD) && P.thresh) {
       const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
       bool k0[4], k1[4];
       mms_keep4(P.seed, c0, P.thresh, k0);
@@ -421,6 +460,18 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
         o8[e] = (h16)(tv + g * (ov - tv));
       }
       *reinterpret_cast<h16x8*>(P.out2 + (long)m * P.ldo2 + n) = g8;
+    } else if (EPI == MMS_EPI_GELU_DROP) {
+      h16x8 z8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        z8[e] = (h16)x[e];
+        o8[e] = (h16)(keep[e] ? gelu_((float)z8[e]) * dscale : 0.f);
+      }
+      *reinterpret_cast<h16x8*>(P.out2 + (long)m * P.ldo2 + n) = z8;
+    } else if (EPI == MMS_EPI_GELU_DROP_BWD) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o8[e] = (h16)(keep[e] ? x[e] * dscale * gelu_grad_((float)ax[pass][e]) : 0.f);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -1008,7 +1059,7 @@ int launch_256(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
 #define CASE(E) case E: if (var == 4) hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, E, 4>), grid, block, 0, s, P, tm, tn, total); \
                         else hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, E, 5>), grid, block, 0, s, P, tm, tn, total); break;
       CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
       default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
     }
@@ -1017,7 +1068,7 @@ int launch_256(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, E>), grid, block, 0, s, P, tm, tn, total); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
@@ -1031,7 +1082,7 @@ int launch_dma32(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s)
   switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm_dma32_kernel<A_KC, B_KC, E>), grid, block, 0, s, P, tm, tn, total); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
@@ -1050,7 +1101,7 @@ int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
     switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 2>), grid, block, 0, s, P, tm, tn, total); break;
       CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
       default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
     }
@@ -1059,7 +1110,7 @@ int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 3>), grid, block, 0, s, P, tm, tn, total); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
@@ -1074,7 +1125,7 @@ int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, E>), grid, block, lds, s, P, tm, tn, total); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
@@ -1232,8 +1283,9 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.out2 = a->out2; P.ldo2 = a->ldo2;
   P.p = a->dropout_p; P.thresh = mms_drop_thresh(a->dropout_p); P.seed = a->seed; P.offset = a->offset;
   P.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
-  MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
-  MMS_REQUIRE(a->epi != MMS_EPI_GATE || a->out2, "gemm: gate epilogue needs out2");
+  MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD ||
+                a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
+  MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");
   {
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     bool v = al16(a->C) && a->ldc % 8 == 0 && a->sC1 % 8 == 0 && a->sC2 % 8 == 0;

@@ -11,7 +11,8 @@ import torch
 from . import _lib
 from ._lib import GemmArgs, call
 
-EPI_F16, EPI_RELU_DROP, EPI_DROP_RESID, EPI_F32, EPI_GATE, EPI_RELU_DROP_BWD, EPI_F16_ACC = range(7)
+EPI_F16, EPI_RELU_DROP, EPI_DROP_RESID, EPI_F32, EPI_GATE, EPI_RELU_DROP_BWD, EPI_F16_ACC, EPI_GELU_DROP, \
+    EPI_GELU_DROP_BWD = range(9)
 F16 = torch.float16
 
 
@@ -194,22 +195,26 @@ class TransposedWeights:
         return self.flatT[off:off + W.numel()].view(W.shape[1], W.shape[0])
 
 
-def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False):
+def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None):
     """dx[M,K] = dy[M,N] @ W[N,K]  (W row-major, reduction over N).  Reads the W^T image when one
-    is registered (TransposedWeights), else W itself through transposed fragment reads."""
+    is registered (TransposedWeights), else W itself through transposed fragment reads.
+    drop=(seed, offset): the forward dropout mask of the [M, K] output (EPI_GELU_DROP_BWD)."""
     M, N = dy.shape
     K = W.shape[1]
     if out is None:
         out = torch.empty(M, K, dtype=F16, device=dy.device)
     if accumulate:
         epi = EPI_F16_ACC
+    seed, off = drop if (drop is not None and p > 0) else (0, 0)
     WT = TransposedWeights.active.get(W) if TransposedWeights.active is not None else None
     if WT is not None:
         gemm(dy, WT, out, M, K, N, a_kc=True, b_kc=True, lda=dy.stride(0), ldb=WT.stride(0),
-             ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p)
+             ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p,
+             seed=seed, offset=off, ld_rng=K)
         return out
     gemm(dy, W, out, M, K, N, a_kc=True, b_kc=False, lda=dy.stride(0), ldb=W.stride(0),
-         ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p)
+         ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p,
+         seed=seed, offset=off, ld_rng=K)
     return out
 
 
@@ -412,8 +417,9 @@ def layernorm(x, g, b, eps=1e-5, *, out=None, grp=0, grp_out=0, p=0.0, drop=None
 
 
 def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None, dy_grp=0, dy_grp_out=0,
-                  dy_p=0.0, dy_drop=None):
-    """Returns dx (+dres). dgb: fp16 view of [dgamma | dbeta] (2*D contiguous).
+                  dy_p=0.0, dy_drop=None, dgb_accumulate=False):
+    """Returns dx (+dres). dgb: fp16 view of [dgamma | dbeta] (2*D contiguous), overwritten, or
+    added to with dgb_accumulate (one LayerNorm applied at several places).
     emit=(p, (seed, offset)): also return dropout(dx) for the sublayer below -> (dx, dxd).
     dy_grp/dy_grp_out/dy_p: dy is read through layernorm(out=, grp=, p=)'s layout and dropout."""
     R, D = x.shape
@@ -445,7 +451,7 @@ def layernorm_bwd(dy, x, g, mean, rstd, dgb, dres=None, want_dx=True, emit=None,
     # critical path for the weight-gradient side stream
     ctx = side_begin(part)
     with (ctx or _NULLCTX):
-        call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), 0, _s())
+        call("mms2ut_colsum_parts", part.data_ptr(), nparts, 2 * D, dgb.data_ptr(), int(dgb_accumulate), _s())
     if emit is not None:
         return dx, (dxd if dxd is not None else dx)
     return dx

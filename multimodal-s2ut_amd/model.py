@@ -49,6 +49,7 @@ def default_cfg(**over):
         image_feat_dim=768, image_pre_norm=True, SA_image_dropout=0.1, SA_text_dropout=0.0,
         SA_attention_dropout=0.1, modality_dropout=-0.5, audio_dropout=-0.5,
         max_source_positions=6000, max_target_positions=3000, no_scale_embedding=False,
+        external_multimodal_transformer_layers=None,
     )
     cfg.update(over)
     return cfg
@@ -113,6 +114,44 @@ def _decoder_param_specs(S, spec, mha, ln):
         S.extend([(f"{p}.k_proj.bias", (dd,)), (f"{p}.v_proj.bias", (dd,))])
     S.append((f"{p0}.embed_tokens.weight", (spec.V, dd)))
 
+EXT = "encoder.multimodal_transformer.0"
+
+
+def external_dims(cfg):
+    """(d, Di, heads, head dim, FFN, layers) of the external transformer as the reference builds it
+    (mm_s2s_transformer.py:156-171: kdim = vdim = Di, nhead = Di // 64, FFN 4 Di)."""
+    d, Di = cfg["encoder_embed_dim"], cfg["image_feat_dim"]
+    N = cfg["external_multimodal_transformer_layers"]
+    if not N or N < 1 or N > cfg["encoder_layers"]:
+        raise ValueError(f"external_multimodal_transformer_layers={N!r} (1..encoder_layers)")
+    H = Di // 64
+    if H < 1 or d % H:
+        raise NotImplementedError(f"external transformer: nhead = Di // 64 = {H} must divide embed_dim {d}")
+    return d, Di, H, d // H, 4 * Di, N
+
+
+def _external_param_specs(S, cfg, ln):
+    """ExternalMultimodalTransformerEncoder (fuse.py:288-357) parameter names / shapes, layers in
+    backward-completion order, the shared layer_norm1 last."""
+    d, Di, H, hd, F_, N = external_dims(cfg)
+    for i in reversed(range(N)):
+        p = f"{EXT}.layers.{i}"
+        S.extend([(p + ".linear2.weight", (d, F_)), (p + ".linear2.bias", (d,)),
+                  (p + ".linear1.weight", (F_, d)), (p + ".linear1.bias", (F_,))])
+        ln(p + ".norm3", d)
+        ln(p + ".norm2", d)
+        S.extend([(p + ".multihead_attn.out_proj.weight", (d, d)), (p + ".multihead_attn.out_proj.bias", (d,))])
+        if Di == d:
+            S.append((p + ".multihead_attn.in_proj_weight", (3 * d, d)))
+        else:
+            S.extend([(p + ".multihead_attn.q_proj_weight", (d, d)), (p + ".multihead_attn.k_proj_weight", (d, Di)),
+                      (p + ".multihead_attn.v_proj_weight", (d, Di))])
+        S.append((p + ".multihead_attn.in_proj_bias", (3 * d,)))
+        ln(p + ".norm1", d)
+        S.extend([(p + ".self_attn.out_proj.weight", (d, d)), (p + ".self_attn.out_proj.bias", (d,)),
+                  (p + ".self_attn.in_proj_weight", (3 * d, d)), (p + ".self_attn.in_proj_bias", (3 * d,))])
+    ln(EXT + ".layer_norm1", d)
+
 # ============================================================================ parameter layout
 
 
@@ -150,9 +189,11 @@ def param_specs(cfg):
             _decoder_param_specs(S, DecoderSpec.aux(cfg, t), mha, ln)
         elif t["input_from"] == "encoder":
             S.extend([(f"{t['name']}_decoder.proj.weight", (t["V"], d)), (f"{t['name']}_decoder.proj.bias", (t["V"],))])
+    ext = cfg["fusion"] and cfg["multimodal_attention_type"] == "external_multimodal_transformer"
+    if cfg["fusion"] and not ext:
+        S.extend([("encoder.gate_denses.0.weight", (d, 2 * d)), ("encoder.gate_denses.0.bias", (d,))])
     if cfg["fusion"]:
         Di = cfg["image_feat_dim"]
-        S.extend([("encoder.gate_denses.0.weight", (d, 2 * d)), ("encoder.gate_denses.0.bias", (d,))])
         if cfg["multimodal_attention_type"] == "multimodal_attention":
             p = "encoder.multimodal_attns.0"
             S.extend([(p + ".out_proj.weight", (d, d)), (p + ".out_proj.bias", (d,))])
@@ -163,6 +204,8 @@ def param_specs(cfg):
                           (p + ".v_proj_weight", (d, Di))])
             S.extend([(p + ".in_proj_bias", (3 * d,)), (p + ".bias_k", (1, 1, d)),
                       (p + ".bias_v", (1, 1, d))])
+        elif cfg["multimodal_attention_type"] == "external_multimodal_transformer":
+            _external_param_specs(S, cfg, ln)
         elif cfg["multimodal_attention_type"] == "selective_attention":
             p = "encoder.selective_attns.0"
             S.extend([(p + ".proj.weight", (d, d)), (p + ".proj.bias", (d,)),
@@ -171,7 +214,7 @@ def param_specs(cfg):
                       (p + ".k_proj.bias", (d,)), (p + ".v_proj.bias", (d,))])
         else:
             raise NotImplementedError(cfg["multimodal_attention_type"])
-        if cfg["image_pre_norm"]:
+        if cfg["image_pre_norm"] and not ext:
             ln("encoder.image_pre_norm_module", Di)
     ln("encoder.layer_norm", d)
     for l in reversed(range(cfg["encoder_layers"])):
@@ -194,6 +237,13 @@ def param_specs(cfg):
                        (f"encoder.wav2vec2_adaptor.layers.{j}.bias", (1536,))])
     unused.extend([("encoder.wav2vec2_adaptor.layernorm.weight", (1024,)),
                    ("encoder.wav2vec2_adaptor.layernorm.bias", (1024,))])
+    if ext:
+        # built by the reference for every fusion type but unused by the external transformer
+        # (mm_s2s_transformer.py:173-190): kept in the state dict, never computed (as Q3)
+        unused.extend([("encoder.gate_denses.0.weight", (d, 2 * d)), ("encoder.gate_denses.0.bias", (d,))])
+        if cfg["image_pre_norm"]:
+            Di = cfg["image_feat_dim"]
+            unused.extend([("encoder.image_pre_norm_module.weight", (Di,)), ("encoder.image_pre_norm_module.bias", (Di,))])
     return S, unused
 
 
@@ -447,7 +497,13 @@ class MMS2UTModel:
         for i in range(1, len(cfg["conv_kernel_sizes"])):
             W = P(f"encoder.subsample.conv_layers.{i}.weight")
             mats.append(W.view(W.shape[0], -1))
-        if cfg["fusion"]:
+        if cfg["fusion"] and cfg["multimodal_attention_type"] == "external_multimodal_transformer":
+            for i in range(cfg["external_multimodal_transformer_layers"]):
+                p = f"{EXT}.layers.{i}"
+                Wq, _, _, _ = self._ext_w(i)
+                mats.extend([P(p + ".linear2.weight"), P(p + ".linear1.weight"), P(p + ".multihead_attn.out_proj.weight"),
+                             Wq, P(p + ".self_attn.out_proj.weight"), P(p + ".self_attn.in_proj_weight")])
+        elif cfg["fusion"]:
             Di = cfg["image_feat_dim"]
             mats.append(P("encoder.gate_denses.0.weight"))
             if cfg["multimodal_attention_type"] == "multimodal_attention":
@@ -483,9 +539,11 @@ class MMS2UTModel:
         g = torch.Generator().manual_seed(seed)
         sd = {}
         for name, shape in self.params.specs:
-            if name.endswith("layer_norm.weight") or name.endswith("image_pre_norm_module.weight"):
+            if name.endswith("layer_norm.weight") or name.endswith("image_pre_norm_module.weight") or \
+                    re.search(r"\.(norm[123]|layer_norm1)\.weight$", name):
                 t = torch.ones(shape)
-            elif name.endswith(".bias") and ("layer_norm" in name or "out_proj" in name or "image_pre_norm" in name):
+            elif name.endswith(".bias") and ("layer_norm" in name or "out_proj" in name or "image_pre_norm" in name
+                                             or re.search(r"\.norm[123]\.bias$", name) or "in_proj_bias" in name):
                 t = torch.zeros(shape)
             elif name.endswith("embed_tokens.weight"):
                 t = torch.randn(shape, generator=g) * shape[1] ** -0.5
@@ -886,6 +944,155 @@ class MMS2UTModel:
             dtext_total = K.dropout(dtext_total, c["ptxt"], c["drop_txt"])
         return dtext_total
 
+    # -------------------------------------------------------------- external multimodal transformer
+    def _ext_w(self, i):
+        """(Wq, Wkv, bq, bkv) of layer i's cross-attention (packed or separate q/k/v weights)."""
+        d, Di = self.cfg["encoder_embed_dim"], self.cfg["image_feat_dim"]
+        p = f"{EXT}.layers.{i}.multihead_attn"
+        b = self.P(p + ".in_proj_bias")
+        if Di == d:
+            W = self.P(p + ".in_proj_weight")
+            return W[:d], W[d:], b[:d], b[d:]
+        return (self.P(p + ".q_proj_weight"), self.params.span(p + ".k_proj_weight", p + ".v_proj_weight").view(2 * d, Di),
+                b[:d], b[d:])
+
+    def _ext_g(self, i):
+        d, Di = self.cfg["encoder_embed_dim"], self.cfg["image_feat_dim"]
+        p = f"{EXT}.layers.{i}.multihead_attn"
+        b = self.G(p + ".in_proj_bias")
+        if Di == d:
+            W = self.G(p + ".in_proj_weight")
+            return W[:d], W[d:], b[:d], b[d:]
+        return (self.G(p + ".q_proj_weight"),
+                self.params.span(p + ".k_proj_weight", p + ".v_proj_weight", grad=True).view(2 * d, Di), b[:d], b[d:])
+
+    def ext_layer_fwd(self, i, x, img2, B, Te, Ti, lens32, img_km):
+        """MultimodalTransformerDecoderLayer.forward (fuse.py:237-285; norm_first False,
+        self-attention first): x = norm1(x + drop(SA(x))); x = norm2(x + drop(MHA(x, img)));
+        x = norm3(x + drop(linear2(drop(gelu(linear1(x)))))).  x [B*Te, d], img2 [B*Ti, Di]."""
+        d, Di, H, hd, F_, _ = external_dims(self.cfg)
+        R = B * Te
+        p = f"{EXT}.layers.{i}"
+        pp = self._p("SA_attention_dropout")
+        c = {"x": x, "pp": pp, "B": B, "Te": Te, "Ti": Ti, "img2": img2}
+        qkv = K.linear(x, self.P(p + ".self_attn.in_proj_weight"), self.P(p + ".self_attn.in_proj_bias"))
+        O = torch.empty(R, d, dtype=F16, device=x.device)
+        c["drop_sa"] = self._drop(pp, B * H * Te * Te)
+        c["sattn"] = attn_forward(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Te, Te, hd, hd ** -0.5,
+                                  O, d, key_len=lens32, p=pp, drop=c["drop_sa"])
+        c["qkv"], c["sO"] = qkv, O
+        c["drop1"] = self._drop(pp, R * d)
+        y1 = K.linear(O, self.P(p + ".self_attn.out_proj.weight"), self.P(p + ".self_attn.out_proj.bias"),
+                      epi=K.EPI_DROP_RESID, aux=x, p=pp, drop=c["drop1"])
+        x1, c["m1"], c["r1"] = K.layernorm(y1, self.P(p + ".norm1.weight"), self.P(p + ".norm1.bias"))
+        c["y1"], c["x1"] = y1, x1
+        Wq, Wkv, bq, bkv = self._ext_w(i)
+        q = K.linear(x1, Wq, bq)
+        kv = K.linear(img2, Wkv, bkv)
+        O2 = torch.empty(R, d, dtype=F16, device=x.device)
+        c["drop_ca"] = self._drop(pp, B * H * Te * Ti)
+        c["cattn"] = attn_forward(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Te, Ti, hd, hd ** -0.5, O2, d,
+                                  key_mask=img_km, p=pp, drop=c["drop_ca"])
+        c["q"], c["kv"], c["cO"] = q, kv, O2
+        c["drop2"] = self._drop(pp, R * d)
+        y2 = K.linear(O2, self.P(p + ".multihead_attn.out_proj.weight"), self.P(p + ".multihead_attn.out_proj.bias"),
+                      epi=K.EPI_DROP_RESID, aux=x1, p=pp, drop=c["drop2"])
+        x2, c["m2"], c["r2"] = K.layernorm(y2, self.P(p + ".norm2.weight"), self.P(p + ".norm2.bias"))
+        c["y2"], c["x2"] = y2, x2
+        c["drop_act"] = self._drop(pp, R * F_)
+        z = torch.empty(R, F_, dtype=F16, device=x.device)
+        h = K.linear(x2, self.P(p + ".linear1.weight"), self.P(p + ".linear1.bias"), epi=K.EPI_GELU_DROP, out2=z,
+                     p=pp, drop=c["drop_act"])
+        c["z"], c["h"] = z, h
+        c["drop3"] = self._drop(pp, R * d)
+        y3 = K.linear(h, self.P(p + ".linear2.weight"), self.P(p + ".linear2.bias"), epi=K.EPI_DROP_RESID, aux=x2,
+                      p=pp, drop=c["drop3"])
+        x3, c["m3"], c["r3"] = K.layernorm(y3, self.P(p + ".norm3.weight"), self.P(p + ".norm3.bias"))
+        c["y3"] = y3
+        return x3, c
+
+    def _lnspan(self, n):
+        return self.params.span(n + ".weight", n + ".bias", grad=True)
+
+    def ext_layer_bwd(self, i, c, dx3):
+        """Hand-written backward of ext_layer_fwd: returns d(layer input).  Post-LN: every
+        residual add happens before a LayerNorm, so each sublayer's input gradient is
+        (LayerNorm backward) + (the sublayer's dgrad), summed into a fresh buffer (the LayerNorm
+        output is still read by side-stream weight gradients)."""
+        d, Di, H, hd, F_, _ = external_dims(self.cfg)
+        p = f"{EXT}.layers.{i}"
+        B, Te, Ti, pp = c["B"], c["Te"], c["Ti"], c["pp"]
+        dy3, dl2 = K.layernorm_bwd(dx3, c["y3"], self.P(p + ".norm3.weight"), c["m3"], c["r3"], self._lnspan(p + ".norm3"),
+                                   emit=(pp, c["drop3"]))
+        dz = K.linear_dgrad(dl2, self.P(p + ".linear2.weight"), epi=K.EPI_GELU_DROP_BWD, aux=c["z"], p=pp,
+                            drop=c["drop_act"])
+        K.linear_wgrad(dl2, c["h"], self.G(p + ".linear2.weight"), db=self.G(p + ".linear2.bias"))
+        dx2 = K.add_f16(K.linear_dgrad(dz, self.P(p + ".linear1.weight")), dy3)
+        K.linear_wgrad(dz, c["x2"], self.G(p + ".linear1.weight"), db=self.G(p + ".linear1.bias"))
+        dy2, dlo2 = K.layernorm_bwd(dx2, c["y2"], self.P(p + ".norm2.weight"), c["m2"], c["r2"], self._lnspan(p + ".norm2"),
+                                    emit=(pp, c["drop2"]))
+        dO2 = K.linear_dgrad(dlo2, self.P(p + ".multihead_attn.out_proj.weight"))
+        K.linear_wgrad(dlo2, c["cO"], self.G(p + ".multihead_attn.out_proj.weight"),
+                       db=self.G(p + ".multihead_attn.out_proj.bias"))
+        q, kv = c["q"], c["kv"]
+        dq, dkv = torch.empty_like(q), torch.empty_like(kv)
+        attn_backward(c["cattn"], dO2, d, c["cO"], q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Te, Ti, hd, hd ** -0.5,
+                      dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pp, drop=c["drop_ca"])
+        Wq, _, _, _ = self._ext_w(i)
+        gWq, gWkv, gbq, gbkv = self._ext_g(i)
+        dx1 = K.add_f16(K.linear_dgrad(dq, Wq), dy2)
+        K.linear_wgrad(dq, c["x1"], gWq, db=gbq)
+        K.linear_wgrad(dkv, c["img2"], gWkv, db=gbkv)   # the image features are leaves: no dgrad
+        dy1, dso = K.layernorm_bwd(dx1, c["y1"], self.P(p + ".norm1.weight"), c["m1"], c["r1"], self._lnspan(p + ".norm1"),
+                                   emit=(pp, c["drop1"]))
+        dO = K.linear_dgrad(dso, self.P(p + ".self_attn.out_proj.weight"))
+        K.linear_wgrad(dso, c["sO"], self.G(p + ".self_attn.out_proj.weight"), db=self.G(p + ".self_attn.out_proj.bias"))
+        qkv = c["qkv"]
+        dqkv = torch.empty_like(qkv)
+        attn_backward(c["sattn"], dO, d, c["sO"], qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Te, Te,
+                      hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pp, drop=c["drop_sa"])
+        dx = K.add_f16(K.linear_dgrad(dqkv, self.P(p + ".self_attn.in_proj_weight")), dy1)
+        K.linear_wgrad(dqkv, c["x"], self.G(p + ".self_attn.in_proj_weight"), db=self.G(p + ".self_attn.in_proj_bias"))
+        return dx
+
+    def ext_fwd(self, states, img, img_km, B, Te, lens32):
+        """ExternalMultimodalTransformerEncoder.forward (fuse.py:323-357) over the last N encoder
+        states (m1) and the image features (m2 = the same [B, Ti, Di] for every layer)."""
+        N = len(states)
+        _, Ti, Di = img.shape
+        img2 = img.reshape(B * Ti, Di)
+        ctx = {"layers": [], "ln1": [], "N": N}
+        out = None
+        for i in range(N):
+            if out is None:
+                inp = states[i]
+                ctx["ln1"].append(None)
+            else:
+                s_ = K.add_f16(states[i], out)
+                inp, mi, ri = K.layernorm(s_, self.P(EXT + ".layer_norm1.weight"), self.P(EXT + ".layer_norm1.bias"))
+                ctx["ln1"].append((s_, mi, ri))
+            out, c = self.ext_layer_fwd(i, inp, img2, B, Te, Ti, lens32, img_km)
+            ctx["layers"].append(c)
+        return out, ctx
+
+    def ext_bwd(self, ctx, dout):
+        """-> {i: gradient of the i-th external input state} (i over the N states)."""
+        N = ctx["N"]
+        d = dout
+        out = {}
+        for i in reversed(range(N)):
+            dinp = self.ext_layer_bwd(i, ctx["layers"][i], d)
+            ctx["layers"][i] = None
+            if i == 0:
+                out[0] = dinp
+            else:
+                s_, mi, ri = ctx["ln1"][i]
+                ds = K.layernorm_bwd(dinp, s_, self.P(EXT + ".layer_norm1.weight"), mi, ri, self._lnspan(EXT + ".layer_norm1"),
+                                     dgb_accumulate=True)
+                out[i] = ds         # s = m1[i] + out_{i-1}: the same gradient for both
+                d = ds
+        return out
+
     # -------------------------------------------------------------- decoder layer
     def _sp(self, p):
         return p if self.training else 0.0
@@ -1038,9 +1245,24 @@ class MMS2UTModel:
             x, c = self.enc_layer_fwd(l, x, B, Te, lens32)
             ctx["layers"].append(c)
         self.params.await_group("enc_tail")
-        xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("encoder.layer_norm.weight"), self.P("encoder.layer_norm.bias"))
         ctx["lx"] = x
         ctx["fusion"] = None
+        ctx["ext"] = None
+        if cfg["fusion"] and imgs is not None and cfg["multimodal_attention_type"] == "external_multimodal_transformer":
+            # mm_s2s_transformer.py:531-554: the external transformer reads the last N encoder
+            # states (the final LayerNorm's output is replaced, so it is not computed) and the raw
+            # image features; modality dropout: audio-drop zeroes only the replaced encoder_out
+            # (no effect), image-drop zeroes the features (:496-512)
+            if self.training:
+                mod_p, aud_p = self.np_rng.random(), self.np_rng.random()
+                if mod_p < cfg["modality_dropout"] and not aud_p < cfg["audio_dropout"]:
+                    imgs = torch.zeros_like(imgs)
+            N = cfg["external_multimodal_transformer_layers"]
+            states = self.encoder_states(ctx)[-N:]
+            out, ctx["ext"] = self.ext_fwd(states, imgs, img_mask, B, Te, lens32)
+            ctx["B"], ctx["Te"] = B, Te
+            return out, lens32, Te, ctx
+        xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("encoder.layer_norm.weight"), self.P("encoder.layer_norm.bias"))
         out = xl
         if cfg["fusion"] and imgs is not None:
             # modality dropout (mm_s2s_transformer.py:496-512): two host draws every training forward
@@ -1061,7 +1283,16 @@ class MMS2UTModel:
     def encoder_backward(self, ctx, denc, dstates=None):
         """dstates: {l: gradient of encoder_states[l]} (layer l's output, fairseq's
         ``encoder_states`` with return_all_hiddens) from multitask heads."""
-        dstates = dstates or {}
+        dstates = dict(dstates or {})
+        L = self.cfg["encoder_layers"]
+        if ctx.get("ext") is not None:
+            N = ctx["ext"]["N"]
+            for i, g in self.ext_bwd(ctx["ext"], denc).items():
+                l = L - N + i
+                dstates[l] = g if l not in dstates else K.add_f16(dstates[l], g)
+            self._ready(EXT + ".layer_norm1.bias")
+            self._ready("encoder.layer_norm.bias")   # unused by this fusion type: its gradient stays 0
+            return self._encoder_layers_bwd(ctx, dstates.pop(L - 1), None, dstates)
         if ctx["fusion"] is not None:
             denc = self.fusion_bwd(ctx["fusion"], denc)
         last_fusion = [n for n, _ in self.params.specs if n.startswith(("encoder.gate", "encoder.multimodal",
@@ -1078,7 +1309,6 @@ class MMS2UTModel:
         if ctx.get("audio_dropped"):
             denc = torch.zeros_like(denc)   # only the multitask heads' state gradients remain
         layers = ctx["layers"]
-        L = self.cfg["encoder_layers"]
         emit = lambda l: (layers[l]["pd"], layers[l]["drop2"]) if l >= 0 else None  # noqa: E731
         gln = self.params.span("encoder.layer_norm.weight", "encoder.layer_norm.bias", grad=True)
         if (L - 1) in dstates:     # encoder_states[L-1] = the final LayerNorm's input
@@ -1089,6 +1319,14 @@ class MMS2UTModel:
             dx, dmask = K.layernorm_bwd(denc, ctx["lx"], self.P("encoder.layer_norm.weight"), ctx["lm"], ctx["lr"],
                                         gln, emit=emit(L - 1))
         self._ready("encoder.layer_norm.bias")
+        return self._encoder_layers_bwd(ctx, dx, dmask, dstates)
+
+    def _encoder_layers_bwd(self, ctx, dx, dmask, dstates):
+        """Encoder layers L-1..0, the embedding and the subsampler; dx = gradient of the top
+        layer's output, dstates = {l: extra gradient of layer l's output} for l < L-1."""
+        layers = ctx["layers"]
+        L = self.cfg["encoder_layers"]
+        emit = lambda l: (layers[l]["pd"], layers[l]["drop2"]) if l >= 0 else None  # noqa: E731
         for l in reversed(range(L)):
             em = None if (l - 1) in dstates else emit(l - 1)
             dx, dmask = self.enc_layer_bwd(l, layers[l], dx, dy2=dmask, emit=em)

@@ -53,7 +53,8 @@ def set_seed(seed=42):
 FUSION_KEYS = ("SA_image_dropout", "SA_text_dropout", "SA_attention_dropout", "image_pre_norm",
                "is_fusion_top", "image_feat_path", "image_feat_dim", "flickr30k_root",
                "load_visual_extractor_type", "load_visual_extractor", "modality_dropout",
-               "audio_dropout", "multimodal_attention_type", "use_selective_gate", "is_merge_text_img")
+               "audio_dropout", "multimodal_attention_type", "use_selective_gate", "is_merge_text_img",
+               "external_multimodal_transformer_layers")
 
 
 def load_fusion_yaml(path):
@@ -138,8 +139,10 @@ def cfg_from_args(args, fusion_cfg=None, vocab_size=1004):
         if len(dims) != 1:
             raise NotImplementedError("one image-feature type (SURVEY Q8)")
         att = fusion_cfg.multimodal_attention_type
-        if att not in ("selective_attention", "multimodal_attention"):
+        if att not in ("selective_attention", "multimodal_attention", "external_multimodal_transformer"):
             raise NotImplementedError(f"multimodal_attention_type={att!r} (out of scope: SURVEY §2)")
+        if att == "external_multimodal_transformer" and getattr(fusion_cfg, "load_visual_extractor_type", None):
+            raise NotImplementedError("on-line visual extractors (ViT / CLIP) are out of scope: pre-extracted features")
         if getattr(fusion_cfg, "is_merge_text_img", False):
             raise NotImplementedError("is_merge_text_img=True")
         cfg.update(fusion=bool(fusion_cfg.is_fusion_top), multimodal_attention_type=att,
@@ -149,7 +152,8 @@ def cfg_from_args(args, fusion_cfg=None, vocab_size=1004):
                    SA_text_dropout=float(fusion_cfg.SA_text_dropout),
                    SA_attention_dropout=float(fusion_cfg.SA_attention_dropout),
                    modality_dropout=float(fusion_cfg.modality_dropout),
-                   audio_dropout=float(fusion_cfg.audio_dropout))
+                   audio_dropout=float(fusion_cfg.audio_dropout),
+                   external_multimodal_transformer_layers=getattr(fusion_cfg, "external_multimodal_transformer_layers", None))
     return cfg
 
 # ------------------------------------------------------------------------------------ task

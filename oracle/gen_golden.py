@@ -157,6 +157,56 @@ def _make_case(M, F, name, *, att, gate, d, Di, B, Te, Ti, text_pad, img_pad,
     return res
 
 
+def _make_external_case(F, name, *, d, Di, N, B, Te, Ti, text_pad, img_pad, seed=0):
+    """The reference's ExternalMultimodalTransformerEncoder (fuse.py:288-357) exactly as
+    MM_S2STransformerEncoder builds it for multimodal_attention_type
+    "external_multimodal_transformer" (mm_s2s_transformer.py:156-171: TransformerLayerConfig(
+    embed_dim=d, kdim=vdim=Di, nhead=Di // 64, dim_feedforward=4 Di, dropout, batch_first=False))
+    and calls it (:531-554, :582-591: m1 = the last N encoder states, m2 = the image features
+    expanded N times, key padding masks).  Dropout 0 (torch MHA's internal dropout cannot be
+    replayed); train mode."""
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    cfgl = F.TransformerLayerConfig(embed_dim=d, kdim=Di, vdim=Di, nhead=Di // 64, dim_feedforward=Di * 4,
+                                    dropout=0.0, batch_first=False)
+    enc = F.ExternalMultimodalTransformerEncoder(layer_config=cfgl, num_layers=N)
+    with torch.no_grad():
+        for n, prm in enc.named_parameters():
+            if n.endswith("bias"):
+                prm.copy_(0.1 * torch.randn(prm.shape, generator=g))
+            elif "norm" in n:
+                prm.copy_(1.0 + 0.1 * torch.randn(prm.shape, generator=g))
+    enc = enc.double().train()
+    feats = [torch.randn(Te, B, d, generator=g, dtype=torch.float64).requires_grad_(True) for _ in range(N)]
+    img = torch.randn(Ti, B, Di, generator=g, dtype=torch.float64)
+    text_len = torch.full((B,), Te, dtype=torch.long)
+    if text_pad:
+        text_len = torch.randint(max(1, Te // 2), Te + 1, (B,), generator=g)
+        text_len[0] = Te
+    text_mask = torch.arange(Te)[None, :] >= text_len[:, None]
+    img_mask = None
+    if img_pad:
+        img_len = torch.randint(max(1, Ti // 2), Ti + 1, (B,), generator=g)
+        img_len[0] = Ti
+        img_mask = torch.arange(Ti)[None, :] >= img_len[:, None]
+    m2 = img.unsqueeze(0).expand(N, -1, -1, -1)   # mm_s2s_transformer.expand(img, N)
+    res = enc(m1=feats, m2=m2, m1_mask=None, m2_mask=None, m1_key_padding_mask=text_mask,
+              m2_key_padding_mask=img_mask)
+    gout = torch.randn(res.shape, generator=g, dtype=torch.float64)
+    (res * gout).sum().backward()
+    out = dict(d=np.array(d), Di=np.array(Di), N=np.array(N), img=img.numpy(), text_mask=text_mask.numpy(),
+               img_mask=(img_mask.numpy() if img_mask is not None else np.zeros((0,), bool)),
+               res=res.detach().numpy(), gout=gout.numpy())
+    for i, f in enumerate(feats):
+        out[f"feat{i}"] = f.detach().numpy()
+        out[f"grad_feat{i}"] = f.grad.numpy()
+    for k, v in enc.named_parameters():
+        out["param." + k] = v.detach().numpy()
+        out["grad." + k] = (v.grad.numpy() if v.grad is not None else np.zeros_like(v.detach().numpy()))
+    np.savez_compressed(os.path.join(OUT, f"external_{name}.npz"), **out)
+    return res
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference absent; nothing to do")
@@ -181,6 +231,15 @@ def main():
         _make_case(M, F, name, att=att, gate=gate, d=d, Di=Di, B=B, Te=Te, Ti=Ti,
                    text_pad=tp, img_pad=ip, p_img=pi, p_txt=pt, p_attn=pa, seed=100 + i)
         print("wrote", name)
+    ext = [
+        # name, d, Di, N layers, B, Te, Ti, text_pad, img_pad
+        ("packed_2l", 64, 64, 2, 3, 9, 17, True, False),
+        ("packed_3l_masks", 128, 128, 3, 2, 11, 13, True, True),
+        ("separate_2l", 128, 64, 2, 3, 7, 10, False, True),
+    ]
+    for i, (name, d, Di, N, B, Te, Ti, tp, ip) in enumerate(ext):
+        _make_external_case(F, name, d=d, Di=Di, N=N, B=B, Te=Te, Ti=Ti, text_pad=tp, img_pad=ip, seed=200 + i)
+        print("wrote external", name)
 
 
 if __name__ == "__main__":

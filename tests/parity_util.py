@@ -64,6 +64,18 @@ def hip_masks(mm, cfg, ectx, dctx, B, Te, Tt, relu=True):
             out[p + ".act"] = tb(m(c["drop_act"], B * Te * F, pact), Te, F)
         if relu:
             out[p + ".relu"] = tb((c["f1"] > 0).cpu(), Te, F)
+    xc = ectx.get("ext")
+    if xc is not None:       # external multimodal transformer (oracle external_multimodal_transformer sites)
+        Hx = cfg["image_feat_dim"] // 64
+        for i, c in enumerate(xc["layers"]):
+            p = f"encoder.multimodal_transformer.0.layers.{i}"
+            pp, Ti, Fx = c["pp"], c["Ti"], 4 * cfg["image_feat_dim"]
+            if pp > 0:
+                out[p + ".self_attn"] = m(c["drop_sa"], B * Hx * Te * Te, pp).view(B * Hx, Te, Te)
+                out[p + ".cross_attn"] = m(c["drop_ca"], B * Hx * Te * Ti, pp).view(B * Hx, Te, Ti)
+                for s_ in ("drop1", "drop2", "drop3"):
+                    out[f"{p}.{s_}"] = tb(m(c[s_], B * Te * d, pp), Te, d)
+                out[p + ".act"] = tb(m(c["drop_act"], B * Te * Fx, pp), Te, Fx)
     fc = ectx.get("fusion")
     if fc is not None:
         Ti, Di, Tk = fc["Ti"], fc["Di"], fc["Tk"]

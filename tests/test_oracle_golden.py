@@ -42,3 +42,29 @@ def test_fusion_oracle_matches_reference(path):
             g = P[name].grad
             g = np.zeros_like(z[k]) if g is None else g.numpy()
             np.testing.assert_allclose(g, z[k], rtol=1e-9, atol=1e-10, err_msg=name)
+
+
+@pytest.mark.parametrize("path", golden_files("external_"), ids=lambda p: p.split("/")[-1])
+def test_external_transformer_oracle_matches_reference(path):
+    """the oracle's ExternalMultimodalTransformerEncoder restatement vs the
+    reference's own fuse.py run (oracle/gen_golden.py _make_external_case), float64, exact."""
+    z = np.load(path)
+    pre = "encoder.multimodal_transformer.0."
+    P = {pre + k[len("param."):]: torch.from_numpy(z[k]).clone().requires_grad_(True)
+         for k in z.files if k.startswith("param.")}
+    N = int(z["N"])
+    feats = [torch.from_numpy(z[f"feat{i}"]).clone().requires_grad_(True) for i in range(N)]
+    img_mask = torch.from_numpy(z["img_mask"]) if z["img_mask"].size else None
+    cfg = R.base_config(SA_attention_dropout=0.0)
+    res = R.external_multimodal_transformer(P, feats, torch.from_numpy(z["img"]), torch.from_numpy(z["text_mask"]),
+                                            img_mask, cfg, dtype=torch.float64)
+    np.testing.assert_allclose(res.detach().numpy(), z["res"], rtol=1e-9, atol=1e-10)
+    (res * torch.from_numpy(z["gout"])).sum().backward()
+    for i, f in enumerate(feats):
+        np.testing.assert_allclose(f.grad.numpy(), z[f"grad_feat{i}"], rtol=1e-8, atol=1e-10)
+    for k in z.files:
+        if k.startswith("grad."):
+            name = pre + k[len("grad."):]
+            g = P[name].grad
+            g = np.zeros_like(z[k]) if g is None else g.numpy()
+            np.testing.assert_allclose(g, z[k], rtol=1e-8, atol=1e-10, err_msg=name)
