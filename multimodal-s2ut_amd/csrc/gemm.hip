@@ -371,6 +371,12 @@ MMS_DEV void tile_coords(int bid, int tiles_m, int tiles_n, int total, int& z, i
 }
 
 template <int EPI>
+constexpr bool epi_drops() {
+  return EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GELU_DROP ||
+         EPI == MMS_EPI_GELU_DROP_BWD;
+}
+
+template <int EPI>
 MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4], int bm, int bn,
                              int wm, int wn, int wid, int lane, void* Cz, const h16* auxz) {
   float* stage = reinterpret_cast<float*>(smem) + wid * 64 * 64;
@@ -432,6 +438,19 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
     }
   }
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  constexpr bool DROPS = EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GELU_DROP ||
+                         EPI == MMS_EPI_GELU_DROP_BWD;
+  // the seed / high-counter half of the dropout hash is one constant for all 64 of this lane's
+  // counters whenever they share the high word (always, unless the run straddles a 2^33
+  // boundary): one mixer per pair of elements instead of two (bit-identical to mms_keep4)
+  uint32_t hmix = 0;
+  bool same_hi = false;
+  if (DROPS && P.thresh) {
+    const uint64_t cf = P.offset + (uint64_t)m0 * P.ld_rng + n;
+    const uint64_t cl = P.offset + (uint64_t)(m0 + 56) * P.ld_rng + n + 7;
+    same_hi = mms_same_hi(cf, cl) && ((cf & 1) == 0) && ((P.ld_rng & 1) == 0);
+    hmix = mms_hi_mix(P.seed, cf);
+  }
 #pragma unroll
   for (int pass = 0; pass < 8; ++pass) {
     const int m = m0 + 8 * pass;
@@ -441,12 +460,16 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] = x[e] * P.alpha + bv[e];
     bool keep[8] = {true, true, true, true, true, true, true, true};
-    if ((EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GELU_DROP ||
-         EPI == MMS_EPI_GELU_DROP_BWD) && P.thresh) {
+    if (DROPS && P.thresh) {
       const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
       bool k0[4], k1[4];
-      mms_keep4(P.seed, c0, P.thresh, k0);
-      mms_keep4(P.seed, c0 + 4, P.thresh, k1);
+      if (same_hi) {
+        mms_keep4_hi(hmix, c0, P.thresh, k0);
+        mms_keep4_hi(hmix, c0 + 4, P.thresh, k1);
+      } else {
+        mms_keep4(P.seed, c0, P.thresh, k0);
+        mms_keep4(P.seed, c0 + 4, P.thresh, k1);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) { keep[e] = k0[e]; keep[e + 4] = k1[e]; }
     }

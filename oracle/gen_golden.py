@@ -234,8 +234,9 @@ def main():
     ext = [
         # name, d, Di, N layers, B, Te, Ti, text_pad, img_pad
         ("packed_2l", 64, 64, 2, 3, 9, 17, True, False),
-        ("packed_3l_masks", 128, 128, 3, 2, 11, 13, True, True),
-        ("separate_2l", 128, 64, 2, 3, 7, 10, False, True),
+        ("packed_3l_masks", 64, 64, 3, 2, 11, 13, True, True),
+        ("heads2_2l", 64, 128, 2, 2, 6, 9, True, True),
+        ("separate_2l", 96, 64, 2, 3, 7, 10, False, True),
     ]
     for i, (name, d, Di, N, B, Te, Ti, tp, ip) in enumerate(ext):
         _make_external_case(F, name, d=d, Di=Di, N=N, B=B, Te=Te, Ti=Ti, text_pad=tp, img_pad=ip, seed=200 + i)
