@@ -246,6 +246,10 @@ def main():
                     help="detr = BASELINE configs[4]: DETR feats [100, 256], SA_image_dropout 0.5, "
                          "modality_dropout = audio_dropout = 0.5")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--graph", choices=("on", "off"), default="off",
+                    help="replay each training step as a captured HIP graph (world size 1).  Off by "
+                         "default: ROCm 7 executes the captured step without the weight-gradient "
+                         "side stream's overlap (22.6 ms vs 18.3 ms eager, DESIGN.md §7)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gemm-timing", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -265,15 +269,18 @@ def main():
                                                              modality_dropout=0.5, audio_dropout=0.5)
                                                         if detr else {}))
     model = mm.MMS2UTModel(cfg, device=device).init_params(seed=1)
-    tr = trainer_mod.Trainer(model, lr=5e-4, world_size=world, bucket_mb=args.bucket_mb)
+    graph = args.graph == "on"
+    tr = trainer_mod.Trainer(model, lr=5e-4, world_size=world, bucket_mb=args.bucket_mb, graph=graph)
     fe = frontend_mod.FbankFrontend(device)
     nb = cycle_batches(args.steps, args.nbatches)
     batches = make_batches(cfg, rank, nb, args.max_tokens, device, fe, img_tokens=img_tokens)
 
-    def step(i):
+    def step(i, eager=False, draws=None):
         wb, batch = batches[i % len(batches)][:2]
-        batch.src = fe(wb)
-        tr.train_step(batch)
+
+        def frontend():     # GPU fbank + CMVN of the resident waveforms, part of the step
+            batch.src = fe(wb)
+        tr.train_step(batch, prologue=frontend, eager=eager, draws=draws)
 
     # untimed loss-scale settling: the fp16 optimizer starts at scale 128 (fairseq --fp16-init-scale)
     # and skips the update of every overflowing step while it halves the scale; run until a step
@@ -287,6 +294,20 @@ def main():
             break
     for i in range(args.warmup):
         step(i)
+    n_graphs = 0
+    if graph:
+        # capture every (batch, modality-dropout branch) the timed window can meet, so no capture
+        # lands inside it (each first encounter is one eager update + a capture; replays follow)
+        branches = [(0.99, 0.99)]
+        if cfg["modality_dropout"] > 0:
+            if cfg["audio_dropout"] > 0:
+                branches.append((0.0, 0.0))
+            if cfg["audio_dropout"] < 1:
+                branches.append((0.0, 0.99))
+        for i in range(len(batches)):
+            for dr in branches:
+                step(i, draws=[dr])
+        n_graphs = len(tr.graphs)
     base = args.warmup   # the timed batch sequence does not depend on how many settling steps ran
     def timed(profile):
         """K steps between barrier + synchronize on both sides -> (seconds, host issue seconds, GEMM stats).
@@ -303,10 +324,19 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        prof = None
+        if not profile and os.environ.get("MMS2UT_HOST_PROFILE"):
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(base + i)
+            step(base + i, eager=profile)
         t_issue = time.perf_counter()  # host finished enqueueing (host-bound if ~ t1)
+        if prof is not None:
+            import pstats
+            prof.disable()
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(40)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -403,6 +433,7 @@ def main():
                          "dominant": dominant,
                          "classes": class_lines,
                          "host_issue_ms_per_step": 1e3 * (t_issue - t0) / args.steps,
+                         "hip_graph": {"enabled": graph, "graphs": n_graphs},
                          "roofline_pass_ms_per_step": (1e3 * t_prof / args.steps) if t_prof else None,
                          "note": "achieved = SURVEY §8d algorithmic GEMM FLOPs (true lengths, 3x fwd, "
                                  "multi-head attention products excluded) / summed HIP-event durations of "

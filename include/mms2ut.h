@@ -118,6 +118,13 @@ int mms2ut_transpose_batch(const mms2ut_half* src, mms2ut_half* dst, const mms2u
 /* `waiter` waits for all work enqueued on `signaler` so far (event record + stream wait).
  * Forks/joins the weight-gradient side stream (the reference's DDP/autograd stream overlap). */
 int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler);
+/* HIP-graph replay of the training step: every dropout kernel adds *delta (a device uint64) to
+ * the seed it was launched or captured with; delta == NULL (the default) leaves seeds unchanged.
+ * mms2ut_step_seed_advance(delta, inc) is the first node of a captured step (delta += inc), so
+ * each replay draws fresh masks (fairseq reseeds torch's generator per update in
+ * Trainer.train_step; here the per-update seed lives on the device).                           */
+int mms2ut_bind_step_seed(const uint64_t* delta);
+int mms2ut_step_seed_advance(uint64_t* delta, uint64_t inc, hipStream_t stream);
 /* new stream whose kernels may only run on the CUs whose bit is set in mask[nwords]
  * (hipExtStreamCreateWithCUMask); used for the weight-gradient side stream.                    */
 int mms2ut_stream_create_cumask(const uint32_t* mask, int nwords, hipStream_t* out);

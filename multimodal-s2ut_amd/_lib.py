@@ -109,6 +109,8 @@ SIGNATURES = {
     "mms2ut_grad_sqnorm": (i32, [vp, i64, vp, i32, vp]),
     "mms2ut_grad_norm_finalize": (i32, [vp, i32, vp, vp, vp]),
     "mms2ut_stream_wait": (i32, [vp, vp]),
+    "mms2ut_bind_step_seed": (i32, [vp]),
+    "mms2ut_step_seed_advance": (i32, [vp, u64, vp]),
     "mms2ut_optim_prepare": (i32, [vp, f32, f32, f32, f32, f32, f32, f32, f32, vp]),
     "mms2ut_adam_fp16_master": (i32, [vp, vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, vp]),
     "mms2ut_fbank_frames": (i32, [vp, i32, vp, vp]),

@@ -159,6 +159,7 @@ MMS_DEV float xsum16_32(float v) {
 // barriers.
 template <int HD, int NW, bool SHORT = false>
 __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) attn_fwd_kernel(AttnP P) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   constexpr int OWN = 16 * NW;  // query rows owned by the block (16 per wave)
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
   constexpr int KROWS = SHORT ? 2 * KB : KB;
@@ -336,6 +337,7 @@ __global__ void __launch_bounds__(256) attn_bwd_prep_rows_kernel(AttnP P, long n
 // ============================================================================ backward: dK, dV
 template <int HD, int NW>
 __global__ void __launch_bounds__(64 * NW) attn_bwd_kv_kernel(AttnP P) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   constexpr int OWN = 16 * NW;  // keys owned by the block
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
   __shared__ __attribute__((aligned(16))) h16 sQ[QB * LD];
@@ -435,6 +437,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_kv_kernel(AttnP P) {
 // ============================================================================ backward: dQ
 template <int HD, int NW>
 __global__ void __launch_bounds__(64 * NW) attn_bwd_q_kernel(AttnP P) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   constexpr int OWN = 16 * NW;
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16;
   __shared__ __attribute__((aligned(16))) h16 sK[KB * LD];
@@ -539,6 +542,7 @@ struct FusedCfg {
 
 template <int HD, int NKC>
 __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   using F = FusedCfg<HD, NKC>;
   constexpr int LD = Tile<HD>::LD, NKK = HD / 32, NDT = HD / 16, CH = F::CH;
   constexpr int QC = F::QC, TKP = F::TKP, LDS_T = F::LDS_T, NQT = F::NQT, NDW = NDT / F::DSPLIT;
@@ -896,3 +900,7 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
     return mms::check_launch("mha_varlen_bwd_q");
   });
 }
+
+namespace mms {
+int bind_step_seed_attention(const uint64_t* d) { return mms_bind_step_seed_tu(d); }
+}  // namespace mms

@@ -122,6 +122,36 @@ extern "C" int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Step-seed indirection (HIP-graph replay of the training step; common.h mms_step_seed).
+// ------------------------------------------------------------------------------------------
+namespace mms {
+int bind_step_seed_gemm(const uint64_t* d);
+int bind_step_seed_attention(const uint64_t* d);
+int bind_step_seed_ops(const uint64_t* d);
+}  // namespace mms
+
+extern "C" int mms2ut_bind_step_seed(const uint64_t* delta) {
+  if (mms::bind_step_seed_gemm(delta) || mms::bind_step_seed_attention(delta) || mms::bind_step_seed_ops(delta) ||
+      mms_bind_step_seed_tu(delta)) {
+    mms::set_error("bind_step_seed: hipMemcpyToSymbol failed");
+    return 1;
+  }
+  return 0;
+}
+
+namespace {
+__global__ void step_seed_advance_kernel(uint64_t* delta, uint64_t inc) {
+  if (threadIdx.x == 0) delta[0] += inc;
+}
+}  // namespace
+
+extern "C" int mms2ut_step_seed_advance(uint64_t* delta, uint64_t inc, hipStream_t s) {
+  MMS_REQUIRE(delta, "step_seed_advance: null delta");
+  hipLaunchKernelGGL(step_seed_advance_kernel, dim3(1), dim3(64), 0, s, delta, inc);
+  return mms::check_launch("step_seed_advance");
+}
+
+// ------------------------------------------------------------------------------------------
 // A stream restricted to a subset of CUs (bit i of mask = logical CU i), for the weight-gradient
 // side stream: the dgrad chain on the main stream then keeps the remaining CUs to itself.
 // ------------------------------------------------------------------------------------------

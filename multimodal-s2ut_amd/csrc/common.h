@@ -95,6 +95,19 @@ MMS_DEV void mms_keep4_hi(uint32_t hi_mix, uint64_t ctr0, uint32_t thresh, bool 
     for (int e = 0; e < 4; ++e) k[e] = mms_keep_hi(hi_mix, ctr0 + e, thresh);
   }
 }
+// Step-seed indirection for HIP-graph replay.  A captured launch keeps the host seed it was
+// captured with; the per-step variation comes from a device-resident 64-bit delta that every
+// dropout kernel adds to its seed argument on entry (the step's first kernel advances it, see
+// mms2ut_step_seed_advance).  Unbound (the eager default) => delta 0, masks unchanged.  One copy
+// of the pointer per translation unit; mms2ut_bind_step_seed binds all of them.
+static __device__ const uint64_t* mms_step_seed_delta = nullptr;
+MMS_DEV uint64_t mms_step_seed(uint64_t s) {
+  const uint64_t* d = mms_step_seed_delta;
+  return d ? s + *d : s;
+}
+static inline int mms_bind_step_seed_tu(const uint64_t* d) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(mms_step_seed_delta), &d, sizeof(d)) == hipSuccess ? 0 : 1;
+}
 static inline uint32_t mms_drop_thresh(float p) {
   if (p <= 0.f) return 0u;
   double t = (double)p * 65536.0 + 0.5;

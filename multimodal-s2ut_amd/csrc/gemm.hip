@@ -513,6 +513,7 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
 
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   int z, tm, tn;
   tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
@@ -621,6 +622,7 @@ MMS_DEV void wait_vm() {
 
 template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
 __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
   int z, tm, tn;
   tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
@@ -768,6 +770,7 @@ MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
 
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NT, 2) gemm_dma32_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[ST32 * 2 * T32_BYTES];
   int z, tm, tn;
   tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
@@ -873,6 +876,7 @@ MMS_DEV void dma_slot2(__amdgpu_buffer_rsrc_t rs, char* img, long ld, int row0, 
 
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[RING2 * SLOT2];
   int z, tm, tn;
   tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
@@ -958,6 +962,7 @@ __global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, i
 // is issued behind it, leaving RING-3 slots in flight across the barrier.
 template <bool A_KC, bool B_KC, int EPI, int RING>
 __global__ void __launch_bounds__(NT2, 2) gemm256p_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[RING * SLOT2];
   int z, tm, tn;
   tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
@@ -1361,3 +1366,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (!a_kc && b_kc) return launch_epi<false, true>(a->epi, P, tm, tn, nz, s);
   return launch_epi<false, false>(a->epi, P, tm, tn, nz, s);
 }
+
+namespace mms {
+int bind_step_seed_gemm(const uint64_t* d) { return mms_bind_step_seed_tu(d); }
+}  // namespace mms

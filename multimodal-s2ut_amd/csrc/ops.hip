@@ -28,6 +28,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, 
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      long rows, int D, float eps, long grp, long grp_out,
                                                      float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -96,6 +97,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy,
                                                      h16* __restrict__ dx, float* __restrict__ part,
                                                      long rows, int D, h16* __restrict__ dxd, float p,
                                                      uint32_t thresh, uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   __shared__ float red[4][2][CPL * 256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = D >> 2;
@@ -213,6 +215,8 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
                                                        uint32_t thresh, uint64_t seed, uint64_t offset,
                                                        long dgrp, long dgrp_out, float pin, uint32_t thin,
                                                        uint64_t sin, uint64_t oin) {
+  if (thresh) seed = mms_step_seed(seed);
+  if (thin) sin = mms_step_seed(sin);
   __shared__ __attribute__((aligned(16))) float red[4][2][C8 * 256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
   const float dscale = thresh ? 1.f / (1.f - p) : 1.f;
@@ -412,6 +416,7 @@ __global__ void __launch_bounds__(256) softmax_fwd_kernel(const h16* __restrict_
                                                           const uint8_t* __restrict__ key_mask, long ld_mask,
                                                           int causal, int extra_key, float p, uint32_t thresh,
                                                           uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)Z * Tq) return;
@@ -478,6 +483,7 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const h16* __restrict_
                                                           h16* __restrict__ dS, int Z, int H, int Tq, int Tk,
                                                           long ldS, float p, uint32_t thresh, uint64_t seed,
                                                           uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)Z * Tq) return;
@@ -520,6 +526,7 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const h16* __restrict_
 // ============================================================================ elementwise
 __global__ void dropout_kernel(const h16* __restrict__ x, h16* __restrict__ y, long n, float p,
                                uint32_t thresh, uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const float ds = 1.f / (1.f - p);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float v = (float)x[i];
@@ -528,6 +535,7 @@ __global__ void dropout_kernel(const h16* __restrict__ x, h16* __restrict__ y, l
 }
 
 __global__ void dropout_mask_kernel(uint8_t* keep, long n, uint32_t thresh, uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     keep[i] = thresh ? (uint8_t)mms_keep(seed, offset + i, thresh) : 1;
 }
@@ -536,6 +544,7 @@ __global__ void encoder_embed_kernel(const h16* __restrict__ h, const h16* __res
                                      const int* __restrict__ len, h16* __restrict__ x, int B, int T,
                                      int D, float scale, float p, uint32_t thresh, uint64_t seed,
                                      uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const long n4 = (long)B * T * (D / 4);
   const float ds = thresh ? 1.f / (1.f - p) : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
@@ -559,6 +568,7 @@ __global__ void encoder_embed_kernel(const h16* __restrict__ h, const h16* __res
 __global__ void scale_dropout_bwd_kernel(const h16* __restrict__ dx, h16* __restrict__ dh, long n,
                                          float scale, float p, uint32_t thresh, uint64_t seed,
                                          uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const float ds = thresh ? 1.f / (1.f - p) : 1.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float v = (float)dx[i] * scale;
@@ -572,6 +582,7 @@ __global__ void token_embed_fwd_kernel(const int64_t* __restrict__ tok, const h1
                                        const h16* __restrict__ pos, h16* __restrict__ x, int B, int T,
                                        int D, int pad, float scale, float p, uint32_t thresh,
                                        uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const int lane = threadIdx.x & 63;
   const long bt = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bt >= (long)B * T) return;
@@ -598,6 +609,7 @@ __global__ void token_embed_fwd_kernel(const int64_t* __restrict__ tok, const h1
 __global__ void token_embed_bwd_kernel(const int64_t* __restrict__ tok, const h16* __restrict__ dx,
                                        float* __restrict__ dE, int B, int T, int D, int pad, float scale,
                                        float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
   const int lane = threadIdx.x & 63;
   const long bt = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bt >= (long)B * T) return;
@@ -1044,3 +1056,7 @@ extern "C" int mms2ut_copy2d(const h16* src, int64_t lds, h16* dst, int64_t ldd,
                      (long)ldd, (long)rows, cols);
   return mms::check_launch("copy2d");
 }
+
+namespace mms {
+int bind_step_seed_ops(const uint64_t* d) { return mms_bind_step_seed_tu(d); }
+}  // namespace mms

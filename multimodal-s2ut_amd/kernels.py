@@ -250,6 +250,8 @@ class _Side:
     override = 0
     keep = []
     ws = {}
+    retain = False     # graph mode: regrown workspaces are retired, never freed (graphs bake pointers)
+    retired = []
 
 
 class _SideRegion:
@@ -323,7 +325,7 @@ def _workspace(key, numel, device, dtype=torch.float32):
         buf = _Side.ws.get(key)
         if buf is None or buf.numel() < numel:
             if buf is not None:
-                _Side.keep.append(buf)
+                (_Side.retired if _Side.retain else _Side.keep).append(buf)
             buf = torch.empty(max(numel, 1 << 20), dtype=dtype, device=device)
             _Side.ws[key] = buf
         return buf[:numel]
@@ -674,6 +676,25 @@ def grad_norm_check(buf, world, rank, ost, stage):
 def scale_f16(x, alpha):
     call("mms2ut_scale_f16", x.data_ptr(), x.numel(), float(alpha), _s())
     return x
+
+
+_bound_seed = [None]
+
+
+def bind_step_seed(delta):
+    """Bind (or with None unbind) the device step-seed delta every dropout kernel adds to its seed
+    (graph replay; include/mms2ut.h mms2ut_bind_step_seed).  Process-global; rebinding the bound
+    tensor is free."""
+    if delta is _bound_seed[0]:
+        return
+    if delta is not None:
+        assert delta.is_cuda and delta.dtype == torch.int64 and delta.numel() == 1
+    call("mms2ut_bind_step_seed", None if delta is None else delta.data_ptr())
+    _bound_seed[0] = delta
+
+
+def step_seed_advance(delta, inc):
+    call("mms2ut_step_seed_advance", delta.data_ptr(), int(inc) & ((1 << 64) - 1), _s())
 
 
 def accum_f16_f32(acc, x):

@@ -469,6 +469,8 @@ class MMS2UTModel:
         self.dspec = DecoderSpec.main(cfg)
         self.aux_specs = {t["name"]: DecoderSpec.aux(cfg, t) for t in aux_tasks(cfg) if t["type"] == "transformer"}
         self._pos = {}   # sinusoidal tables of other widths (multitask decoders)
+        self.retain_tables = False   # graph mode: grown tables retire the old one (graphs bake it)
+        self._retired = []
         self.np_rng = np.random  # modality-dropout draws use the global numpy stream (reference)
         # autograd anchor: the model's output is connected to the graph through this leaf
         self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
@@ -610,11 +612,15 @@ class MMS2UTModel:
         if isinstance(which, int):       # a decoder width other than the unit decoder's
             tab = self._pos.get(which)
             if tab is None or T + 2 > tab.shape[0]:
+                if tab is not None and self.retain_tables:
+                    self._retired.append(tab)
                 tab = sinusoidal_table(max(T + 2, 1026), which).to(self.device, F16)
                 self._pos[which] = tab
             return tab
         tab = self.enc_pos if which == "enc" else self.dec_pos
         if T + 2 > tab.shape[0]:
+            if self.retain_tables:
+                self._retired.append(tab)
             dim = tab.shape[1]
             tab = sinusoidal_table(T + 2, dim).to(self.device, F16)
             if which == "enc":

@@ -12,6 +12,16 @@ gradients, then multiply_grads(world/sample_size) with sample_size summed over m
 ranks), FP16Optimizer.clip_grad_norm(10), DynamicLossScaler (scale window 2^14/world/update_freq),
 Trainer._check_grad_norms.
 
+HIP-graph mode (``graph=True``, world size 1): the whole update -- forward, hand-written backward
+(both streams), loss scaling, grad norm and the Adam update -- is captured once per (micro-batch
+set, modality-dropout branch) with torch.cuda.graph and replayed, so a step costs one graph launch
+instead of ~2000 kernel launches issued from Python.  What varies between replays lives on the
+device: the dropout seed (a device step counter every dropout kernel adds to its seed,
+include/mms2ut.h mms2ut_bind_step_seed), the loss scale, step count and learning rate (optimizer
+state vector).  The modality-dropout draws (two numpy draws per forward, as the reference) are
+made before the step and select the graph.  Batches must stay resident (the graph bakes their
+device pointers): the first step on a new batch runs eagerly, then captures.
+
 Buffer access: the Adam update and the gradient zeroing run deferred on the side stream
 (optim.FP16Adam.step).  Call ``trainer.sync()`` (or ``model.params.await_all()``) before reading
 ``params.flat`` / ``params.grad`` / ``opt.master`` directly after a step; ``state_dict``,
@@ -19,6 +29,7 @@ Buffer access: the Adam update and the gradient zeroing run deferred on the side
 """
 import os
 
+import numpy as np
 import torch
 
 from . import kernels as K
@@ -28,11 +39,27 @@ from .parallel import GradAllReducer, GradNormCheck, all_reduce_scalars
 
 # log slots (all-reduced SUM over ranks every step)
 LOG_LOSS, LOG_NLL, LOG_NTOKENS, LOG_NSENT, LOG_SS_OVER_WORLD = range(5)
+# per-update increment of the device step seed (odd 64-bit golden-ratio constant)
+STEP_SEED_INC = 0x9E3779B97F4A7C15
+
+
+class _ScriptedDraws:
+    """Stands in for numpy's global stream inside the model while a graph-mode step runs: the
+    step's modality-dropout draws are made up front (they select the graph) and handed out here."""
+
+    def __init__(self):
+        self.vals = []
+
+    def random(self):
+        if not self.vals:
+            raise RuntimeError("graph-mode trainer: unexpected modality-dropout draw")
+        return self.vals.pop(0)
 
 
 class Trainer:
     def __init__(self, model, lr=5e-4, betas=(0.9, 0.98), clip_norm=10.0, warmup_updates=10000,
-                 warmup_init_lr=1e-7, init_scale=128.0, bucket_mb=64.0, world_size=1, update_freq=1):
+                 warmup_init_lr=1e-7, init_scale=128.0, bucket_mb=64.0, world_size=1, update_freq=1,
+                 graph=False, device_seed=None):
         self.model = model
         self.cfg = model.cfg
         self.update_freq = int(update_freq)
@@ -55,19 +82,53 @@ class Trainer:
             if K._Side.stream is None:
                 K._Side.stream = K.make_side_stream(model.params.flat.device)
                 K._Side.ptr = K._Side.stream.cuda_stream
+        # device step seed: every update draws its dropout masks from (base seed + step * INC, offsets
+        # from 0); graph mode needs it (a replay cannot change a kernel's seed argument), eager mode
+        # can opt in (bit-identical to graph mode)
+        self.graph_mode = bool(graph)
+        self.device_seed = self.graph_mode if device_seed is None else bool(device_seed)
+        if self.graph_mode and not self.device_seed:
+            raise ValueError("graph mode needs the device step seed")
+        if self.device_seed:
+            self.seed_delta = torch.zeros(1, dtype=torch.int64, device=model.params.flat.device)
+            self.seed_base = model.drop.seed
+        if self.graph_mode:
+            if world_size != 1 or self.stream is None:
+                raise ValueError("graph mode: single process on a GPU (world size 1) only")
+            self.opt.defer = False        # no cross-step event handoff: each replay is self-contained
+            self.graphs = {}
+            self.pool = torch.cuda.graph_pool_handle()
+            self.draws = _ScriptedDraws()
+            model.np_rng = self.draws
+            # buffers baked into a captured graph must outlive it: regrown scratch / tables are retired,
+            # never freed
+            K._Side.retain = True
+            model.retain_tables = True
 
     def sync(self):
         """Wait (on the current stream) for every deferred optimizer chunk of the last step."""
         self.model.params.await_all()
 
-    def train_step(self, batches):
+    def train_step(self, batches, prologue=None, eager=False, draws=None):
         """batches: one runtime.DeviceBatch or a list of ``update_freq`` micro-batches (fairseq's
         ``samples``).  Returns the device log [loss, nll, ntokens, nsentences, ntokens/world]
-        summed over micro-batches and ranks."""
+        summed over micro-batches and ranks.
+
+        prologue: optional callable run at the start of the step (in graph mode it is captured
+        with it, e.g. the fbank front end refreshing ``batch.src``).  eager=True (graph mode): run
+        this step without capturing or replaying (e.g. for per-kernel timing).  draws (graph mode):
+        explicit (modality, audio) draw pairs per micro-batch instead of numpy's stream (to capture
+        a chosen modality-dropout branch ahead of time)."""
         if not isinstance(batches, (list, tuple)):
             batches = [batches]
         if len(batches) != self.update_freq:
             raise ValueError(f"train_step: {len(batches)} micro-batches for update_freq {self.update_freq}")
+        if self.device_seed:
+            K.bind_step_seed(self.seed_delta)
+        if self.graph_mode:
+            return self._graph_step(batches, prologue, eager, draws)
+        if prologue is not None:
+            prologue()
         if self.stream is None:
             return self._train_step(batches)
         cur = torch.cuda.current_stream()
@@ -77,11 +138,54 @@ class Trainer:
         cur.wait_stream(self.stream)
         return log
 
+    def _graph_step(self, batches, prologue, eager, draws):
+        m, cfg = self.model, self.cfg
+        branches = []
+        for i, b in enumerate(batches):   # the reference's two draws per training forward with images
+            if cfg["fusion"] and b.imgs is not None:
+                mod_p, aud_p = draws[i] if draws is not None else (np.random.random(), np.random.random())
+                self.draws.vals += [mod_p, aud_p]
+                branches.append(None if not mod_p < cfg["modality_dropout"] else
+                                "audio" if aud_p < cfg["audio_dropout"] else "image")
+            else:
+                branches.append(None)
+        key = (tuple(id(b) for b in batches), tuple(branches))
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        entry = None if eager else self.graphs.get(key)
+        if entry is None:
+            # first time: a real eager step (lazy allocations, table growth), then capture the same
+            # step (capture executes nothing) with the same draws
+            vals = list(self.draws.vals)
+            with torch.cuda.stream(self.stream):
+                if prologue is not None:
+                    prologue()
+                log = self._train_step(batches)
+            if not eager:
+                self.draws.vals = vals
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
+                    if prologue is not None:
+                        prologue()
+                    self._train_step(batches)
+                self.graphs[key] = (g, list(batches))    # keep the batches (their pointers are baked)
+            self.draws.vals = []
+        else:
+            self.draws.vals = []
+            with torch.cuda.stream(self.stream):
+                entry[0].replay()
+            log = self.log
+        cur.wait_stream(self.stream)
+        return log
+
     def _train_step(self, batches):
         cfg = self.cfg
         m = self.model
         m.train()
         n = len(batches)
+        if self.device_seed:
+            K.step_seed_advance(self.seed_delta, STEP_SEED_INC)
+            m.drop.reset(self.seed_base)
         if n > 1 and self.acc is None:
             self.acc = torch.zeros(m.params.numel, dtype=torch.float32, device=m.params.flat.device)
         self.log.zero_()
