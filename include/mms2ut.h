@@ -74,6 +74,13 @@ typedef struct mms2ut_gemm_args {
    * partials of the bias gradient (replaces a separate column-sum pass over dy).             */
   float* rowsum;
   int64_t ld_rowsum;
+  /* split-K with a fused-epilogue fixup (any epi but MMS_EPI_F32, batch 1, splitk > 1, N % 4 == 0):
+   * the splits write alpha-scaled fp32 partials to splitk_ws[s][M][N] (>= splitk*M*N floats),
+   * then one pass sums them in split order and applies the epilogue exactly as the unsplit GEMM
+   * (same bias / residual / dropout counters).  For the short-M shapes (decoder tokens) whose
+   * unsplit grid covers a tenth of the CUs.                                                       */
+  float* splitk_ws;
+  int64_t splitk_ws_floats;
 } mms2ut_gemm_args;
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);

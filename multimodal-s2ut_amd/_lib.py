@@ -34,6 +34,7 @@ class GemmArgs(C.Structure):
         ("seed", u64), ("offset", u64),
         ("ld_rng", i64),
         ("rowsum", vp), ("ld_rowsum", i64),
+        ("splitk_ws", vp), ("splitk_ws_floats", i64),
     ]
 
 

@@ -32,8 +32,18 @@ def _deps_mtime():
     return max(ts)
 
 
-def _compile(src):
+def _headers_mtime():
+    ts = [os.path.getmtime(os.path.join(CSRC, f)) for f in os.listdir(CSRC) if f.endswith(".h")]
+    ts += [os.path.getmtime(os.path.join(INCLUDE, f)) for f in os.listdir(INCLUDE)]
+    ts.append(os.path.getmtime(__file__))
+    return max(ts)
+
+
+def _compile(src, force=True):
     obj = os.path.join(OBJDIR, src.replace(".hip", ".o"))
+    if not force and os.path.exists(obj) and \
+            os.path.getmtime(obj) >= max(os.path.getmtime(os.path.join(CSRC, src)), _headers_mtime()):
+        return obj      # object newer than its source and every header: reuse
     cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -47,7 +57,7 @@ def build(force=False, verbose=True):
         return LIB
     srcs = _sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
+        objs = list(ex.map(lambda f: _compile(f, force), srcs))
     tmp = LIB + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -1160,6 +1160,48 @@ int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   return mms::check_launch("gemm");
 }
 
+// Split-K fixup: sum the alpha-scaled fp32 partials of the splits (split order, so the result does
+// not depend on scheduling) and run the unsplit GEMM's epilogue on them -- same bias / residual /
+// gate operands and the same dropout counters (m * ld_rng + n), so masks are identical.  One thread
+// per 8 columns of a row: 32-B slab reads, 16-B operand loads / stores.
+template <int EPI>
+__global__ void __launch_bounds__(256) splitk_fixup_kernel(GemmP P, const float* __restrict__ ws, int nsplit) {
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
+  const int ncg = (P.N + 7) >> 3;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)P.M * ncg) return;
+  const int m = (int)(i / ncg), n = (int)(i % ncg) * 8;
+  const long slab = (long)P.M * P.N;
+  const float* src = ws + (long)m * P.N + n;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n + 7 < P.N) {
+    for (int s = 0; s < nsplit; ++s) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src + s * slab);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + s * slab + 4);
+      v[0] += lo[0]; v[1] += lo[1]; v[2] += lo[2]; v[3] += lo[3];
+      v[4] += hi[0]; v[5] += hi[1]; v[6] += hi[2]; v[7] += hi[3];
+    }
+  } else {
+    for (int s = 0; s < nsplit; ++s)
+      for (int e = 0; e < 8; ++e)
+        if (n + e < P.N) v[e] += src[s * slab + e];
+  }
+  epilogue_store8<EPI>(P, P.C, P.aux, m, n, v);
+}
+
+int launch_fixup(int epi, const GemmP& P, const float* ws, int nsplit, hipStream_t s) {
+  const long n = (long)P.M * ((P.N + 7) / 8);
+  dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((splitk_fixup_kernel<E>), grid, block, 0, s, P, ws, nsplit); break;
+    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
+#undef CASE
+    default: mms::set_error("gemm: bad epilogue %d for the split-K fixup", epi); return 1;
+  }
+  return mms::check_launch("splitk_fixup");
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -1301,6 +1343,38 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.bdiv = a->bdiv > 0 ? a->bdiv : 1;
   P.sA1 = a->sA1; P.sA2 = a->sA2; P.sB1 = a->sB1; P.sB2 = a->sB2; P.sC1 = a->sC1; P.sC2 = a->sC2;
   int splitk = a->splitk > 0 ? a->splitk : 1;
+  if (splitk > 1 && a->epi != MMS_EPI_F32) {
+    // split-K + fixup: the splits as an fp32-slab GEMM into the workspace, then the epilogue pass
+    MMS_REQUIRE(a->batch == 1 && !a->rowsum && a->N % 4 == 0, "gemm: split-K fixup needs batch 1, N %% 4 == 0");
+    MMS_REQUIRE(a->splitk_ws && a->splitk_ws_floats >= (int64_t)splitk * a->M * a->N,
+                "gemm: split-K fixup workspace too small (%ld floats for %d x %d x %d)",
+                (long)a->splitk_ws_floats, splitk, a->M, a->N);
+    MMS_REQUIRE(((uintptr_t)a->splitk_ws & 15) == 0, "gemm: split-K workspace must be 16-B aligned");
+    mms2ut_gemm_args b = *a;
+    b.C = a->splitk_ws; b.ldc = a->N; b.sC1 = b.sC2 = 0; b.sCsplit = (int64_t)a->M * a->N;
+    b.epi = MMS_EPI_F32; b.bias = nullptr; b.aux = nullptr; b.out2 = nullptr; b.dropout_p = 0.f;
+    b.splitk_ws = nullptr;
+    const int rc = gemm_dispatch(&b, stream);
+    if (rc) return rc;
+    GemmP F{};
+    F.C = a->C; F.M = a->M; F.N = a->N; F.K = a->K; F.ldc = a->ldc;
+    F.alpha = 1.f; F.bias = a->bias;
+    F.aux = a->aux; F.ldaux = a->ldaux; F.out2 = a->out2; F.ldo2 = a->ldo2;
+    F.p = a->dropout_p; F.thresh = mms_drop_thresh(a->dropout_p); F.seed = a->seed; F.offset = a->offset;
+    F.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
+    MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD ||
+                  a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
+    MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");
+    MMS_REQUIRE(a->ldc % 4 == 0 && (!a->aux || (a->ldaux % 4 == 0 && ((uintptr_t)a->aux & 7) == 0)) &&
+                (!a->bias || ((uintptr_t)a->bias & 7) == 0), "gemm: fixup operand alignment");
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    bool v = al16(a->C) && a->ldc % 8 == 0;
+    if (a->aux) v = v && al16(a->aux) && a->ldaux % 8 == 0 && (a->epi != MMS_EPI_GATE || a->N % 8 == 0);
+    if (a->out2) v = v && al16(a->out2) && a->ldo2 % 8 == 0;
+    if (a->bias) v = v && al16(a->bias);
+    F.vec16 = v ? 1 : 0;
+    return launch_fixup(a->epi, F, a->splitk_ws, splitk, stream);
+  }
   MMS_REQUIRE(splitk == 1 || a->epi == MMS_EPI_F32, "gemm: split-K needs the fp32 slab epilogue");
   int kchunk = (a->K + splitk - 1) / splitk;
   kchunk = ((kchunk + BK - 1) / BK) * BK;

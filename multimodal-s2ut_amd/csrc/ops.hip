@@ -349,26 +349,30 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
   }
 }
 
-// [nparts][ncol] fp32 -> ncol: a block owns 64 columns, its 16 waves split the parts; fixed
-// summation order (deterministic).
+// [nparts][ncol] fp32 -> ncol: a block owns 16 columns; its 1024 threads are 64 part slots x 16
+// columns (lane l: column l & 15, slot 4w + (l >> 4)), slot j summing parts j, j + 64, ... -- 6x the
+// blocks of a 64-column layout, so the L2-hot partials of a LayerNorm backward (~1000 parts x 2D)
+// are read by enough waves to hide their latency.  Fixed summation order (deterministic).
 __global__ void __launch_bounds__(1024) colsum_parts_kernel(const float* __restrict__ part, int nparts, int ncol,
                                                             h16* __restrict__ out, int accumulate) {
-  __shared__ float red[16][64];
+  __shared__ float red[64][17];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int col = lane & 15, slot = 4 * w + (lane >> 4);
+  const int c = blockIdx.x * 16 + col;
   float s = 0.f;
   if (c < ncol) {
 #pragma unroll 4
-    for (int p = w; p < nparts; p += 16) s += part[(long)p * ncol + c];
+    for (int p = slot; p < nparts; p += 64) s += part[(long)p * ncol + c];
   }
-  red[w][lane] = s;
+  red[slot][col] = s;
   __syncthreads();
-  if (w == 0 && c < ncol) {
+  if (threadIdx.x < 16 && blockIdx.x * 16 + (int)threadIdx.x < ncol) {
     float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][lane];
-    if (accumulate) t += (float)out[c];
-    out[c] = (h16)t;
+#pragma unroll 8
+    for (int i = 0; i < 64; ++i) t += red[i][threadIdx.x];
+    const int cc = blockIdx.x * 16 + threadIdx.x;
+    if (accumulate) t += (float)out[cc];
+    out[cc] = (h16)t;
   }
 }
 
@@ -871,7 +875,7 @@ extern "C" int mms2ut_layernorm_bwd_ex(const h16* dy, const h16* x, const h16* g
 extern "C" int mms2ut_colsum_parts(const float* part, int nparts, int ncol, h16* out, int accumulate,
                                    hipStream_t s) {
   if (ncol == 0) return 0;
-  hipLaunchKernelGGL(colsum_parts_kernel, dim3((ncol + 63) / 64), dim3(1024), 0, s, part, nparts,
+  hipLaunchKernelGGL(colsum_parts_kernel, dim3((ncol + 15) / 16), dim3(1024), 0, s, part, nparts,
                      ncol, out, accumulate);
   return mms::check_launch("colsum_parts");
 }

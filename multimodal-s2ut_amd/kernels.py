@@ -82,7 +82,28 @@ def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv
     a.out2, a.ldo2 = _p(out2), int(ldo2)
     a.dropout_p, a.seed, a.offset, a.ld_rng = float(p), int(seed), int(offset), int(ld_rng)
     a.rowsum, a.ld_rowsum = _p(rowsum), int(ld_rowsum)
+    ws = None
+    if splitk == 1 and epi != EPI_F32 and batch == 1 and rowsum is None and _SPLITK_FIX:
+        s = _fixup_splits(M, N, K)
+        if s > 1:
+            ws = _workspace("splitk_fix", s * M * N, C.device)
+            a.splitk, a.splitk_ws, a.splitk_ws_floats = s, ws.data_ptr(), ws.numel()
     call("mms2ut_gemm_f16", a, _s())
+
+
+_SPLITK_FIX = os.environ.get("MMS2UT_SPLITK_FIX", "1") != "0"
+
+
+def _fixup_splits(M, N, K):
+    """Split count for a short-M fused-epilogue GEMM (decoder tokens): its 128x128 grid covers a
+    fraction of the 256 CUs, so K is split until ~512 workgroups (2 per CU) run, each split keeping
+    >= 4 k-tiles (include/mms2ut.h splitk_ws)."""
+    if N % 4 or K < 512:
+        return 1
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    if tiles >= 128:
+        return 1
+    return max(1, min(512 // tiles, K // 256, 16))
 
 
 def gemm_profile_begin(max_launches=100000):
