@@ -46,6 +46,7 @@ struct GemmP {
   float p; uint32_t thresh; uint64_t seed, offset; long ld_rng;
   int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity
   float* rowsum; long ld_rowsum;  // RS kernels: split-K partial A-row sums (bias gradient)
+  int group_m;  // tile-rows per L2 group (tile_coords)
 };
 
 MMS_DEV int swz_mn(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
@@ -355,8 +356,7 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
 // slice, or a batch entry, stays on one XCD.  Inside a z slice tiles go in groups of GROUP_M
 // tile-rows, column by column, so the ~64 blocks an XCD runs at once share 8 A row-panels and 8
 // B column-panels (~3 MiB at K = 768) instead of streaming the whole B operand per row.
-constexpr int GROUP_M = 8;
-MMS_DEV void tile_coords(int bid, int tiles_m, int tiles_n, int total, int& z, int& tm, int& tn) {
+MMS_DEV void tile_coords(int bid, int tiles_m, int tiles_n, int total, int& z, int& tm, int& tn, int GROUP_M) {
   const int q = total / 8, r = total % 8, x = bid % 8;
   const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   const int ntiles = tiles_m * tiles_n;
@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int t
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const h16* A = P.A + z1 * P.sA1 + z2 * P.sA2;
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
   int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const int kbeg = zs * P.kchunk;
@@ -773,7 +773,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_dma32_kernel(GemmP P, int tiles_m,
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[ST32 * 2 * T32_BYTES];
   int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const int kbeg = zs * P.kchunk;
@@ -879,7 +879,7 @@ __global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, i
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[RING2 * SLOT2];
   int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const int kbeg = zs * P.kchunk;
@@ -965,7 +965,7 @@ __global__ void __launch_bounds__(NT2, 2) gemm256p_kernel(GemmP P, int tiles_m, 
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[RING * SLOT2];
   int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn);
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const int kbeg = zs * P.kchunk;
@@ -1268,6 +1268,17 @@ extern "C" int mms2ut_profile_end(float* total_ms, int* launches, double* flops)
 
 static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream);
 
+// tile-rows per L2 group of the tile order (tile_coords); MMS2UT_GEMM_GROUP overrides (A/B runs)
+static int gemm_group_m() {
+  static int g = 0;
+  if (g == 0) {
+    const char* e = getenv("MMS2UT_GEMM_GROUP");
+    g = e ? atoi(e) : 8;
+    if (g < 1) g = 8;
+  }
+  return g;
+}
+
 extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (!g_prof.on || g_prof.n >= g_prof.cap) return gemm_dispatch(a, stream);
   const int i = g_prof.n++;
@@ -1385,6 +1396,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.out2 = a->out2; P.ldo2 = a->ldo2;
   P.p = a->dropout_p; P.thresh = mms_drop_thresh(a->dropout_p); P.seed = a->seed; P.offset = a->offset;
   P.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
+  P.group_m = gemm_group_m();
   MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD ||
                 a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
   MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");

@@ -1,6 +1,6 @@
 """HBM traffic of the GEMM launches from two rocprofv3 PMC passes of bench.py (FETCH_SIZE, WRITE_SIZE;
 separate passes as MI355X_MICROARCH.md §HBM / §PMC slots prescribe; FETCH_SIZE doubled for gfx950's
-half-counted 128-B requests).  One full step (between the last two optimizer launches) is used.
+half-counted 128-B requests).  Mean over the complete steps after the first.
 
 usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR [--out profiles/roundN_gemm_traffic.json]
 """
@@ -30,9 +30,13 @@ def main():
     a = ap.parse_args()
     F = load(a.fetch + "/run_counter_collection.csv")
     W = {r["Dispatch_Id"]: float(r["Counter_Value"]) for r in load(a.write + "/run_counter_collection.csv")}
-    # steps start at the fbank launch (the optimizer is chunked and deferred into the next step)
+    # steps start at the fbank launch (the optimizer is chunked and deferred into the next step);
+    # every complete step after the first (warm-up) one is averaged, so batches of every length
+    # bucket count in proportion
     starts = [i for i, r in enumerate(F) if "fbank_kernel" in r["Kernel_Name"]]
-    step = F[starts[-2]: starts[-1]]
+    first = 1 if len(starts) > 2 else 0
+    nsteps = len(starts) - 1 - first
+    step = F[starts[first]: starts[-1]]
     per = defaultdict(lambda: [0, 0.0, 0.0])
     tot = [0.0, 0.0]
     for r in step:
@@ -44,13 +48,21 @@ def main():
         per[k][2] += write
         tot[0] += fetch
         tot[1] += write
-    gemm = [(k, v) for k, v in per.items() if "gemm" in k]
-    gl = sum(v[0] for _, v in gemm)
-    gb = sum(v[1] + v[2] for _, v in gemm)
+    # a GEMM call is its gemm launch plus, for split-K forward / dgrad GEMMs, its fixup pass
+    gemm = [(k, v) for k, v in per.items() if "gemm" in k or "splitk_fixup" in k]
+    gl = sum(v[0] for k, v in gemm if "gemm" in k) / nsteps
+    gb = sum(v[1] + v[2] for _, v in gemm) / nsteps
+    for v in per.values():
+        v[0] /= nsteps
+        v[1] /= nsteps
+        v[2] /= nsteps
+    tot = [t / nsteps for t in tot]
     out = {
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                  "`python bench.py --steps 3 --warmup 1`; one full training step; FETCH x2 (gfx950)",
-        "step_dispatches": len(step),
+                  "`python bench.py --steps 3 --warmup 1`; mean over the complete steps after the first; "
+                  "FETCH x2 (gfx950); GEMM = gemm launches + their split-K fixup passes",
+        "steps_averaged": nsteps,
+        "step_dispatches": len(step) / nsteps,
         "step_hbm_bytes": tot[0] + tot[1],
         "gemm_launches": gl,
         "gemm_hbm_bytes_per_step": gb,
@@ -61,7 +73,7 @@ def main():
     }
     print(json.dumps({k: v for k, v in out.items() if k != "per_kernel"}, indent=1))
     for k, v in list(out["per_kernel"].items())[:20]:
-        print(f"{v['read_bytes'] / 1e6:9.1f} MB rd {v['write_bytes'] / 1e6:9.1f} MB wr {v['launches']:4d}x  {k}")
+        print(f"{v['read_bytes'] / 1e6:9.1f} MB rd {v['write_bytes'] / 1e6:9.1f} MB wr {v['launches']:6.1f}x  {k}")
     if a.out:
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)
