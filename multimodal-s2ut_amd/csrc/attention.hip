@@ -186,8 +186,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   f32x4 o[NDT];
 #pragma unroll
   for (int i = 0; i < NDT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;   // running max of the unscaled scores, running sum
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  const float c2 = P.scale * 1.4426950408889634f;   // scale * log2(e)
   const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
   const uint64_t zctr = P.offset + (uint64_t)z * P.Tq * P.Tk;
   const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)P.Tq * P.Tk - 1);  // uniform per head
@@ -238,20 +239,31 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) s[t] = mfma(frag_rows<HD>(tK, 16 * t, kk * 32, lane), qf[kk], s[t]);
     }
+    // scores stay unscaled: the max commutes with the positive scale, and exp(scale*(s - m)) is one
+    // FMA + v_exp_f32 in base 2.  A key tile that is valid for every row of the wave (inside the
+    // key length and, causal, entirely at or before the wave's first row) skips the masking.
+    const bool full = kb + KB <= kmax && (!P.causal || kb + KB - 1 <= w_row0);
     float bmax = -INFINITY;
+    if (full) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t)
+        bmax = fmaxf(bmax, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
+    } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb + 16 * t + 4 * g + r;
-        const bool ok = key < kmax && (!P.causal || key <= q_own);
-        const float x = ok ? s[t][r] * P.scale : -INFINITY;
-        s[t][r] = x;
-        bmax = fmaxf(bmax, x);
-      }
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb + 16 * t + 4 * g + r;
+          const bool ok = key < kmax && (!P.causal || key <= q_own);
+          const float x = ok ? s[t][r] : -INFINITY;
+          s[t][r] = x;
+          bmax = fmaxf(bmax, x);
+        }
+    }
     bmax = xmax16_32(bmax);
     const float mn = fmaxf(m, bmax);
-    const float alpha = (mn == -INFINITY) ? 1.f : __expf(m - mn);
+    const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m - mn) * c2);
+    const float mnc = (mn == -INFINITY) ? 0.f : mn * c2;   // masked s = -inf -> exp2(-inf) = 0
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -262,9 +274,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = (s[t][r] == -INFINITY) ? 0.f : __expf(s[t][r] - mn);
+        const float e = __builtin_amdgcn_exp2f(fmaf(s[t][r], c2, -mnc));
         rs += e;
-        s[t][r] = keep[r] ? e * dscale : 0.f;
+        s[t][r] = keep[r] ? e : 0.f;   // the 1/(1-p) of the kept probabilities is applied once at the end
       }
     }
     rs = xsum16_32(rs);
@@ -281,13 +293,14 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
     }
   }
   if (q_own < P.Tq) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const float inv = l > 0.f ? dscale / l : 0.f;
     h16* O = P.o + b * P.sob + h * HD + (long)q_own * P.ldo;
 #pragma unroll
     for (int i = 0; i < NDT; ++i)
       *reinterpret_cast<h16x4*>(O + 16 * i + 4 * g) =
           h16x4{(h16)(o[i][0] * inv), (h16)(o[i][1] * inv), (h16)(o[i][2] * inv), (h16)(o[i][3] * inv)};
-    if (g == 0 && P.lse) P.lse[(long)z * P.Tq + q_own] = (l > 0.f) ? m + __logf(l) : -INFINITY;
+    // natural-log LSE of the scaled scores (the backward's exp(s*scale - L))
+    if (g == 0 && P.lse) P.lse[(long)z * P.Tq + q_own] = (l > 0.f) ? m * P.scale + __logf(l) : -INFINITY;
   }
 }
 
@@ -558,6 +571,7 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
   const int Tq = P.Tq, nch = (Tq + QC - 1) / QC;
   const s16x8 zz = {0, 0, 0, 0, 0, 0, 0, 0};
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  const float c2 = P.scale * 1.4426950408889634f;   // scale * log2(e); sL holds the LSE * log2(e)
   // register staging: the rows of one query chunk, K of one head, V fragments of the wave's keys
   s16x8 rq[NLQ], rd[NLQ], ro[NLQ], rk[NLK];
   float rl = 0.f;
@@ -659,7 +673,7 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
           if (qbase + r < Tq) atomicAdd(&Dr[r], dot);
         }
       }
-      if (tid < QC) { L[tid] = rl; sD[buf ^ 1][tid] = 0.f; }
+      if (tid < QC) { L[tid] = rl * 1.4426950408889634f; sD[buf ^ 1][tid] = 0.f; }   // LSE in log2 units
       if (!LAST) load_chunk(z, qbase + QC);
       else if (znext < Z) load_chunk(znext, 0);
       __syncthreads();
@@ -686,6 +700,9 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
             }
             const f32x4 Lv = *reinterpret_cast<const f32x4*>(L + q0 + 4 * g);
             const f32x4 Dv = *reinterpret_cast<const f32x4*>(Dr + q0 + 4 * g);
+            // a 16x16 (query, key) tile valid everywhere (rows < Tq, keys < klen, causal: every key
+            // at or before every row) skips the per-element masks
+            const bool full = qbase + q0 + 15 < Tq && kw0 + 15 < klen && (!P.causal || kw0 + 15 <= qbase + q0);
             // dropout keep flags, branch-free; one mixer per element on the fast path
             bool keep[4] = {true, true, true, true};
             if (P.thresh) {
@@ -701,11 +718,12 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int q = qbase + q0 + 4 * g + r;
-              const bool ok = q < Tq && key_own < klen && (!P.causal || key_own <= q);
-              const float pr = ok ? __expf(sc[r] * P.scale - Lv[r]) : 0.f;
+              const bool ok = full || (q < Tq && key_own < klen && (!P.causal || key_own <= q));
+              const float e = __builtin_amdgcn_exp2f(fmaf(sc[r], c2, -Lv[r]));
+              const float pr = ok ? e : 0.f;
               const float mk = keep[r] ? dscale : 0.f;
               pt[tt][r] = pr * mk;
-              dst[tt][r] = pr * (dp[r] * mk - Dv[r]);
+              dst[tt][r] = pr * fmaf(dp[r], mk, -Dv[r]);
             }
             *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + q0 + 4 * g) =
                 h16x4{(h16)dst[tt][0], (h16)dst[tt][1], (h16)dst[tt][2], (h16)dst[tt][3]};
