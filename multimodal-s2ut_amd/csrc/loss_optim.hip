@@ -180,23 +180,60 @@ __global__ void optim_prepare_kernel(float* ost, float lr_peak, float warmup_ini
   ost[MMS_OST_ITER] = it + 1.f;
 }
 
-__global__ void adam_kernel(h16* __restrict__ param, const h16* __restrict__ grad, float* __restrict__ master,
-                            float* __restrict__ m, float* __restrict__ v, long n, const float* __restrict__ ost,
-                            float b1, float b2, float eps, float wd) {
+// One thread per 8 parameters: 16-B fp16 param / grad accesses, 2 x 16-B fp32 master / m / v
+// accesses (the flat buffers are 8-element aligned per tensor, so every optimizer chunk starts on
+// a 16-B boundary); a scalar tail covers n % 8.  Per-element arithmetic is the scalar update's.
+MMS_DEV void adam_elem(float g, float& p, float& mi, float& vi, float lr, float step_size, float b1, float b2,
+                       float eps, float wd) {
+  if (wd != 0.f) p -= wd * lr * p;
+  mi = b1 * mi + (1.f - b1) * g;
+  vi = b2 * vi + (1.f - b2) * g * g;
+  p -= step_size * mi / (sqrtf(vi) + eps);
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(h16* __restrict__ param, const h16* __restrict__ grad,
+                                                   float* __restrict__ master, float* __restrict__ m,
+                                                   float* __restrict__ v, long n, const float* __restrict__ ost,
+                                                   float b1, float b2, float eps, float wd) {
   // overflow: skip (FP16Optimizer OverflowError path); inconsistent grads across ranks: no update
   if (ost[MMS_OST_OVERFLOW] != 0.f || ost[MMS_OST_INCONSISTENT] != 0.f) return;
   const float lr = ost[MMS_OST_LR];
   const float mult = ost[MMS_OST_MULT] * ost[MMS_OST_CLIP_COEF];
   const float step_size = ost[MMS_OST_STEP_SIZE];
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const float g = (float)grad[i] * mult;
-    float p = master[i];
-    if (wd != 0.f) p -= wd * lr * p;
-    const float mi = b1 * m[i] + (1.f - b1) * g;
-    const float vi = b2 * v[i] + (1.f - b2) * g * g;
+  const long n8 = n / 8;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const h16x8 gv = *reinterpret_cast<const h16x8*>(grad + 8 * i);
+    f32x4 p[2], mv[2], vv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      p[h] = *reinterpret_cast<const f32x4*>(master + 8 * i + 4 * h);
+      mv[h] = *reinterpret_cast<const f32x4*>(m + 8 * i + 4 * h);
+      vv[h] = *reinterpret_cast<const f32x4*>(v + 8 * i + 4 * h);
+    }
+    h16x8 out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float pe = p[e >> 2][e & 3], me = mv[e >> 2][e & 3], ve = vv[e >> 2][e & 3];
+      adam_elem((float)gv[e] * mult, pe, me, ve, lr, step_size, b1, b2, eps, wd);
+      p[e >> 2][e & 3] = pe;
+      mv[e >> 2][e & 3] = me;
+      vv[e >> 2][e & 3] = ve;
+      out[e] = (h16)pe;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<f32x4*>(master + 8 * i + 4 * h) = p[h];
+      *reinterpret_cast<f32x4*>(m + 8 * i + 4 * h) = mv[h];
+      *reinterpret_cast<f32x4*>(v + 8 * i + 4 * h) = vv[h];
+    }
+    *reinterpret_cast<h16x8*>(param + 8 * i) = out;
+  }
+  for (long i = 8 * n8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    float p = master[i], mi = m[i], vi = v[i];
+    adam_elem((float)grad[i] * mult, p, mi, vi, lr, step_size, b1, b2, eps, wd);
     m[i] = mi;
     v[i] = vi;
-    p -= step_size * mi / (sqrtf(vi) + eps);
     master[i] = p;
     param[i] = (h16)p;
   }
@@ -309,8 +346,12 @@ extern "C" int mms2ut_adam_fp16_master(h16* param, const h16* grad, float* maste
                                        float* exp_avg_sq, int64_t n, const float* ost, float beta1,
                                        float beta2, float eps, float weight_decay, hipStream_t s) {
   if (n == 0) return 0;
-  long g = (n + 255) / 256;
-  if (g > 16384) g = 16384;
+  MMS_REQUIRE(((uintptr_t)param & 15) == 0 && ((uintptr_t)grad & 15) == 0 && ((uintptr_t)master & 15) == 0 &&
+                  ((uintptr_t)exp_avg & 15) == 0 && ((uintptr_t)exp_avg_sq & 15) == 0,
+              "adam: buffers must be 16-B aligned");
+  long g = (n / 8 + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > 8192) g = 8192;
   hipLaunchKernelGGL(adam_kernel, dim3((int)g), dim3(256), 0, s, param, grad, master, exp_avg, exp_avg_sq,
                      (long)n, ost, beta1, beta2, eps, weight_decay);
   return mms::check_launch("adam");
