@@ -85,6 +85,70 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, 
   }
 }
 
+// D % 256 == 0 (the model widths 256 / 512 / 768 / 1024): a half-wave per row, C8 16-B chunks per
+// lane, two rows per wave and 8 per block -- twice the bytes per load instruction of the 4-wide
+// kernel and two independent rows in flight per wave.  Same statistics / dropout counters.
+MMS_DEV float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int C8>
+__global__ void __launch_bounds__(256) ln_fwd16_kernel(const h16* __restrict__ x, const h16* __restrict__ g,
+                                                       const h16* __restrict__ b, h16* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                       long rows, int D, float eps, long grp, long grp_out,
+                                                       float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
+  if (thresh) seed = mms_step_seed(seed);
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const long row = (long)blockIdx.x * 8 + (threadIdx.x >> 6) * 2 + (lane >> 5);
+  if (row >= rows) return;
+  const h16* xr = x + row * D;
+  h16x8 xv[C8];
+#pragma unroll
+  for (int c = 0; c < C8; ++c) xv[c] = *reinterpret_cast<const h16x8*>(xr + (hl + 32 * c) * 8);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < C8; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += (float)xv[c][e];
+  const float mean = half_sum(s) / D;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < C8; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = (float)xv[c][e] - mean; ss += d * d; }
+  const float rstd = rsqrtf(half_sum(ss) / D + eps);
+  if (hl == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  const long orow = grp ? (row / grp) * grp_out + row % grp : row;
+  h16* yr = y + orow * D;
+  const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+#pragma unroll
+  for (int c = 0; c < C8; ++c) {
+    const int col = (hl + 32 * c) * 8;
+    const h16x8 gg = *reinterpret_cast<const h16x8*>(g + col), bb = *reinterpret_cast<const h16x8*>(b + col);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = ((float)xv[c][e] - mean) * rstd * (float)gg[e] + (float)bb[e];
+    if (thresh) {
+      bool k0[4], k1[4];
+      const uint64_t c0 = offset + (uint64_t)(row * D + col);
+      mms_keep4(seed, c0, thresh, k0);
+      mms_keep4(seed, c0 + 4, thresh, k1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = k0[e] ? (float)(h16)o[e] * ds : 0.f;
+        o[e + 4] = k1[e] ? (float)(h16)o[e + 4] * ds : 0.f;
+      }
+    }
+    h16x8 ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ov[e] = (h16)o[e];
+    *reinterpret_cast<h16x8*>(yr + col) = ov;
+  }
+}
+
 constexpr int LN_BWD_ROWS = 16;  // rows per block (4 consecutive rows per wave): ~600 blocks for 10k rows
 constexpr int LN_RPW = 4;
 
@@ -757,12 +821,35 @@ int pick_cpl(int chunks_per_row, F&& f) {
 
 }  // namespace
 
+// the half-wave LayerNorm forward: D a multiple of 256 (<= 1024), 16-B aligned rows and operands
+static bool ln_fwd16_ok(const h16* x, const h16* g, const h16* b, const h16* y, int D) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const char* e = getenv("MMS2UT_LN_FWD16");
+  return !(e && e[0] == '0') && D % 256 == 0 && D <= 1024 && al(x) && al(g) && al(b) && al(y);
+}
+
+static int ln_fwd16_launch(const h16* x, const h16* g, const h16* b, h16* y, float* mean, float* rstd,
+                           int64_t rows, int D, float eps, int64_t grp, int64_t grp_out, float p, uint32_t th,
+                           uint64_t seed, uint64_t offset, hipStream_t s) {
+  const dim3 grid((unsigned)((rows + 7) / 8)), block(256);
+  switch (D / 256) {
+#define CASE(C) case C: hipLaunchKernelGGL((ln_fwd16_kernel<C>), grid, block, 0, s, x, g, b, y, mean, rstd, \
+                                           (long)rows, D, eps, (long)grp, (long)grp_out, p, th, seed, offset); break;
+    CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+    default: mms::set_error("layernorm_fwd16: D=%d", D); return 1;
+  }
+  return mms::check_launch("layernorm_fwd16");
+}
+
 // ============================================================================ C-ABI
 extern "C" int mms2ut_layernorm_fwd(const h16* x, const h16* gamma, const h16* beta, h16* y,
                                     float* mean, float* rstd, int64_t rows, int D, float eps,
                                     hipStream_t s) {
   MMS_REQUIRE(D % 4 == 0, "layernorm: D must be a multiple of 4");
   if (rows == 0) return 0;
+  if (ln_fwd16_ok(x, gamma, beta, y, D))
+    return ln_fwd16_launch(x, gamma, beta, y, mean, rstd, rows, D, eps, 0, 0, 0.f, 0u, 0, 0, s);
   return pick_cpl(D / 4, [&](auto C) {
     hipLaunchKernelGGL((ln_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
                        x, gamma, beta, y, mean, rstd, (long)rows, D, eps, 0L, 0L, 0.f, 0u, (uint64_t)0,
@@ -780,6 +867,8 @@ extern "C" int mms2ut_layernorm_fwd_ex(const h16* x, const h16* gamma, const h16
   MMS_REQUIRE(p < 1.f, "layernorm_fwd_ex: p must be < 1");
   if (rows == 0) return 0;
   const uint32_t th = mms_drop_thresh(p);
+  if (ln_fwd16_ok(x, gamma, beta, y, D))
+    return ln_fwd16_launch(x, gamma, beta, y, mean, rstd, rows, D, eps, grp, grp_out, p, th, seed, offset, s);
   return pick_cpl(D / 4, [&](auto C) {
     hipLaunchKernelGGL((ln_fwd_kernel<decltype(C)::value>), dim3((rows + 3) / 4), dim3(256), 0, s,
                        x, gamma, beta, y, mean, rstd, (long)rows, D, eps, (long)grp, (long)grp_out, p, th,
