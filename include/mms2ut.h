@@ -81,6 +81,15 @@ typedef struct mms2ut_gemm_args {
    * unsplit grid covers a tenth of the CUs.                                                       */
   float* splitk_ws;
   int64_t splitk_ws_floats;
+  /* in-launch split-K reduction (epi = MMS_EPI_F32, batch 1, N % 4 == 0): each split still writes
+   * its alpha-scaled fp32 slab to C, then the last split to finish a tile (per-tile arrival counter
+   * red_cnt[tiles_m*tiles_n], zero on entry and left zero on exit) sums the tile's slabs in split
+   * order -> fp16 red_out (ld_red_out), and with rowsum the bias partials -> fp16 red_bias.  The
+   * same bytes mms2ut_splitk_reduce(_bias) produces, without its launch.                         */
+  mms2ut_half* red_out;
+  int64_t ld_red_out;
+  mms2ut_half* red_bias;
+  int32_t* red_cnt;
 } mms2ut_gemm_args;
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);

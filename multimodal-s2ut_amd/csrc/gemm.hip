@@ -47,7 +47,10 @@ struct GemmP {
   int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity
   float* rowsum; long ld_rowsum;  // RS kernels: split-K partial A-row sums (bias gradient)
   int group_m;  // tile-rows per L2 group (tile_coords)
+  h16* red_out; long ld_red_out; h16* red_bias; int* red_cnt;  // in-launch split-K reduction
 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 MMS_DEV int swz_mn(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
@@ -253,7 +256,16 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
   const int N = P.N;
   if (EPI == MMS_EPI_F32) {
     float* C = reinterpret_cast<float*>(Cz) + (long)m * P.ldc;
-    if (n + 7 < N) {
+    if (P.red_cnt && n + 7 < N) {
+      // slab of an in-launch split-K reduction: write-through (sc1) stores, so the reducing block on
+      // any XCD sees them after its acquire without a release (L2 write-back) in every split block
+      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(Cz, (short)0, 0x7fffffff, 0x00020000);
+      const int off = (int)(((long)m * P.ldc + n) * 4);
+      const f32x4 lo = {v[0] * P.alpha, v[1] * P.alpha, v[2] * P.alpha, v[3] * P.alpha};
+      const f32x4 hi = {v[4] * P.alpha, v[5] * P.alpha, v[6] * P.alpha, v[7] * P.alpha};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), rc, off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), rc, off + 16, 0, 16);
+    } else if (n + 7 < N) {
       *reinterpret_cast<f32x4*>(C + n) = f32x4{v[0] * P.alpha, v[1] * P.alpha, v[2] * P.alpha, v[3] * P.alpha};
       *reinterpret_cast<f32x4*>(C + n + 4) = f32x4{v[4] * P.alpha, v[5] * P.alpha, v[6] * P.alpha, v[7] * P.alpha};
     } else {
@@ -620,6 +632,54 @@ MMS_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// In-launch split-K reduction (MI355X guide §5 'Projection GEMM at M = 256' item 2, write-through
+// form): every split stores its slab tile (and bias partials) with sc1 write-through stores, drains
+// them (vmcnt(0) in every wave) and takes a relaxed agent-scope ticket on the tile's counter; the
+// split drawing the last ticket acquires and sums the tile's slabs in split order (bit-identical
+// to splitk_reduce_kernel) into the fp16 output, plus the bias partials of the first tile column.
+// It leaves the counter at zero for the next launch.  (The release-fence form costs an L2
+// write-back per split block: measured 20.6 vs 18.2 ms per training step.)
+template <bool RS>
+MMS_DEV void splitk_inlaunch_reduce(const GemmP& P, char* smem, int tile, int bm, int bn, bool rs_tile) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab (and rowsum) stores are done
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);             // the staging ring is idle: reuse it for the flag
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(P.red_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = old == P.splitk - 1;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const float* slab0 = reinterpret_cast<const float*>(P.C);
+  const int c = bn + 4 * (threadIdx.x & 31);
+  if (c < P.N) {
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const int m = bm + (threadIdx.x >> 5) + 8 * i;
+      if (m >= P.M) break;
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < P.splitk; ++k)
+        sum += *reinterpret_cast<const f32x4*>(slab0 + k * P.sCsplit + (long)m * P.ldc + c);
+      *reinterpret_cast<h16x4*>(P.red_out + (long)m * P.ld_red_out + c) =
+          h16x4{(h16)sum[0], (h16)sum[1], (h16)sum[2], (h16)sum[3]};
+    }
+  }
+  if (RS && rs_tile && P.red_bias && threadIdx.x < BM) {
+    const int m = bm + threadIdx.x;
+    if (m < P.M) {
+      float sum = 0.f;
+      for (int k = 0; k < P.splitk; ++k) sum += P.rowsum[(long)k * P.ld_rowsum + m];
+      P.red_bias[m] = (h16)sum;
+    }
+  }
+  if (threadIdx.x == 0) P.red_cnt[tile] = 0;
+}
+
 template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
 __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
   if (P.thresh) P.seed = mms_step_seed(P.seed);
@@ -712,7 +772,16 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = bm + wm * 64 + i * 16 + lane;
-      if (m < P.M) P.rowsum[(long)zs * P.ld_rowsum + m] = rs[i][0] * P.alpha;
+      if (m < P.M) {
+        const float val = rs[i][0] * P.alpha;
+        if (P.red_cnt) {   // read by the in-launch reducer: write-through, as the slab
+          const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(P.rowsum, (short)0, 0x7fffffff, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rr,
+                                                (int)(((long)zs * P.ld_rowsum + m) * 4), 0, 16);
+        } else {
+          P.rowsum[(long)zs * P.ld_rowsum + m] = val;
+        }
+      }
     }
   }
   char* Cz;
@@ -725,6 +794,12 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   // last k-step waited for vmcnt(0))
   __syncthreads();
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+  if constexpr (EPI == MMS_EPI_F32) {
+    if (P.red_cnt) {
+      __syncthreads();   // every wave is past its staged-epilogue reads of the ring
+      splitk_inlaunch_reduce<RS>(P, smem, tm * tiles_n + tn, bm, bn, tn == 0);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1397,6 +1472,12 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.p = a->dropout_p; P.thresh = mms_drop_thresh(a->dropout_p); P.seed = a->seed; P.offset = a->offset;
   P.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
   P.group_m = gemm_group_m();
+  if (a->red_cnt) {
+    MMS_REQUIRE(a->epi == MMS_EPI_F32 && a->batch == 1 && a->N % 4 == 0 && a->ldc % 4 == 0 && a->red_out &&
+                    a->ld_red_out % 4 == 0 && ((uintptr_t)a->red_out & 7) == 0 && ((uintptr_t)a->C & 15) == 0,
+                "gemm: in-launch split-K reduction needs epi F32, batch 1, N %% 4 == 0, aligned buffers");
+    P.red_out = a->red_out; P.ld_red_out = a->ld_red_out; P.red_bias = a->red_bias; P.red_cnt = a->red_cnt;
+  }
   MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD ||
                 a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
   MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");
@@ -1433,6 +1514,16 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     dim3 grid(tm * tn * nz), block(NT);
     hipLaunchKernelGGL((gemm_dma_kernel<false, false, MMS_EPI_F32, 2, true>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
     return mms::check_launch("gemm_dma_rs");
+  }
+  if (a->red_cnt) {
+    // the reduction lives in the 2-stage LDS-DMA kernel only: no other kernel may take this GEMM
+    MMS_REQUIRE(dma_ok, "gemm: in-launch split-K reduction needs the LDS-DMA path (K %% 64, extents)");
+    dim3 grid(tm * tn * nz), block(NT);
+    if (a_kc && b_kc) hipLaunchKernelGGL((gemm_dma_kernel<true, true, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
+    else if (a_kc) hipLaunchKernelGGL((gemm_dma_kernel<true, false, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
+    else if (b_kc) hipLaunchKernelGGL((gemm_dma_kernel<false, true, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
+    else hipLaunchKernelGGL((gemm_dma_kernel<false, false, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
+    return mms::check_launch("gemm_dma_red");
   }
   if (!force_reg && dma_ok) {
     if (use_256(a, nz)) {

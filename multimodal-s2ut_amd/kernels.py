@@ -63,7 +63,7 @@ class Dropout:
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv=1,
          sA=(0, 0), sB=(0, 0), sC=(0, 0), epi=EPI_F16, alpha=1.0, bias=None, aux=None, ldaux=0,
          sX=(0, 0), out2=None, ldo2=0, p=0.0, seed=0, offset=0, ld_rng=0, splitk=1, sCsplit=0,
-         rowsum=None, ld_rowsum=0):
+         rowsum=None, ld_rowsum=0, red_out=None, red_bias=None, red_cnt=None):
     a = GemmArgs()
     a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
     a.M, a.N, a.K = int(M), int(N), int(K)
@@ -82,6 +82,9 @@ def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv
     a.out2, a.ldo2 = _p(out2), int(ldo2)
     a.dropout_p, a.seed, a.offset, a.ld_rng = float(p), int(seed), int(offset), int(ld_rng)
     a.rowsum, a.ld_rowsum = _p(rowsum), int(ld_rowsum)
+    if red_cnt is not None:
+        a.red_out, a.ld_red_out = red_out.data_ptr(), int(red_out.stride(0))
+        a.red_bias, a.red_cnt = _p(red_bias), red_cnt.data_ptr()
     ws = None
     if splitk == 1 and epi != EPI_F32 and batch == 1 and rowsum is None and _SPLITK_FIX:
         s = _fixup_splits(M, N, K)
@@ -339,6 +342,27 @@ def side_join():
         _Side.keep.clear()
 
 
+# In-launch split-K reduction of the weight gradients (gemm.hip splitk_inlaunch_reduce): bit-identical
+# to the splitk_reduce launch, but measured slower in the training step (19.6 vs 18.2 ms: the last
+# split of a tile reads 3-4 x 64 KiB of slabs serially while the side stream holds few CUs), so it
+# is opt-in (MMS2UT_WGRAD_INLAUNCH=1).
+_INLAUNCH_RED = os.environ.get("MMS2UT_WGRAD_INLAUNCH", "0") == "1"
+_RED_CNT = {}
+_RED_CNT_CAP = 1 << 16
+
+
+def _red_counters(device):
+    """Per-stream tile-arrival counters of the in-launch split-K reduction: zero-initialised once,
+    every launch leaves them at zero (the last split of a tile resets its counter).  Kernels on one
+    stream serialise, so one buffer per stream suffices."""
+    key = _s()
+    buf = _RED_CNT.get(key)
+    if buf is None:
+        buf = torch.zeros(_RED_CNT_CAP, dtype=torch.int32, device=device)
+        _RED_CNT[key] = buf
+    return buf
+
+
 def _workspace(key, numel, device, dtype=torch.float32):
     """Scratch owned by the stream it is used on (side-stream serialised reuse; regrowth keeps the
     old buffer alive until the next join)."""
@@ -388,6 +412,12 @@ def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
         s = _splitk_for(tiles, M)
         slabs = _workspace("slab", s * N * K, dy.device)
         rs = _workspace("rowsum", s * N, dy.device) if db is not None else None
+        if accumulate_f32 is None and _INLAUNCH_RED and K % 4 == 0 and dW.stride(0) % 4 == 0 and tiles <= _RED_CNT_CAP:
+            # the last split of each tile reduces the slabs (and the bias partials) itself
+            gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
+                 epi=EPI_F32, splitk=s, sCsplit=N * K, rowsum=rs, ld_rowsum=N, red_out=dW, red_bias=db,
+                 red_cnt=_red_counters(dy.device))
+            return dW
         gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
              epi=EPI_F32, splitk=s, sCsplit=N * K, rowsum=rs, ld_rowsum=N)
         if db is not None and accumulate_f32 is None and N % 4 == 0:
