@@ -214,8 +214,10 @@ def test_linear_splitk_epilogue(M, N, Kd, s, relu, res):
 
 
 @pytest.mark.parametrize("M,N,Kd,s", [(160, 768, 3072, 8), (37, 768, 768, 3), (200, 256, 1024, 4)])
-def test_splitk_epilogue_ln_bit_identical(M, N, Kd, s):
-    """Fused split-K reduction + residual + LayerNorm == the two-launch sequence, bit for bit."""
+def test_splitk_epilogue_ln_bit_identical(M, N, Kd, s, monkeypatch):
+    """Fused split-K reduction + residual + LayerNorm == the two-launch sequence, bit for bit (the
+    one-wave-per-row LayerNorm kernel, whose reduction order the fused epilogue follows)."""
+    monkeypatch.setenv("MMS2UT_LN_FWD16", "0")
     K = pkg("kernels")
     g = torch.Generator().manual_seed(N + M)
     x = (torch.randn(M, Kd, generator=g) * 0.5).half().cuda()
