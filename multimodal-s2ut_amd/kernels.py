@@ -91,10 +91,59 @@ def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv
         if s > 1:
             ws = _workspace("splitk_fix", s * M * N, C.device)
             a.splitk, a.splitk_ws, a.splitk_ws_floats = s, ws.data_ptr(), ws.numel()
+        elif _TAIL_SPLIT:
+            M1 = _tail_split_rows(M, N, K)
+            if M1:
+                return _gemm_tail_split(a, M1, C.device)
     call("mms2ut_gemm_f16", a, _s())
 
 
 _SPLITK_FIX = os.environ.get("MMS2UT_SPLITK_FIX", "1") != "0"
+# Tail split (below) measured slower in the training step (19.03 vs 18.46 ms over three interleaved
+# pairs) although faster in isolation: opt-in, MMS2UT_GEMM_TAILSPLIT=1.
+_TAIL_SPLIT = os.environ.get("MMS2UT_GEMM_TAILSPLIT", "0") == "1"
+_SLOTS = 512      # 128x128 blocks resident at once: 2 per CU x 256 CUs
+
+
+def _tail_split_rows(M, N, K):
+    """Rows of a fused-epilogue 128x128 GEMM whose grid overflows the 512 block slots by at most a
+    quarter round: the head (whole rounds of row tiles) runs as usual and the tail rows run split-K
+    with the fixup, instead of a nearly empty last round of lone, latency-bound tiles (M = 11000,
+    N = 768, K = 768: 516 tiles take 31.7 us against 18 us for 474).  0 = no split.  The 256x256
+    kernel's shapes (gemm.hip use_256) are left alone."""
+    if K < 512 or N % 4 or (K >= 2048 and N >= 1536 and M >= 4096):
+        return 0
+    tn = (N + 127) // 128
+    tiles = ((M + 127) // 128) * tn
+    if tiles <= _SLOTS:
+        return 0
+    head_rows = ((tiles // _SLOTS) * _SLOTS // tn)        # whole row tiles in the full rounds
+    if tiles - head_rows * tn > _SLOTS // 4:
+        return 0
+    return head_rows * 128
+
+
+def _gemm_tail_split(a, M1, device):
+    """Launch rows [0, M1) of the GEMM described by ``a`` as is, rows [M1, M) split-K + fixup.  The
+    tail's operand / output pointers move by M1 rows and its dropout counters by M1 * ld_rng, so
+    every element keeps its counter (masks identical to the single launch)."""
+    M = a.M
+    t = GemmArgs.from_buffer_copy(a)
+    a.M = M1
+    call("mms2ut_gemm_f16", a, _s())
+    M2 = M - M1
+    t.M = M2
+    t.A = a.A + 2 * M1 * (a.lda if a.a_kcontig else 1)
+    t.C = a.C + 2 * M1 * a.ldc
+    if a.aux:
+        t.aux = a.aux + 2 * M1 * a.ldaux
+    if a.out2:
+        t.out2 = a.out2 + 2 * M1 * a.ldo2
+    t.offset = a.offset + M1 * (a.ld_rng if a.ld_rng > 0 else a.N)
+    s = max(2, _fixup_splits(M2, a.N, a.K))
+    ws = _workspace("splitk_fix", s * M2 * a.N, device)
+    t.splitk, t.splitk_ws, t.splitk_ws_floats = s, ws.data_ptr(), ws.numel()
+    call("mms2ut_gemm_f16", t, _s())
 
 
 def _fixup_splits(M, N, K):

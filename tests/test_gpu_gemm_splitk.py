@@ -91,3 +91,35 @@ def test_fixup_accumulate_dgrad():
     exact = base.float() + dy.float() @ W.float()
     assert _rel(outs[1], outs[0]) < 2e-3
     assert _rel(outs[1], exact) < 2e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(11000, 768, 768), (11000, 768, 3072), (11000, 2304, 768), (12000, 768, 768)])
+def test_tail_split_matches_single_launch(M, N, K):
+    """A grid that overflows the 512 block slots by a small tail: head rows as usual, tail rows
+    split-K + fixup (kernels._tail_split_rows) == one launch, masks identical."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mm = pkg()
+    K_ = mm.kernels
+    M1 = K_._tail_split_rows(M, N, K)
+    assert 0 < M1 < M
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
+    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).half()
+    aux = torch.randn(M, N, device="cuda", generator=g).half()
+    big = torch.full((N,), 30.0, device="cuda").half()
+    for name, kw in (("relu_drop_open", dict(epi=K_.EPI_RELU_DROP, p=0.1, drop=(3, 512))),
+                     ("drop_resid", dict(epi=K_.EPI_DROP_RESID, p=0.1, drop=(5, 0), aux=aux))):
+        outs = []
+        tail0 = K_._TAIL_SPLIT
+        for tail in (False, True):
+            K_._TAIL_SPLIT = tail
+            try:
+                outs.append(K_.linear(x, W, big, **kw).clone())
+            finally:
+                K_._TAIL_SPLIT = tail0
+        torch.cuda.synchronize()
+        assert _rel(outs[1], outs[0]) < 2e-3, name
+        assert torch.equal(outs[1][:M1], outs[0][:M1]), name        # the head is the same launch
+        if name == "relu_drop_open":
+            assert torch.equal(outs[1] == 0, outs[0] == 0)
