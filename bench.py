@@ -328,10 +328,12 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        prof = None
+        prof = bprof = None
         if not profile and os.environ.get("MMS2UT_HOST_PROFILE"):
             import cProfile
             prof = cProfile.Profile()
+            bprof = cProfile.Profile()
+            runtime._BWD_PROFILE = bprof
             prof.enable()
         t0 = time.perf_counter()
         for i in range(args.steps):
@@ -340,7 +342,11 @@ def main():
         if prof is not None:
             import pstats
             prof.disable()
-            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(40)
+            runtime._BWD_PROFILE = None
+            print("== host profile: main thread (forward, loss, optimizer)", file=sys.stderr)
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
+            print("== host profile: autograd thread (hand-written backward)", file=sys.stderr)
+            pstats.Stats(bprof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

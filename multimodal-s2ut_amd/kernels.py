@@ -291,14 +291,18 @@ def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=Fa
     return out
 
 
+_WGRAD_SPLITK_CAP = int(os.environ.get("MMS2UT_WGRAD_SPLITK", "16"))
+_WGRAD_SLOTS = os.environ.get("MMS2UT_WGRAD_SLOTS")
+
+
 def _splitk_for(tiles, kred, slots=512):
     """split-K count for a weight gradient (reduction over kred token rows): the largest s whose
     tiles*s blocks still fit one round of the 512 block slots (2 per CU), so every block runs
     concurrently and no partial second round trails (scripts/wgrad_sweep.py, isolated GEMM +
     slab reduction on the step's shapes: fc 3072x768 s3 vs the old fixed s8, qkv 2304x768 s4
     49 vs 60 us, cross-KV 9216x768 s1 174 vs 234 us).  MMS2UT_WGRAD_SPLITK caps s."""
-    cap = int(os.environ.get("MMS2UT_WGRAD_SPLITK", "16"))
-    slots = int(os.environ.get("MMS2UT_WGRAD_SLOTS", slots))
+    cap = _WGRAD_SPLITK_CAP
+    slots = int(_WGRAD_SLOTS) if _WGRAD_SLOTS else slots
     s = max(1, min(cap, slots // max(tiles, 1)))
     while s > 1 and kred // s < 256:
         s -= 1

@@ -156,12 +156,22 @@ class _ModelFn(torch.autograd.Function):
         dinner = MT.aux_backward_decoder_heads(model, actx, daux) if use_aux else None
         if dlogits is None:    # only the multitask losses were differentiated
             dlogits = torch.zeros(dctx["B"] * dctx["Tt"], dctx["Vp"], dtype=F16, device=enc.device)
+        prof = _BWD_PROFILE
+        if prof is not None:
+            prof.enable()
         model.decoder_backward(dctx, dlogits.contiguous(), enc, denc, dinner=dinner)
         del dctx
         dstates = MT.aux_backward_encoder_heads(model, actx, daux, batch.prev.shape[0], Te) if use_aux else None
         model.encoder_backward(ectx, denc, dstates)
         K.side_join()  # weight gradients (side stream) complete before anyone reads them
+        if prof is not None:
+            prof.disable()
         return None, None, None
+
+
+# host-side profile of the hand-written backward (it runs on the autograd engine's thread, which a
+# profiler enabled on the main thread does not see): bench.py sets a cProfile.Profile here
+_BWD_PROFILE = None
 
 
 def model_outputs(model, batch):
