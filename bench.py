@@ -315,16 +315,22 @@ def main():
     base = args.warmup   # the timed batch sequence does not depend on how many settling steps ran
     def timed(profile):
         """K steps between barrier + synchronize on both sides -> (seconds, host issue seconds, GEMM stats).
-        profile=True: the roofline pass — every GEMM launch bracketed by HIP events on its own
-        stream, with the weight-gradient side stream folded into the main stream so no two GEMMs
-        overlap and each event pair times exactly one kernel."""
+        profile=True: the roofline pass — every GEMM kernel's workgroups store their start / end
+        s_memrealtime ticks (mms2ut_profile_stamps), with the weight-gradient side stream folded
+        into the main stream so no two GEMMs overlap: a launch's duration is max(end) - min(start)
+        over its workgroups, the dispatch span rocprofv3 reports, without the 1.3-1.5x inflation
+        per-launch HIP event pairs added to 20-90 us kernels (round 2 measurement)."""
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         side_was = kernels._Side.enabled
+        stamps = None
         if profile:
             kernels._Side.enabled = False
             kernels.gemm_profile_begin(2000 * args.steps)
+            # in-kernel block stamps (2 x int64 per workgroup; ~0.2 M workgroups per step)
+            stamps = torch.zeros(2 * 400_000 * args.steps, dtype=torch.int64, device=device)
+            kernels.gemm_profile_stamps(stamps)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -355,16 +361,21 @@ def main():
         launches = None
         if profile:
             g = kernels.gemm_profile_end()
-            launches = kernels.gemm_profile_launches(g[1])
+            _, l_fl, l_cls = kernels.gemm_profile_launches(g[1])
+            l_ms = kernels.gemm_profile_durations(stamps, g[1])
+            if np.isnan(l_ms).any():
+                raise SystemExit(f"bench: GEMM stamp buffer overflowed ({int(np.isnan(l_ms).sum())} launches)")
+            launches = (l_ms, l_fl, l_cls)
+            g = (float(l_ms.sum()), g[1], g[2], g[3])
             kernels._Side.enabled = side_was
         return t1 - t0, t_issue - t0, g, launches
 
-    # the throughput region runs uninstrumented (per-launch HIP events cost ~5 % of the step);
-    # the same K steps are then re-run serially with the library's per-GEMM events for the roofline
+    # the throughput region runs uninstrumented; the same K steps are then re-run serially with the
+    # library's in-kernel workgroup stamps for the roofline
     t_run, t_issue_run, _, _ = timed(False)
     t_prof = None
     gemm_ms, n_launch, launched_flops, gemm_bytes = 0.0, 0, 0.0, 0.0
-    classes = {}
+    classes, templates = {}, {}
     if not args.no_gemm_timing:
         t_prof, _, (gemm_ms, n_launch, launched_flops, gemm_bytes), (l_ms, l_fl, l_cls) = timed(True)
         if os.environ.get("MMS2UT_GEMM_DUMP"):
@@ -379,6 +390,13 @@ def main():
             else:
                 name = "forward / dgrad (NT, fused epilogues)"
             e = classes.setdefault(name, [0.0, 0.0, 0])
+            e[0] += ms_
+            e[1] += fl_
+            e[2] += 1
+            # per kernel template (rocprofv3 names them gemm_dma_kernel<A_KC, B_KC, EPI, ...>)
+            t = f"gemm<{'true' if c_ & 1 else 'false'}, {'true' if c_ & 2 else 'false'}, {(c_ >> 2) & 63}>" + \
+                (" batched" if c_ & 256 else "") + (" split-K" if c_ & 512 else "")
+            e = templates.setdefault(t, [0.0, 0.0, 0])
             e[0] += ms_
             e[1] += fl_
             e[2] += 1
@@ -415,6 +433,10 @@ def main():
         if class_lines:
             dn = max(class_lines, key=lambda k: class_lines[k]["ms_per_step"])
             dominant = dict(class_lines[dn], name=dn)
+        tmpl_lines = {k: {"us_per_launch": 1e3 * v[0] / max(v[2], 1), "launches_per_step": v[2] / args.steps,
+                          "ms_per_step": v[0] / args.steps, "launched_tflops": v[1] / max(v[0], 1e-9) / 1e9,
+                          "frac": v[1] / max(v[0], 1e-9) / 1e9 / MFMA_PEAK_F16}
+                      for k, v in sorted(templates.items(), key=lambda kv: -kv[1][0])}
         line = {
             "metric": "audio-frames/sec/node, mm_s2ut_transformer fp16, max-tokens 40000, 1/2/4/8 GPUs",
             "value": frames_all / elapsed,
@@ -442,15 +464,19 @@ def main():
                          "gemm_launched_tflops": launched_flops / max(gemm_ms, 1e-9) / 1e9,
                          "dominant": dominant,
                          "classes": class_lines,
+                         "kernels": tmpl_lines,
                          "host_issue_ms_per_step": 1e3 * (t_issue - t0) / args.steps,
                          "hip_graph": {"enabled": graph, "graphs": n_graphs},
                          "roofline_pass_ms_per_step": (1e3 * t_prof / args.steps) if t_prof else None,
                          "note": "achieved = SURVEY §8d algorithmic GEMM FLOPs (true lengths, 3x fwd, "
-                                 "multi-head attention products excluded) / summed HIP-event durations of "
-                                 "every GEMM launch, measured on a second pass of the same K steps run "
-                                 "serially (side stream folded into the main one, so each event pair times "
-                                 "one kernel alone); value comes from the uninstrumented overlapped pass. "
-                                 "classes/dominant: launched (padded-shape) FLOPs per class / its kernel time"},
+                                 "multi-head attention products excluded) / summed kernel durations of every "
+                                 "GEMM launch, measured on a second pass of the same K steps run serially "
+                                 "(side stream folded into the main one): each workgroup stores its "
+                                 "s_memrealtime start / end ticks, a launch lasts max(end) - min(start) over "
+                                 "its workgroups (split-K fixup included); value comes from the "
+                                 "uninstrumented overlapped pass. classes/dominant/kernels: launched "
+                                 "(padded-shape) FLOPs / kernel time; kernels are keyed like rocprofv3's "
+                                 "gemm_dma_kernel<A_KC, B_KC, EPI, ...> names"},
             "cpu_baseline": cpu,
             "optimizer": ost,
         }

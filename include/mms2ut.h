@@ -108,6 +108,16 @@ int mms2ut_profile_bytes(double* bytes);
 int mms2ut_profile_launches(float* ms, double* flops, int* cls, int n);
 /* the same window's shapes: mnk[4i..4i+3] = M, N, K, batch * splitk of launch i                  */
 int mms2ut_profile_shapes(int* mnk, int n);
+/* stamp mode for the open window (call right after profile_begin): instead of events, every GEMM
+ * kernel's blocks store {start, end} s_memrealtime ticks (2 x u64 per block) into `stamps`
+ * (device, 16-B aligned, room for cap_blocks blocks).  profile_blocks then gives, per launch,
+ * the first block slot and one past the last (a split-K fixup's blocks follow its GEMM's; a
+ * value > cap_blocks means the buffer overflowed and the launch was not recorded).  A launch's
+ * duration = max(end) - min(start) over its slots, in ticks of mms2ut_wallclock_khz.  Bench-only
+ * instrumentation (no reference counterpart).                                                    */
+int mms2ut_profile_stamps(unsigned long long* stamps, long cap_blocks);
+int mms2ut_profile_blocks(long* first_last, int n);
+int mms2ut_wallclock_khz(int* khz);
 
 /* sum `nsplit` fp32 slabs [rows, cols] (slab stride `slab`) * alpha -> out, row stride ldo.
  * mode bit0: fp16 output (else fp32); bit1: accumulate into out (else overwrite)            */

@@ -64,6 +64,9 @@ SIGNATURES = {
     "mms2ut_profile_bytes": (i32, [C.POINTER(C.c_double)]),
     "mms2ut_profile_launches": (i32, [C.c_void_p, C.c_void_p, C.c_void_p, i32]),
     "mms2ut_profile_shapes": (i32, [C.c_void_p, i32]),
+    "mms2ut_profile_stamps": (i32, [vp, C.c_long]),
+    "mms2ut_profile_blocks": (i32, [C.c_void_p, i32]),
+    "mms2ut_wallclock_khz": (i32, [C.POINTER(C.c_int)]),
     "mms2ut_grad_norm_check": (i32, [vp, i32, i32, vp, i32, vp]),
     "mms2ut_ctc_workspace_floats": (i32, [i32, i32, i32, C.POINTER(C.c_int64)]),
     "mms2ut_ctc_loss_fwd": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp, vp, i32, i32, vp, vp, vp]),

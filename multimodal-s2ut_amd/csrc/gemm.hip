@@ -48,7 +48,25 @@ struct GemmP {
   float* rowsum; long ld_rowsum;  // RS kernels: split-K partial A-row sums (bias gradient)
   int group_m;  // tile-rows per L2 group (tile_coords)
   h16* red_out; long ld_red_out; h16* red_bias; int* red_cnt;  // in-launch split-K reduction
+  unsigned long long* stamps;  // profiling: per block {first, last} s_memrealtime tick, or null
 };
+
+// Live kernel timing (bench roofline): with P.stamps set, thread 0 of every block stores the
+// block's start tick and its end tick (after the block's last global store has completed) at
+// stamps[2 * blockIdx.x].  A launch's duration is max(end) - min(start) over its blocks — the
+// dispatch span rocprofv3's kernel trace reports, measured inside the real (overlapped) step.
+// One 16-B store per block; nothing is recorded when stamps is null.
+MMS_DEV unsigned long long stamp_now() { return __builtin_amdgcn_s_memrealtime(); }
+MMS_DEV void stamp_end(unsigned long long* stamps, unsigned long long t0) {
+  if (!stamps) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t1 = stamp_now();
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    *reinterpret_cast<u64x2*>(stamps + 2 * (long)blockIdx.x) = u64x2{t0, t1};
+  }
+}
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -525,6 +543,7 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
 
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   int z, tm, tn;
@@ -595,6 +614,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int t
     Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
   const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+  stamp_end(P.stamps, t_start);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -682,6 +702,7 @@ MMS_DEV void splitk_inlaunch_reduce(const GemmP& P, char* smem, int tile, int bm
 
 template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
 __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
   int z, tm, tn;
@@ -800,6 +821,7 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
       splitk_inlaunch_reduce<RS>(P, smem, tm * tiles_n + tn, bm, bn, tn == 0);
     }
   }
+  stamp_end(P.stamps, t_start);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -845,6 +867,7 @@ MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
 
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NT, 2) gemm_dma32_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[ST32 * 2 * T32_BYTES];
   int z, tm, tn;
@@ -914,6 +937,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_dma32_kernel(GemmP P, int tiles_m,
   const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
   __syncthreads();
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+  stamp_end(P.stamps, t_start);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -951,6 +975,7 @@ MMS_DEV void dma_slot2(__amdgpu_buffer_rsrc_t rs, char* img, long ld, int row0, 
 
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[RING2 * SLOT2];
   int z, tm, tn;
@@ -1027,6 +1052,7 @@ __global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, i
   __syncthreads();
   staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[4]), bm + wr * 128 + 64, bn + wc * 64,
                        0, 0, wid, lane, Cz, auxz);
+  stamp_end(P.stamps, t_start);
 }
 
 // Software-pipelined form of the same tile: each 32-deep slot runs in two MFMA phases (rows
@@ -1037,6 +1063,7 @@ __global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, i
 // is issued behind it, leaving RING-3 slots in flight across the barrier.
 template <bool A_KC, bool B_KC, int EPI, int RING>
 __global__ void __launch_bounds__(NT2, 2) gemm256p_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[RING * SLOT2];
   int z, tm, tn;
@@ -1149,6 +1176,7 @@ __global__ void __launch_bounds__(NT2, 2) gemm256p_kernel(GemmP P, int tiles_m, 
   __syncthreads();
   staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[4]), bm + wr * 128 + 64, bn + wc * 64,
                        0, 0, wid, lane, Cz, auxz);
+  stamp_end(P.stamps, t_start);
 }
 
 template <bool A_KC, bool B_KC>
@@ -1241,10 +1269,11 @@ int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
 // per 8 columns of a row: 32-B slab reads, 16-B operand loads / stores.
 template <int EPI>
 __global__ void __launch_bounds__(256) splitk_fixup_kernel(GemmP P, const float* __restrict__ ws, int nsplit) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   const int ncg = (P.N + 7) >> 3;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)P.M * ncg) return;
+  if (i >= (long)P.M * ncg) return;   // never thread 0: the grid is ceil(rows * ncg / 256)
   const int m = (int)(i / ncg), n = (int)(i % ncg) * 8;
   const long slab = (long)P.M * P.N;
   const float* src = ws + (long)m * P.N + n;
@@ -1262,6 +1291,13 @@ __global__ void __launch_bounds__(256) splitk_fixup_kernel(GemmP P, const float*
         if (n + e < P.N) v[e] += src[s * slab + e];
   }
   epilogue_store8<EPI>(P, P.C, P.aux, m, n, v);
+  if (P.stamps) {   // no barrier here (threads of the last block may have returned): thread 0's own end
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) {
+      typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u64x2*>(P.stamps + 2 * (long)blockIdx.x) = u64x2{t_start, stamp_now()};
+    }
+  }
 }
 
 int launch_fixup(int epi, const GemmP& P, const float* ws, int nsplit, hipStream_t s) {
@@ -1294,7 +1330,20 @@ struct GemmProfile {
   int* l_mnk = nullptr;   // M, N, K, batch*splitk per launch
   double flops = 0.0;
   double bytes = 0.0;  // algorithmic HBM bytes: A, B (and aux / accumulated C) read once, C written once
+  // stamp mode (mms2ut_profile_stamps): block stamps instead of events, [2*cursor...) next free slot
+  unsigned long long* stamps = nullptr;
+  long stamp_cap = 0, cursor = 0;
+  long* l_blk = nullptr;  // per launch: first block slot, one past the last (both kernels of a split-K fixup)
 } g_prof;
+
+// stamp slots for the next kernel launch of `blocks` workgroups (null when not in stamp mode or full)
+unsigned long long* stamp_take(long blocks) {
+  if (!g_prof.on || !g_prof.stamps) return nullptr;
+  if (g_prof.cursor + blocks > g_prof.stamp_cap) { g_prof.cursor = g_prof.stamp_cap + 1; return nullptr; }
+  unsigned long long* p = g_prof.stamps + 2 * g_prof.cursor;
+  g_prof.cursor += blocks;
+  return p;
+}
 }  // namespace
 
 extern "C" int mms2ut_profile_begin(int max_launches) {
@@ -1307,7 +1356,11 @@ extern "C" int mms2ut_profile_begin(int max_launches) {
   g_prof.l_ms = (float*)calloc((size_t)max_launches, sizeof(float));
   g_prof.l_flops = (double*)calloc((size_t)max_launches, sizeof(double));
   g_prof.l_cls = (int*)calloc((size_t)max_launches, sizeof(int));
-  MMS_REQUIRE(g_prof.l_ms && g_prof.l_flops && g_prof.l_cls, "profile_begin: out of host memory");
+  free(g_prof.l_blk);
+  g_prof.l_blk = (long*)calloc(2 * (size_t)max_launches, sizeof(long));
+  g_prof.stamps = nullptr;
+  g_prof.stamp_cap = g_prof.cursor = 0;
+  MMS_REQUIRE(g_prof.l_ms && g_prof.l_flops && g_prof.l_cls && g_prof.l_blk, "profile_begin: out of host memory");
   for (int i = 0; i < 2 * max_launches; ++i)
     if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) { mms::set_error("profile_begin: hipEventCreate"); return 1; }
   g_prof.cap = max_launches;
@@ -1322,7 +1375,7 @@ extern "C" int mms2ut_profile_end(float* total_ms, int* launches, double* flops)
   MMS_REQUIRE(g_prof.on, "profile_end: not active");
   g_prof.on = false;
   float tot = 0.f;
-  for (int i = 0; i < g_prof.n; ++i) {
+  for (int i = 0; i < g_prof.n && !g_prof.stamps; ++i) {
     float ms = 0.f;
     if (hipEventSynchronize(g_prof.ev[2 * i + 1]) != hipSuccess ||
         hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]) != hipSuccess) {
@@ -1357,9 +1410,16 @@ static int gemm_group_m() {
 extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (!g_prof.on || g_prof.n >= g_prof.cap) return gemm_dispatch(a, stream);
   const int i = g_prof.n++;
-  hipEventRecord(g_prof.ev[2 * i], stream);
-  const int rc = gemm_dispatch(a, stream);
-  hipEventRecord(g_prof.ev[2 * i + 1], stream);
+  int rc;
+  if (g_prof.stamps) {
+    g_prof.l_blk[2 * i] = g_prof.cursor;
+    rc = gemm_dispatch(a, stream);
+    g_prof.l_blk[2 * i + 1] = g_prof.cursor;   // > stamp_cap: overflowed, not recorded
+  } else {
+    hipEventRecord(g_prof.ev[2 * i], stream);
+    rc = gemm_dispatch(a, stream);
+    hipEventRecord(g_prof.ev[2 * i + 1], stream);
+  }
   if (a) {
     const double nb = a->batch > 0 ? a->batch : 1;
     g_prof.flops += 2.0 * a->M * a->N * a->K * nb;
@@ -1392,6 +1452,35 @@ extern "C" int mms2ut_profile_shapes(int* mnk, int n) {
   MMS_REQUIRE(!g_prof.on && g_prof.l_mnk != nullptr, "profile_shapes: no finished profile window");
   MMS_REQUIRE(n >= 0 && n <= g_prof.n, "profile_shapes: n=%d > %d launches", n, g_prof.n);
   for (int i = 0; i < 4 * n; ++i) mnk[i] = g_prof.l_mnk[i];
+  return 0;
+}
+
+// Stamp mode for the open profile window: every GEMM launch records per-block {start, end}
+// s_memrealtime ticks into `stamps` (device, 2 x u64 per block, `cap_blocks` blocks) instead of
+// HIP events around the launch.  The caller owns the buffer.
+extern "C" int mms2ut_profile_stamps(unsigned long long* stamps, long cap_blocks) {
+  MMS_REQUIRE(g_prof.on && g_prof.n == 0, "profile_stamps: call right after profile_begin");
+  MMS_REQUIRE(stamps != nullptr && cap_blocks > 0 && ((uintptr_t)stamps & 15) == 0, "profile_stamps: bad buffer");
+  g_prof.stamps = stamps;
+  g_prof.stamp_cap = cap_blocks;
+  g_prof.cursor = 0;
+  return 0;
+}
+
+extern "C" int mms2ut_profile_blocks(long* first_last, int n) {
+  MMS_REQUIRE(!g_prof.on && g_prof.l_blk != nullptr, "profile_blocks: no finished profile window");
+  MMS_REQUIRE(n >= 0 && n <= g_prof.n, "profile_blocks: n=%d > %d launches", n, g_prof.n);
+  for (int i = 0; i < 2 * n; ++i) first_last[i] = g_prof.l_blk[i];
+  return 0;
+}
+
+extern "C" int mms2ut_wallclock_khz(int* khz) {
+  MMS_REQUIRE(khz != nullptr, "wallclock_khz: null");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) {
+    mms::set_error("wallclock_khz: hipDeviceGetAttribute failed");
+    return 1;
+  }
   return 0;
 }
 
@@ -1459,6 +1548,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     if (a->out2) v = v && al16(a->out2) && a->ldo2 % 8 == 0;
     if (a->bias) v = v && al16(a->bias);
     F.vec16 = v ? 1 : 0;
+    F.stamps = stamp_take(((long)a->M * ((a->N + 7) / 8) + 255) / 256);
     return launch_fixup(a->epi, F, a->splitk_ws, splitk, stream);
   }
   MMS_REQUIRE(splitk == 1 || a->epi == MMS_EPI_F32, "gemm: split-K needs the fp32 slab epilogue");
@@ -1511,6 +1601,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
                 "gemm: rowsum needs the fp32 slab epilogue, M/N-contiguous operands, batch 1");
     MMS_REQUIRE(a->ld_rowsum >= a->M, "gemm: ld_rowsum < M");
     P.rowsum = a->rowsum; P.ld_rowsum = a->ld_rowsum;
+    P.stamps = stamp_take((long)tm * tn * nz);
     dim3 grid(tm * tn * nz), block(NT);
     hipLaunchKernelGGL((gemm_dma_kernel<false, false, MMS_EPI_F32, 2, true>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
     return mms::check_launch("gemm_dma_rs");
@@ -1518,6 +1609,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (a->red_cnt) {
     // the reduction lives in the 2-stage LDS-DMA kernel only: no other kernel may take this GEMM
     MMS_REQUIRE(dma_ok, "gemm: in-launch split-K reduction needs the LDS-DMA path (K %% 64, extents)");
+    P.stamps = stamp_take((long)tm * tn * nz);
     dim3 grid(tm * tn * nz), block(NT);
     if (a_kc && b_kc) hipLaunchKernelGGL((gemm_dma_kernel<true, true, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
     else if (a_kc) hipLaunchKernelGGL((gemm_dma_kernel<true, false, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
@@ -1528,16 +1620,19 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (!force_reg && dma_ok) {
     if (use_256(a, nz)) {
       const int tm2 = (a->M + BM2 - 1) / BM2, tn2 = (a->N + BN2 - 1) / BN2;
+      P.stamps = stamp_take((long)tm2 * tn2 * nz);
       if (a_kc && b_kc) return launch_256<true, true>(a->epi, P, tm2, tn2, nz, s);
       if (a_kc && !b_kc) return launch_256<true, false>(a->epi, P, tm2, tn2, nz, s);
       if (!a_kc && b_kc) return launch_256<false, true>(a->epi, P, tm2, tn2, nz, s);
       return launch_256<false, false>(a->epi, P, tm2, tn2, nz, s);
     }
+    P.stamps = stamp_take((long)tm * tn * nz);
     if (a_kc && b_kc) return launch_dma<true, true>(a->epi, P, tm, tn, nz, s);
     if (a_kc && !b_kc) return launch_dma<true, false>(a->epi, P, tm, tn, nz, s);
     if (!a_kc && b_kc) return launch_dma<false, true>(a->epi, P, tm, tn, nz, s);
     return launch_dma<false, false>(a->epi, P, tm, tn, nz, s);
   }
+  P.stamps = stamp_take((long)tm * tn * nz);
   if (a_kc && b_kc) return launch_epi<true, true>(a->epi, P, tm, tn, nz, s);
   if (a_kc && !b_kc) return launch_epi<true, false>(a->epi, P, tm, tn, nz, s);
   if (!a_kc && b_kc) return launch_epi<false, true>(a->epi, P, tm, tn, nz, s);

@@ -190,6 +190,32 @@ def gemm_profile_shapes(n):
     return mnk
 
 
+def gemm_profile_stamps(buf):
+    """Stamp mode for the open profile window: every GEMM kernel's blocks record {start, end}
+    s_memrealtime ticks into `buf` (int64 device tensor, 2 per block) instead of HIP events."""
+    assert buf.dtype == torch.int64 and buf.is_cuda and buf.numel() % 2 == 0
+    call("mms2ut_profile_stamps", buf.data_ptr(), buf.numel() // 2)
+
+
+def gemm_profile_durations(buf, n):
+    """Per-launch kernel durations (ms, numpy float64) of the last stamp-mode window: max(end) -
+    min(start) over each launch's blocks; NaN for launches past the buffer's capacity."""
+    import ctypes
+    import numpy as np
+    fl = np.zeros((max(n, 0), 2), np.int64)
+    if n:
+        call("mms2ut_profile_blocks", fl.ctypes.data, int(n))
+    khz = ctypes.c_int()
+    call("mms2ut_wallclock_khz", ctypes.byref(khz))
+    st = buf.view(-1, 2).cpu().numpy()
+    cap = st.shape[0]
+    out = np.full(n, np.nan)
+    for i, (b0, b1) in enumerate(fl.tolist()):
+        if b1 <= cap and b1 > b0:
+            out[i] = (st[b0:b1, 1].max() - st[b0:b1, 0].min()) / khz.value   # ticks / kHz = ms
+    return out
+
+
 def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
            ldc=None, alpha=1.0):
     """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue)."""
