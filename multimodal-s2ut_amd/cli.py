@@ -19,7 +19,7 @@ import time
 
 import torch
 
-from . import runtime
+from . import data, runtime
 from .data import SyntheticSpeechMulti30K
 from .parallel import init_from_env
 from .plugins import REGISTRY, build_parser
@@ -61,13 +61,14 @@ def main(argv=None):
                                  vocab=cfg["vocab_size"], img_dim=cfg["image_feat_dim"],
                                  with_images=bool(fus is not None and cfg["fusion"]))
     batches = ds.batches(args.max_tokens)
-    g = torch.Generator().manual_seed(args.seed)
     upd, t0, ntok = start, time.time(), 0.0
+    costs = [data.padded_cost([int(ds.lengths[i]) for i in b]) for b in batches]
+    epoch = 1
     while upd < args.max_update:
-        order = torch.randperm(len(batches), generator=g).tolist()
-        # equal batch count per rank (fairseq pads the last shard with dummy batches)
-        order = order[: len(order) // world * world]
-        mine = order[rank::world]
+        # equal batch count per rank (fairseq pads the last shard with dummy batches); with balanced
+        # sharding the ranks of one step get batches of near-equal padded cost
+        mine = data.deal_batches(costs, world, args.seed, epoch, balanced=args.balanced_sharding)[rank]
+        epoch += 1
         mine = mine[: len(mine) // args.update_freq * args.update_freq]
         if not mine:
             raise SystemExit(f"mms2ut-train: {len(batches)} synthetic batches cannot feed {world} ranks x "
@@ -141,8 +142,7 @@ def _train_manifest(args, task, cfg, tr, fus, rank, world, dev, start=0):
     are shuffled with (seed, epoch) and dealt round-robin to ranks (fairseq ShardedIterator)."""
     import os
 
-    import numpy as np
-
+    from . import data as D
     from . import manifest as M
     if args.target_code_size is None:
         raise SystemExit("mms2ut-train: --target-is-code --target-code-size N is required for unit targets")
@@ -157,9 +157,9 @@ def _train_manifest(args, task, cfg, tr, fus, rank, world, dev, start=0):
     uf = args.update_freq
     while upd < args.max_update:
         batches = ds.batches(args.max_tokens, seed=args.seed, epoch=epoch, skip_invalid=True)
-        order = np.random.RandomState((args.seed + epoch) % 2 ** 32).permutation(len(batches)).tolist()
-        order = order[: len(order) // world * world]
-        mine = [batches[i] for i in order[rank::world]]
+        costs = [D.padded_cost(ds.n_frames[b].tolist()) for b in batches]
+        mine = [batches[i] for i in D.deal_batches(costs, world, args.seed, epoch,
+                                                      balanced=args.balanced_sharding)[rank]]
         mine = mine[: len(mine) // uf * uf]
         if not mine:
             raise SystemExit(f"mms2ut-train: {len(batches)} batches cannot feed {world} ranks x update-freq {uf}")

@@ -97,6 +97,38 @@ def batch_by_size(lengths, max_tokens, order=None):
     return batches
 
 
+def padded_cost(batch_lengths):
+    """Cost proxy of one batch for DP balancing: padded source frames B * Ts_max (what the GEMMs and
+    the fbank front end scale with) times 1 + Ts_max / 18432, the self-attention share of an encoder
+    layer at the base dims (4 Te^2 d over Te (8d^2 + 4dF) with Te = Ts / 4)."""
+    if not len(batch_lengths):
+        return 0.0
+    t = max(batch_lengths)
+    return len(batch_lengths) * t * (1.0 + t / 18432.0)
+
+
+def deal_batches(costs, world, seed, epoch=1, balanced=True):
+    """Assign batches to DP ranks for one epoch -> list (per rank) of batch indices, equal lengths.
+
+    balanced=False: fairseq's ShardedIterator — shuffle with (seed, epoch), drop the tail that does
+    not fill every rank, rank r takes positions r, r+world, ...
+    balanced=True (token-balanced sharding): sort the batches by ``costs``, cut the
+    sorted list into groups of ``world`` neighbours (similar padded cost), shuffle the group order
+    with (seed, epoch) and give rank r the r-th member of every group, so the ranks of one update
+    step run batches of near-equal cost and no rank waits on a long-tail batch of another.  The
+    dropped tail is the ``len % world`` cheapest batches."""
+    n = len(costs)
+    rs = np.random.RandomState((seed + epoch) % 2 ** 32)
+    if not balanced or world == 1:
+        order = rs.permutation(n).tolist()
+        order = order[: n // world * world]
+        return [order[r::world] for r in range(world)]
+    srt = np.argsort(np.asarray(costs, dtype=np.float64), kind="stable")[n % world:]
+    groups = srt.reshape(-1, world) if len(srt) else np.zeros((0, world), np.int64)
+    groups = groups[rs.permutation(len(groups))]
+    return [groups[:, r].tolist() for r in range(world)]
+
+
 class SyntheticSpeechMulti30K:
     """Deterministic synthetic corpus: per-utterance fbank-like features (or waveforms for the
     GPU front end), unit targets and ViT/DETR image features."""

@@ -602,6 +602,9 @@ def build_parser():
     p.add_argument("--gen-subset", default="test")
     p.add_argument("--required-batch-size-multiple", type=int, default=1)
     p.add_argument("--synthetic", action="store_true", help="synthetic Speech-Multi30K-shaped data")
+    p.add_argument("--no-balanced-sharding", dest="balanced_sharding", action="store_false",
+                   help="deal batches to DP ranks round-robin (fairseq ShardedIterator) instead of in "
+                        "groups of equal padded cost (SURVEY 8e token-balanced sharding)")
     # fairseq-generate (scripts/textless/2_inference.sh:34-44)
     p.add_argument("--beam", type=int, default=5)
     p.add_argument("--max-len-a", type=float, default=0.0)

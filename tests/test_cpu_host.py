@@ -193,3 +193,30 @@ def test_param_groups_tile_flat_buffer():
         a, b = [(x, y) for n, x, y in g if n == grp][0]
         off, _, n = ps.offsets[name]
         assert a <= off and off + n <= b, name
+
+
+def test_deal_batches_balanced_and_round_robin():
+    """DP batch dealing: equal batch counts per rank; balanced groups pair batches of
+    near-equal padded cost per update step; round-robin is fairseq's shuffled ShardedIterator."""
+    D = pkg("data")
+    corpus = D.SyntheticSpeechMulti30K(n_utts=3000, seed=1, with_images=False)
+    batches = corpus.batches(40000)
+    costs = [D.padded_cost([int(corpus.lengths[i]) for i in b]) for b in batches]
+    for world in (1, 2, 8):
+        bal = D.deal_batches(costs, world, seed=1, epoch=3)
+        rr = D.deal_batches(costs, world, seed=1, epoch=3, balanced=False)
+        assert len({len(m) for m in bal}) == 1 and len({len(m) for m in rr}) == 1
+        assert len(bal[0]) == len(batches) // world == len(rr[0])
+        flat = sorted(i for m in bal for i in m)
+        assert len(set(flat)) == len(flat)                      # no batch dealt twice
+        assert bal == D.deal_batches(costs, world, seed=1, epoch=3)   # deterministic per (seed, epoch)
+        if world > 1:
+            def eff(m):   # per-step DP efficiency: mean / max cost over the ranks (max sets the step time)
+                c = np.array([[costs[m[r][s]] for r in range(world)] for s in range(len(m[0]))])
+                return c.mean(1) / c.max(1)
+            eb, er = eff(bal), eff(rr)
+            assert eb.mean() >= er.mean() and np.median(eb) > 0.99
+    # round-robin: the legacy permutation dealing
+    order = np.random.RandomState(4).permutation(len(batches)).tolist()
+    order = order[: len(order) // 2 * 2]
+    assert D.deal_batches(costs, 2, seed=1, epoch=3, balanced=False) == [order[0::2], order[1::2]]
