@@ -43,6 +43,7 @@ struct AttnP {
   const float* Dd;                  // [Z*Tq] rowsum(dO*O)
   h16* dq; h16* dk; h16* dv;
   long lddq, lddk, lddv, sdqb, sdkb, sdvb;
+  int kv16;                         // dK / dV rows 16-B aligned: the fused backward stores 16 B per lane
 };
 
 template <int HD>
@@ -153,6 +154,18 @@ MMS_DEV float xsum16_32(float v) {
   return v + __shfl_xor(v, 32, 64);
 }
 
+#ifdef MMS_ATTN_PHASES
+// diagnostic build only (scripts/attn_phases.py): s_memtime at the phase boundaries of the first
+// blocks' first chunks, read back with mms2ut_diag_attn_phases
+__device__ unsigned long long g_attn_ph[64 * 64];
+#define PH_STAMP(slot)                                                                          \
+  do {                                                                                          \
+    if (ph_blk < 64 && tid == 0 && (slot) < 64) g_attn_ph[ph_blk * 64 + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PH_STAMP(slot) do { } while (0)
+#endif
+
 // ============================================================================ forward
 // SHORT (Tk <= 128): the head's whole K / V (<= 2 tiles) is loaded into LDS in one burst up front
 // — one load latency per block instead of one per 64-key tile — and the tile loop runs without
@@ -175,6 +188,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   const h16* Q = P.q + b * P.sqb + h * HD;
   const h16* K = P.k + b * P.skb + h * HD;
   const h16* V = P.v + b * P.svb + h * HD;
+  const int tid = threadIdx.x, ph_blk = blockIdx.y * gridDim.x + blockIdx.x;
+  (void)tid; (void)ph_blk;
+  PH_STAMP(0);
   // Q^T fragments (B operand): lane -> Q[q_own][kk*32 + 8g .. +7]
   h16x8 qf[NKK];
 #pragma unroll
@@ -219,7 +235,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   } else {
     if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
   }
+  PH_STAMP(1);
   for (int kb = 0; kb < kmax; kb += KB) {
+    PH_STAMP(2 + 2 * (kb / KB));
     const h16* tK = SHORT ? sK + kb * LD : sK;
     const h16* tV = SHORT ? sV + kb * LD : sV;
     if constexpr (!SHORT) {
@@ -228,6 +246,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
       __syncthreads();
       if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
     }
+    PH_STAMP(3 + 2 * (kb / KB));
     // a wave past the last query row, or whose rows all precede this key tile (causal), only
     // helps stage K/V
     if (w_row0 >= P.Tq || (P.causal && kb > w_row0 + 15)) continue;
@@ -292,6 +311,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
       for (int i = 0; i < NDT; ++i) o[i] = mfma(frag_tr<HD>(tV, 32 * c, 16 * i, lane), pf, o[i]);
     }
   }
+  PH_STAMP(40);
   if (q_own < P.Tq) {
     const float inv = l > 0.f ? dscale / l : 0.f;
     h16* O = P.o + b * P.sob + h * HD + (long)q_own * P.ldo;
@@ -302,6 +322,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
     // natural-log LSE of the scaled scores (the backward's exp(s*scale - L))
     if (g == 0 && P.lse) P.lse[(long)z * P.Tq + q_own] = (l > 0.f) ? m * P.scale + __logf(l) : -INFINITY;
   }
+  PH_STAMP(41);
 }
 
 // ============================================================================ backward prep
@@ -553,6 +574,7 @@ struct FusedCfg {
   static constexpr int CH = HD / 8, NLQ = (QC * CH + 511) / 512, NLK = (TKP * CH + 511) / 512;
 };
 
+
 template <int HD, int NKC>
 __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
   if (P.thresh) P.seed = mms_step_seed(P.seed);
@@ -625,6 +647,9 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
   // are loaded into registers while the current head's MFMA phases run
   int z = blockIdx.x;
   if (z >= Z) return;
+  const int ph_blk = blockIdx.x;
+  (void)ph_blk;
+  PH_STAMP(0);
   load_chunk(z, 0);
   load_kv(z);
   if (tid < QC) sD[0][tid] = 0.f;
@@ -659,7 +684,9 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
       const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)Tq * P.Tk - 1);  // uniform
       const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
       // ---- phase 1: staged rows -> LDS, D = rowsum(dO*O); prefetch the next chunk / head
+      PH_STAMP(1 + 5 * gc);
       __syncthreads();  // previous chunk's phase 3 is done with sDS, its phase 2 with sQ / sDO
+      PH_STAMP(2 + 5 * gc);
 #pragma unroll
       for (int n = 0; n < NLQ; ++n) {
         const int i = tid + n * 512, r = i / CH, c = i % CH;
@@ -677,6 +704,7 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
       if (!LAST) load_chunk(z, qbase + QC);
       else if (znext < Z) load_chunk(znext, 0);
       __syncthreads();
+      PH_STAMP(3 + 5 * gc);
       // ---- phase 2: wave w owns keys 16w + 128j: dV, dK accumulate, dS^T -> LDS
 #pragma unroll
       for (int j = 0; j < NKC; ++j) {
@@ -739,7 +767,37 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
       }
       if constexpr (LAST) {
         // dK, dV of the wave's own keys (keys in [klen, Tk) are written as zeros); then the next
-        // head's K / V start loading behind phase 3
+        // head's K / V start loading behind phase 3.  Lane (key, g) holds d = 16i + 4g .. +3 of its
+        // key row: with 16-B rows the lanes g and g ^ 1 (lane ^ 16, same key) swap halves so that
+        // each stores 8 consecutive d (even g for even i, odd g for odd i) — half the store
+        // instructions of the 8-B form, whose issue queue otherwise stalls phase 3's dQ stores.
+        if (P.kv16) {
+          typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+          const bool godd = (g & 1) != 0;
+#pragma unroll
+          for (int j = 0; j < NKC; ++j) {
+            const int key_own = 16 * w + 128 * j + (lane & 15);
+            h16* DK = P.dk + b * P.sdkb + h * HD + (long)key_own * P.lddk;
+            h16* DV = P.dv + b * P.sdvb + h * HD + (long)key_own * P.lddv;
+            const int gb = 4 * (g & 2);   // first d of the lane pair's 8-column group
+#pragma unroll
+            for (int i = 0; i < NDT; ++i) {
+              const f32x4 a = dk[j][i] * P.scale, c = dv[j][i];
+              const h16x4 ah = h16x4{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3]};
+              const h16x4 ch = h16x4{(h16)c[0], (h16)c[1], (h16)c[2], (h16)c[3]};
+              typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+              const u32x2_ au = __builtin_bit_cast(u32x2_, ah), cu = __builtin_bit_cast(u32x2_, ch);
+              const u32x2_ ap = {(unsigned)__shfl_xor((int)au[0], 16, 64), (unsigned)__shfl_xor((int)au[1], 16, 64)};
+              const u32x2_ cp = {(unsigned)__shfl_xor((int)cu[0], 16, 64), (unsigned)__shfl_xor((int)cu[1], 16, 64)};
+              if (key_own < P.Tk && godd == ((i & 1) != 0)) {
+                const u32x4_ ka = godd ? u32x4_{ap[0], ap[1], au[0], au[1]} : u32x4_{au[0], au[1], ap[0], ap[1]};
+                const u32x4_ va = godd ? u32x4_{cp[0], cp[1], cu[0], cu[1]} : u32x4_{cu[0], cu[1], cp[0], cp[1]};
+                *reinterpret_cast<u32x4_*>(DK + 16 * i + gb) = ka;
+                *reinterpret_cast<u32x4_*>(DV + 16 * i + gb) = va;
+              }
+            }
+          }
+        } else {
 #pragma unroll
         for (int j = 0; j < NKC; ++j) {
           const int key_own = 16 * w + 128 * j + (lane & 15);
@@ -754,9 +812,12 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
             }
           }
         }
+        }
         if (znext < Z) load_kv(znext);
       }
+      PH_STAMP(4 + 5 * gc);
       __syncthreads();
+      PH_STAMP(5 + 5 * gc);
       // ---- phase 3: query tile w % NQT, d tiles (w / NQT)*NDW ..: dQ^T[d][q] = K^T[d][keys] dS^T[keys][q]
       {
         const int q0 = 16 * (w % NQT), qa0 = qbase + q0, d0 = (w / NQT) * NDW, q_own = qa0 + (lane & 15);
@@ -842,13 +903,21 @@ extern "C" int mms2ut_mha_varlen_fwd(const mms2ut_attn_args* a, hipStream_t s) {
   AttnP P = make_params(a);
   // each wave owns 16 query rows: 8 waves (128 rows) for Tq <= 128, else 16 waves (256 rows), so
   // that for every length up to 256 each (b, h) streams its K/V exactly once
-  const int nw = a->Tq > 16 * ATTN_NW ? 2 * ATTN_NW : ATTN_NW;
+  int nw = a->Tq > 16 * ATTN_NW ? 2 * ATTN_NW : ATTN_NW;
+  {
+    // MMS2UT_ATTN_FWD_NW=4: 64 query rows per block (A/B runs)
+    const char* ne = getenv("MMS2UT_ATTN_FWD_NW");
+    if (ne && ne[0] == '4') nw = ATTN_NW / 2;
+  }
   dim3 grid((a->Tq + 16 * nw - 1) / (16 * nw), a->B * a->H);
   return pick_hd(a->hd, [&](auto HDc) {
     constexpr int HD = decltype(HDc)::value;
     const char* se = getenv("MMS2UT_ATTN_FWD_SHORT");
     const bool short_k = a->Tk <= 2 * KB && !(se && se[0] == '0') && P.ldk < (1L << 24) && P.ldv < (1L << 24);
-    if (nw == ATTN_NW) {
+    if (nw == ATTN_NW / 2) {
+      if (short_k) hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW / 2, true>), grid, dim3(32 * ATTN_NW), 0, s, P);
+      else hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW / 2>), grid, dim3(32 * ATTN_NW), 0, s, P);
+    } else if (nw == ATTN_NW) {
       if (short_k) hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW, true>), grid, dim3(64 * ATTN_NW), 0, s, P);
       else hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW>), grid, dim3(64 * ATTN_NW), 0, s, P);
     } else {
@@ -872,6 +941,11 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
   P.dq = dq; P.lddq = lddq; P.sdqb = sdqb ? sdqb : (long)a->Tq * lddq;
   P.dk = dk; P.lddk = lddk; P.sdkb = sdkb ? sdkb : (long)a->Tk * lddk;
   P.dv = dv; P.lddv = lddv; P.sdvb = sdvb ? sdvb : (long)a->Tk * lddv;
+  {
+    const char* ke = getenv("MMS2UT_ATTN_KV16");
+    P.kv16 = !(ke && ke[0] == '0') && P.lddk % 8 == 0 && P.lddv % 8 == 0 && P.sdkb % 8 == 0 && P.sdvb % 8 == 0 &&
+             (a->hd % 16) == 0 && ((uintptr_t)P.dk & 15) == 0 && ((uintptr_t)P.dv & 15) == 0;
+  }
   const int Z = a->B * a->H;
   const char* fe = getenv("MMS2UT_ATTN_FUSED");
   const bool fused_ok = !(fe && fe[0] == '0') && a->Tk <= 256 && a->hd <= 96 &&
@@ -922,3 +996,13 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
 namespace mms {
 int bind_step_seed_attention(const uint64_t* d) { return mms_bind_step_seed_tu(d); }
 }  // namespace mms
+
+#ifdef MMS_ATTN_PHASES
+extern "C" int mms2ut_diag_attn_phases(unsigned long long* host, int n, int clear) {
+  if (clear) {
+    static unsigned long long zero[64 * 64] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_attn_ph), zero, sizeof(zero)) != hipSuccess;
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_attn_ph), sizeof(unsigned long long) * (n < 4096 ? n : 4096)) != hipSuccess;
+}
+#endif
