@@ -705,29 +705,49 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
       else if (znext < Z) load_chunk(znext, 0);
       __syncthreads();
       PH_STAMP(3 + 5 * gc);
-      // ---- phase 2: wave w owns keys 16w + 128j: dV, dK accumulate, dS^T -> LDS
+      // ---- phase 2: wave w owns keys 16w + 128j: dV, dK accumulate, dS^T -> LDS.  Query steps
+      // outermost: the step's Q / dO row fragments and the transposed dO / Q operands of the dV / dK
+      // MFMAs are read from LDS once and used for all NKC key groups of the wave (half the LDS
+      // reads of a key-group-outer loop at NKC = 2); values and rounding points are unchanged.
+      for (int qs = 0; qs < QC; qs += 32) {
+        const int qa = qbase + qs;
+        bool act[NKC];
+        bool any = false;
 #pragma unroll
-      for (int j = 0; j < NKC; ++j) {
-        const int kw0 = 16 * w + 128 * j, key_own = kw0 + (lane & 15);
-        for (int qs = 0; qs < QC; qs += 32) {
-          const int qa = qbase + qs;
-          if (kw0 >= klen || qa >= Tq || (P.causal && qa + 31 < kw0)) {
+        for (int j = 0; j < NKC; ++j) {
+          const int kw0 = 16 * w + 128 * j, key_own = kw0 + (lane & 15);
+          act[j] = !(kw0 >= klen || qa >= Tq || (P.causal && qa + 31 < kw0));   // wave-uniform
+          any = any || act[j];
+          if (!act[j]) {
             *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 4 * g) = h16x4{};
             *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + qs + 16 + 4 * g) = h16x4{};
-            continue;
           }
-          f32x4 pt[2], dst[2];
+        }
+        if (!any) continue;
+        h16x8 pf[NKC], sf[NKC];
 #pragma unroll
-          for (int tt = 0; tt < 2; ++tt) {
-            const int q0 = qs + 16 * tt;
-            f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dp = sc;
+        for (int tt = 0; tt < 2; ++tt) {
+          const int q0 = qs + 16 * tt;
+          f32x4 sc[NKC], dp[NKC];
 #pragma unroll
-            for (int kk = 0; kk < NKK; ++kk) {
-              sc = mfma(frag_rows<HD>(sQ, q0, kk * 32, lane), frag_rows<HD>(sK, kw0, kk * 32, lane), sc);
-              dp = mfma(frag_rows<HD>(sDO, q0, kk * 32, lane), vf[j][kk], dp);
+          for (int j = 0; j < NKC; ++j) { sc[j] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[j] = sc[j]; }
+#pragma unroll
+          for (int kk = 0; kk < NKK; ++kk) {
+            const h16x8 qf = frag_rows<HD>(sQ, q0, kk * 32, lane);
+            const h16x8 df = frag_rows<HD>(sDO, q0, kk * 32, lane);
+#pragma unroll
+            for (int j = 0; j < NKC; ++j) {
+              if (!act[j]) continue;
+              sc[j] = mfma(qf, frag_rows<HD>(sK, 16 * w + 128 * j, kk * 32, lane), sc[j]);
+              dp[j] = mfma(df, vf[j][kk], dp[j]);
             }
-            const f32x4 Lv = *reinterpret_cast<const f32x4*>(L + q0 + 4 * g);
-            const f32x4 Dv = *reinterpret_cast<const f32x4*>(Dr + q0 + 4 * g);
+          }
+          const f32x4 Lv = *reinterpret_cast<const f32x4*>(L + q0 + 4 * g);
+          const f32x4 Dv = *reinterpret_cast<const f32x4*>(Dr + q0 + 4 * g);
+#pragma unroll
+          for (int j = 0; j < NKC; ++j) {
+            if (!act[j]) continue;
+            const int kw0 = 16 * w + 128 * j, key_own = kw0 + (lane & 15);
             // a 16x16 (query, key) tile valid everywhere (rows < Tq, keys < klen, causal: every key
             // at or before every row) skips the per-element masks
             const bool full = qbase + q0 + 15 < Tq && kw0 + 15 < klen && (!P.causal || kw0 + 15 <= qbase + q0);
@@ -743,25 +763,35 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
                 for (int r = 0; r < 4; ++r) keep[r] = mms_keep(P.seed, c0 + (uint32_t)(r * P.Tk), P.thresh);
               }
             }
+            f32x4 pt, dst;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int q = qbase + q0 + 4 * g + r;
               const bool ok = full || (q < Tq && key_own < klen && (!P.causal || key_own <= q));
-              const float e = __builtin_amdgcn_exp2f(fmaf(sc[r], c2, -Lv[r]));
+              const float e = __builtin_amdgcn_exp2f(fmaf(sc[j][r], c2, -Lv[r]));
               const float pr = ok ? e : 0.f;
               const float mk = keep[r] ? dscale : 0.f;
-              pt[tt][r] = pr * mk;
-              dst[tt][r] = pr * fmaf(dp[r], mk, -Dv[r]);
+              pt[r] = pr * mk;
+              dst[r] = pr * fmaf(dp[j][r], mk, -Dv[r]);
             }
-            *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + q0 + 4 * g) =
-                h16x4{(h16)dst[tt][0], (h16)dst[tt][1], (h16)dst[tt][2], (h16)dst[tt][3]};
-          }
-          const h16x8 pf = pack8(pt[0], pt[1]);
-          const h16x8 sf = pack8(dst[0], dst[1]);
+            const h16x4 dh = h16x4{(h16)dst[0], (h16)dst[1], (h16)dst[2], (h16)dst[3]};
+            *reinterpret_cast<h16x4*>(sDS + key_own * LDS_T + q0 + 4 * g) = dh;
 #pragma unroll
-          for (int i = 0; i < NDT; ++i) {
-            dv[j][i] = mfma(frag_tr<HD>(sDO, qs, 16 * i, lane), pf, dv[j][i]);
-            dk[j][i] = mfma(frag_tr<HD>(sQ, qs, 16 * i, lane), sf, dk[j][i]);
+            for (int r = 0; r < 4; ++r) {
+              pf[j][4 * tt + r] = (h16)pt[r];
+              sf[j][4 * tt + r] = dh[r];
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NDT; ++i) {
+          const h16x8 td = frag_tr<HD>(sDO, qs, 16 * i, lane);
+          const h16x8 tq = frag_tr<HD>(sQ, qs, 16 * i, lane);
+#pragma unroll
+          for (int j = 0; j < NKC; ++j) {
+            if (!act[j]) continue;
+            dv[j][i] = mfma(td, pf[j], dv[j][i]);
+            dk[j][i] = mfma(tq, sf[j], dk[j][i]);
           }
         }
       }
