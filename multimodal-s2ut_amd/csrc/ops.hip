@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
                                                        long rows, int D, h16* __restrict__ dxd, float p,
                                                        uint32_t thresh, uint64_t seed, uint64_t offset,
                                                        long dgrp, long dgrp_out, float pin, uint32_t thin,
-                                                       uint64_t sin, uint64_t oin) {
+                                                       uint64_t sin, uint64_t oin, int iters) {
   if (thresh) seed = mms_step_seed(seed);
   if (thin) sin = mms_step_seed(sin);
   __shared__ __attribute__((aligned(16))) float red[4][2][C8 * 256];
@@ -292,94 +292,99 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
 #pragma unroll
     for (int e = 0; e < 8; ++e) { gam[c][e] = (float)gg[e]; dg[c][e] = 0.f; db[c][e] = 0.f; }
   }
-  const long rb = (long)blockIdx.x * 8 * NP;
-  const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
-  h16x8 xv[NP][C8], dv[NP][C8], rv[NP][C8];
-  float mu[NP], rs[NP];
-  long row[NP];
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    row[k] = rb + 2 * (w + 4 * k) + half;
-    const bool ok = row[k] < rows;
-    mu[k] = ok ? mean[row[k]] : 0.f;
-    rs[k] = ok ? rstd[row[k]] : 0.f;
-#pragma unroll
-    for (int c = 0; c < C8; ++c) {
-      const long off = row[k] * D + (hl + 32 * c) * 8;
-      xv[k][c] = ok ? *reinterpret_cast<const h16x8*>(x + off) : z8;
-      // optional dy layout remap (rows grouped dgrp at a time into dgrp_out-row groups)
-      const long drow = dgrp ? (row[k] / dgrp) * dgrp_out + row[k] % dgrp : row[k];
-      dv[k][c] = ok ? *reinterpret_cast<const h16x8*>(dy + drow * D + (hl + 32 * c) * 8) : z8;
-      rv[k][c] = (ok && dres && dx) ? *reinterpret_cast<const h16x8*>(dres + off) : z8;
-    }
-  }
-  if (thin) {
-    // dy = dropout(dy_in) with the counters of the unpadded element index, rounded to fp16 as a
-    // separate dropout pass would store it
-    const float dsi = 1.f / (1.f - pin);
-#pragma unroll
-    for (int k = 0; k < NP; ++k)
-#pragma unroll
+  // the block walks `iters` consecutive groups of 8*NP rows, keeping its dgamma / dbeta column sums
+  // in registers across them: one partial row per block instead of one per group
+  for (int it = 0; it < iters; ++it) {
+    const long rb = ((long)blockIdx.x * iters + it) * 8 * NP;
+    if (rb >= rows) break;
+    const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+    h16x8 xv[NP][C8], dv[NP][C8], rv[NP][C8];
+    float mu[NP], rs[NP];
+    long row[NP];
+  #pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      row[k] = rb + 2 * (w + 4 * k) + half;
+      const bool ok = row[k] < rows;
+      mu[k] = ok ? mean[row[k]] : 0.f;
+      rs[k] = ok ? rstd[row[k]] : 0.f;
+  #pragma unroll
       for (int c = 0; c < C8; ++c) {
-        bool k0[4], k1[4];
-        const uint64_t ctr = oin + (uint64_t)(row[k] * D + (hl + 32 * c) * 8);
-        mms_keep4(sin, ctr, thin, k0);
-        mms_keep4(sin, ctr + 4, thin, k1);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          dv[k][c][e] = (h16)(k0[e] ? (float)dv[k][c][e] * dsi : 0.f);
-          dv[k][c][e + 4] = (h16)(k1[e] ? (float)dv[k][c][e + 4] * dsi : 0.f);
-        }
+        const long off = row[k] * D + (hl + 32 * c) * 8;
+        xv[k][c] = ok ? *reinterpret_cast<const h16x8*>(x + off) : z8;
+        // optional dy layout remap (rows grouped dgrp at a time into dgrp_out-row groups)
+        const long drow = dgrp ? (row[k] / dgrp) * dgrp_out + row[k] % dgrp : row[k];
+        dv[k][c] = ok ? *reinterpret_cast<const h16x8*>(dy + drow * D + (hl + 32 * c) * 8) : z8;
+        rv[k][c] = (ok && dres && dx) ? *reinterpret_cast<const h16x8*>(dres + off) : z8;
       }
-  }
-#pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int c = 0; c < C8; ++c)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
-        const float d = (float)dv[k][c][e];
-        const float gd = d * gam[c][e];
-        s1 += gd * xh;
-        s2 += gd;
-        dg[c][e] += d * xh;
-        db[c][e] += d;
-      }
-    if (!dx) continue;
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      s1 += __shfl_xor(s1, o, 64);
-      s2 += __shfl_xor(s2, o, 64);
     }
-    s1 *= invD;
-    s2 *= invD;
-    if (row[k] >= rows) continue;
-#pragma unroll
-    for (int c = 0; c < C8; ++c) {
-      const long off = row[k] * D + (hl + 32 * c) * 8;
-      float o8[8];
-      h16x8 ov;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
-        o8[e] = rs[k] * ((float)dv[k][c][e] * gam[c][e] - xh * s1 - s2) + (float)rv[k][c][e];
-        ov[e] = (h16)o8[e];
+    if (thin) {
+      // dy = dropout(dy_in) with the counters of the unpadded element index, rounded to fp16 as a
+      // separate dropout pass would store it
+      const float dsi = 1.f / (1.f - pin);
+  #pragma unroll
+      for (int k = 0; k < NP; ++k)
+  #pragma unroll
+        for (int c = 0; c < C8; ++c) {
+          bool k0[4], k1[4];
+          const uint64_t ctr = oin + (uint64_t)(row[k] * D + (hl + 32 * c) * 8);
+          mms_keep4(sin, ctr, thin, k0);
+          mms_keep4(sin, ctr + 4, thin, k1);
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            dv[k][c][e] = (h16)(k0[e] ? (float)dv[k][c][e] * dsi : 0.f);
+            dv[k][c][e + 4] = (h16)(k1[e] ? (float)dv[k][c][e + 4] * dsi : 0.f);
+          }
+        }
+    }
+  #pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      float s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+      for (int c = 0; c < C8; ++c)
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
+          const float d = (float)dv[k][c][e];
+          const float gd = d * gam[c][e];
+          s1 += gd * xh;
+          s2 += gd;
+          dg[c][e] += d * xh;
+          db[c][e] += d;
+        }
+      if (!dx) continue;
+  #pragma unroll
+      for (int o = 16; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
       }
-      *reinterpret_cast<h16x8*>(dx + off) = ov;
-      if (dxd) {
-        bool k0[4] = {true, true, true, true}, k1[4] = {true, true, true, true};
-        if (thresh) {
-          mms_keep4(seed, offset + (uint64_t)off, thresh, k0);
-          mms_keep4(seed, offset + (uint64_t)off + 4, thresh, k1);
+      s1 *= invD;
+      s2 *= invD;
+      if (row[k] >= rows) continue;
+  #pragma unroll
+      for (int c = 0; c < C8; ++c) {
+        const long off = row[k] * D + (hl + 32 * c) * 8;
+        float o8[8];
+        h16x8 ov;
+  #pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
+          o8[e] = rs[k] * ((float)dv[k][c][e] * gam[c][e] - xh * s1 - s2) + (float)rv[k][c][e];
+          ov[e] = (h16)o8[e];
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ov[e] = (h16)(k0[e] ? o8[e] * dscale : 0.f);
-          ov[e + 4] = (h16)(k1[e] ? o8[e + 4] * dscale : 0.f);
+        *reinterpret_cast<h16x8*>(dx + off) = ov;
+        if (dxd) {
+          bool k0[4] = {true, true, true, true}, k1[4] = {true, true, true, true};
+          if (thresh) {
+            mms_keep4(seed, offset + (uint64_t)off, thresh, k0);
+            mms_keep4(seed, offset + (uint64_t)off + 4, thresh, k1);
+          }
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ov[e] = (h16)(k0[e] ? o8[e] * dscale : 0.f);
+            ov[e + 4] = (h16)(k1[e] ? o8[e + 4] * dscale : 0.f);
+          }
+          *reinterpret_cast<h16x8*>(dxd + off) = ov;
         }
-        *reinterpret_cast<h16x8*>(dxd + off) = ov;
       }
     }
   }
@@ -896,8 +901,24 @@ extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
   return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
 }
 
+// groups of 8*NP rows per ln_bwd16 block: enough blocks to fill the chip (MMS2UT_LN_BLOCKS, default
+// 1024), each folding its groups' dgamma / dbeta into one partial row — the partials (rows / 8 x 6 KB
+// at D = 768, ~35 MB for the image LayerNorm) are what colsum_parts reads back on the side stream
+static int ln16_iters(int64_t rows) {
+  static long target = 0;
+  if (target == 0) {
+    const char* e = getenv("MMS2UT_LN_BLOCKS");
+    target = e ? atol(e) : 1024;
+    if (target < 1) target = 1024;
+  }
+  const long groups = (rows + 8 * ln16_np() - 1) / (8 * ln16_np());
+  const long it = (groups + target - 1) / target;
+  return (int)(it > 1 ? it : 1);
+}
+
 extern "C" int mms2ut_layernorm_bwd_nparts(int64_t rows, int D) {
-  const int rpb = ln16_path(D) ? 8 * ln16_np() : LN_BWD_ROWS;
+  if (!ln16_path(D)) return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
+  const long rpb = 8L * ln16_np() * ln16_iters(rows);
   return (int)((rows + rpb - 1) / rpb);
 }
 
@@ -915,7 +936,7 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
     const int np = ln16_np();
 #define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
                                           gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
-                                          offset, 0L, 0L, 0.f, 0u, (uint64_t)0, (uint64_t)0); break;
+                                          offset, 0L, 0L, 0.f, 0u, (uint64_t)0, (uint64_t)0, ln16_iters(rows)); break;
     switch ((D / 256) * 8 + np) {
       CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1) CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
       CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
@@ -952,7 +973,8 @@ extern "C" int mms2ut_layernorm_bwd_ex(const h16* dy, const h16* x, const h16* g
   const int np = ln16_np();
 #define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
                                           gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
-                                          offset, (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset); break;
+                                          offset, (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset, \
+                                          ln16_iters(rows)); break;
   switch ((D / 256) * 8 + np) {
     CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1) CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
     CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
