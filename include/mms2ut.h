@@ -90,13 +90,20 @@ typedef struct mms2ut_gemm_args {
   int64_t ld_red_out;
   mms2ut_half* red_bias;
   int32_t* red_cnt;
+  /* 1-bit activity mask of a ReLU+dropout output, bit (n % 8) of byte mask[m*ld_mask + n/8] =
+   * (the stored fp16 C[m][n] > 0): MMS_EPI_RELU_DROP also writes it when mask != null (N % 8 == 0);
+   * MMS_EPI_RELU_DROP_BWD with aux == null reads it instead of the fp16 activation (1/16 of the
+   * bytes for the fc2 dgrad, bit-identical output).                                            */
+  uint8_t* mask;
+  int64_t ld_mask;
 } mms2ut_gemm_args;
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
 
 /* live GEMM timing for the benchmark roofline: between begin/end every mms2ut_gemm_f16 launch
- * is bracketed by HIP events on its own stream; end() synchronises and returns the summed
- * kernel time, the launch count and the launched (padded) FLOPs.  Not thread-safe.          */
+ * is bracketed by HIP events on its own stream (or, in stamp mode below, timed by its own
+ * workgroups); end() synchronises and returns the summed event time (0 in stamp mode), the launch
+ * count and the launched (padded) FLOPs.  Bench-only instrumentation, not thread-safe.      */
 int mms2ut_profile_begin(int max_launches);
 int mms2ut_profile_end(float* total_ms, int* launches, double* flops);
 /* algorithmic HBM bytes of the GEMM launches of the last begin/end window (A and B read once, C

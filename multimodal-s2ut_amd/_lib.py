@@ -36,6 +36,7 @@ class GemmArgs(C.Structure):
         ("rowsum", vp), ("ld_rowsum", i64),
         ("splitk_ws", vp), ("splitk_ws_floats", i64),
         ("red_out", vp), ("ld_red_out", i64), ("red_bias", vp), ("red_cnt", vp),
+        ("mask", vp), ("ld_mask", i64),
     ]
 
 

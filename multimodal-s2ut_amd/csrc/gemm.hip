@@ -49,6 +49,7 @@ struct GemmP {
   int group_m;  // tile-rows per L2 group (tile_coords)
   h16* red_out; long ld_red_out; h16* red_bias; int* red_cnt;  // in-launch split-K reduction
   unsigned long long* stamps;  // profiling: per block {first, last} s_memrealtime tick, or null
+  uint8_t* mask; long ldmask;  // RELU_DROP: written when set; RELU_DROP_BWD: read when aux is null
 };
 
 // Live kernel timing (bench roofline): with P.stamps set, thread 0 of every block stores the
@@ -153,6 +154,14 @@ MMS_DEV h16x8 read_frag(const char* lds, int sub, int kk, int lane) {
   }
 }
 
+// 1-bit ReLU/dropout mask layout (ldmask = N/8 byte columns): 64-row blocks, and inside a block the
+// 8 rows m, m+8, ..., m+56 of one 8-column group in one 8-byte word, so that a lane of the staged
+// epilogue (8 columns x rows m0 + 8*pass) writes / reads its whole mask as one u64:
+//   byte(m, n) = ((m / 64) * ldmask + n / 8) * 64 + (m % 8) * 8 + (m % 64) / 8,  bit = n % 8
+MMS_DEV long mask_byte(long m, int n, long ldmask) {
+  return (((m >> 6) * ldmask + (n >> 3)) << 6) + ((m & 7) << 3) + ((m & 63) >> 3);
+}
+
 MMS_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 // torch F.gelu (approximate='none'): 0.5 z (1 + erf(z / sqrt 2)) and its derivative
 MMS_DEV float gelu_(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
@@ -228,10 +237,16 @@ MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, in
       for (int r = 0; r < 4; ++r) if (n + r < N) g_row[n + r] = (h16)g[r];
     }
   } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
-    float h[4];
-    ld4(auxz + (long)m * P.ldaux, n, h);
+    if (auxz) {
+      float h[4];
+      ld4(auxz + (long)m * P.ldaux, n, h);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
+      for (int r = 0; r < 4; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
+    } else {   // 1-bit mask: bits n%8 .. n%8+3 of byte n/8
+      const unsigned bits = (unsigned)P.mask[mask_byte(m, n, P.ldmask)] >> (n & 7);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = ((bits >> r) & 1u) ? x[r] * dscale : 0.f;
+    }
   } else if (EPI == MMS_EPI_F16_ACC) {
     float c[4];
     ld4(C, n, c);
@@ -294,6 +309,12 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
   if (!(P.vec16 && n + 7 < N)) {
     epilogue_store<EPI>(P, Cz, auxz, m, n, f32x4{v[0], v[1], v[2], v[3]});
     epilogue_store<EPI>(P, Cz, auxz, m, n + 4, f32x4{v[4], v[5], v[6], v[7]});
+    if (EPI == MMS_EPI_RELU_DROP && P.mask) {   // from the values this thread just stored
+      const h16* C = reinterpret_cast<const h16*>(Cz) + (long)m * P.ldc;
+      unsigned b = 0;
+      for (int r = 0; r < 8; ++r) if (n + r < N && (float)C[n + r] > 0.f) b |= 1u << r;
+      P.mask[mask_byte(m, n, P.ldmask)] = (uint8_t)b;
+    }
     return;
   }
   float x[8];
@@ -344,10 +365,16 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
     for (int r = 0; r < 8; ++r) gv[r] = (h16)g[r];
     *reinterpret_cast<h16x8*>(P.out2 + (long)m * P.ldo2 + n) = gv;
   } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
-    float h[8];
-    ld8(auxz + (long)m * P.ldaux + n, h);
+    if (auxz) {
+      float h[8];
+      ld8(auxz + (long)m * P.ldaux + n, h);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
+      for (int r = 0; r < 8; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
+    } else {
+      const unsigned bits = P.mask[mask_byte(m, n, P.ldmask)];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) o[r] = ((bits >> r) & 1u) ? x[r] * dscale : 0.f;
+    }
   } else if (EPI == MMS_EPI_F16_ACC) {
     float c[8];
     ld8(C + n, c);
@@ -374,6 +401,12 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
 #pragma unroll
   for (int r = 0; r < 8; ++r) ov8[r] = (h16)o[r];
   *reinterpret_cast<h16x8*>(C + n) = ov8;
+  if (EPI == MMS_EPI_RELU_DROP && P.mask) {
+    unsigned b = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) b |= ((float)ov8[r] > 0.f ? 1u : 0u) << r;
+    P.mask[mask_byte(m, n, P.ldmask)] = (uint8_t)b;
+  }
 }
 
 // Epilogue through LDS: each wave parks its 64x64 fp32 accumulator tile in 16 KiB of the (now idle)
@@ -453,6 +486,14 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
   h16* C = reinterpret_cast<h16*>(Cz);
   h16x8 ax[8], ax2[8];
   const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+  // this lane's mask word: rows m0 + 8*pass (pass = byte), columns n..n+7 (bit); m0 % 64 < 8
+  unsigned long long* mword = nullptr;
+  unsigned long long mbits = 0;
+  // (only lanes with a valid first row: the buffer is padded to whole 64-row blocks of M)
+  if ((EPI == MMS_EPI_RELU_DROP || (EPI == MMS_EPI_RELU_DROP_BWD && !auxz)) && P.mask && m0 < P.M) {
+    mword = reinterpret_cast<unsigned long long*>(P.mask + mask_byte(m0, n, P.ldmask));
+    if (EPI == MMS_EPI_RELU_DROP_BWD) mbits = *mword;
+  }
 #pragma unroll
   for (int pass = 0; pass < 8; ++pass) {
     const int m = m0 + 8 * pass;
@@ -461,6 +502,11 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
     if (LOADS && m < P.M) {
       if (EPI == MMS_EPI_F16_ACC) {
         ax[pass] = *reinterpret_cast<const h16x8*>(C + (long)m * P.ldc + n);
+      } else if (EPI == MMS_EPI_RELU_DROP_BWD && !auxz) {
+        // 1-bit activity mask in place of the fp16 activation: expand to 1 / 0 (only > 0 is tested)
+        const unsigned bits = (unsigned)(mbits >> (8 * pass)) & 0xffu;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ax[pass][e] = (h16)(float)((bits >> e) & 1u);
       } else {
         ax[pass] = *reinterpret_cast<const h16x8*>(auxz + (long)m * P.ldaux + n);
         if (EPI == MMS_EPI_GATE) ax2[pass] = *reinterpret_cast<const h16x8*>(auxz + (long)m * P.ldaux + P.N + n);
@@ -536,9 +582,16 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
         else o = x[e];
         o8[e] = (h16)o;
       }
+      if (EPI == MMS_EPI_RELU_DROP && mword) {
+        unsigned b = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b |= ((float)o8[e] > 0.f ? 1u : 0u) << e;
+        mbits |= (unsigned long long)b << (8 * pass);
+      }
     }
     *reinterpret_cast<h16x8*>(C + (long)m * P.ldc + n) = o8;
   }
+  if (EPI == MMS_EPI_RELU_DROP && mword) *mword = mbits;   // rows past M: zero bits (never read)
 }
 
 template <bool A_KC, bool B_KC, int EPI>
@@ -1431,6 +1484,7 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
     const double c_bytes = (double)a->M * a->N * (a->epi == MMS_EPI_F32 ? 4.0 * (a->splitk > 0 ? a->splitk : 1) : 2.0);
     double extra = 0.0;
     if (a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_RELU_DROP_BWD || a->epi == MMS_EPI_F16_ACC) extra = 2.0 * a->M * a->N;
+    if (a->mask) extra = (double)a->M * a->N / 8.0;   // 1-bit mask written (RELU_DROP) or read instead of aux
     if (a->epi == MMS_EPI_GATE) extra = 6.0 * a->M * a->N;  // o, t read; g written
     g_prof.bytes += nb * (2.0 * ((double)a->M * a->K + (double)a->N * a->K) + c_bytes + extra);
   }
@@ -1528,7 +1582,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     mms2ut_gemm_args b = *a;
     b.C = a->splitk_ws; b.ldc = a->N; b.sC1 = b.sC2 = 0; b.sCsplit = (int64_t)a->M * a->N;
     b.epi = MMS_EPI_F32; b.bias = nullptr; b.aux = nullptr; b.out2 = nullptr; b.dropout_p = 0.f;
-    b.splitk_ws = nullptr;
+    b.splitk_ws = nullptr; b.mask = nullptr;
     const int rc = gemm_dispatch(&b, stream);
     if (rc) return rc;
     GemmP F{};
@@ -1537,8 +1591,10 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     F.aux = a->aux; F.ldaux = a->ldaux; F.out2 = a->out2; F.ldo2 = a->ldo2;
     F.p = a->dropout_p; F.thresh = mms_drop_thresh(a->dropout_p); F.seed = a->seed; F.offset = a->offset;
     F.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
-    MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD ||
-                  a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
+    F.mask = a->mask; F.ldmask = a->ld_mask;
+    MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux,
+                "gemm: epilogue needs aux");
+    MMS_REQUIRE(a->epi != MMS_EPI_RELU_DROP_BWD || a->aux || a->mask, "gemm: RELU_DROP_BWD needs aux or mask");
     MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");
     MMS_REQUIRE(a->ldc % 4 == 0 && (!a->aux || (a->ldaux % 4 == 0 && ((uintptr_t)a->aux & 7) == 0)) &&
                 (!a->bias || ((uintptr_t)a->bias & 7) == 0), "gemm: fixup operand alignment");
@@ -1562,14 +1618,21 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.p = a->dropout_p; P.thresh = mms_drop_thresh(a->dropout_p); P.seed = a->seed; P.offset = a->offset;
   P.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
   P.group_m = gemm_group_m();
+  if (a->mask) {
+    MMS_REQUIRE((a->epi == MMS_EPI_RELU_DROP || a->epi == MMS_EPI_RELU_DROP_BWD) && a->batch == 1 && a->N % 8 == 0 &&
+                    a->ld_mask == a->N / 8 && ((uintptr_t)a->mask & 7) == 0,
+                "gemm: the 1-bit mask needs epi RELU_DROP(_BWD), batch 1, N %% 8 == 0, ld_mask = N/8, 8-B alignment");
+    P.mask = a->mask; P.ldmask = a->ld_mask;
+  }
   if (a->red_cnt) {
     MMS_REQUIRE(a->epi == MMS_EPI_F32 && a->batch == 1 && a->N % 4 == 0 && a->ldc % 4 == 0 && a->red_out &&
                     a->ld_red_out % 4 == 0 && ((uintptr_t)a->red_out & 7) == 0 && ((uintptr_t)a->C & 15) == 0,
                 "gemm: in-launch split-K reduction needs epi F32, batch 1, N %% 4 == 0, aligned buffers");
     P.red_out = a->red_out; P.ld_red_out = a->ld_red_out; P.red_bias = a->red_bias; P.red_cnt = a->red_cnt;
   }
-  MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_RELU_DROP_BWD ||
-                a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux, "gemm: epilogue needs aux");
+  MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux,
+              "gemm: epilogue needs aux");
+  MMS_REQUIRE(a->epi != MMS_EPI_RELU_DROP_BWD || a->aux || a->mask, "gemm: RELU_DROP_BWD needs aux or mask");
   MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");
   {
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };

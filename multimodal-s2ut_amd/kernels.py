@@ -63,7 +63,7 @@ class Dropout:
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv=1,
          sA=(0, 0), sB=(0, 0), sC=(0, 0), epi=EPI_F16, alpha=1.0, bias=None, aux=None, ldaux=0,
          sX=(0, 0), out2=None, ldo2=0, p=0.0, seed=0, offset=0, ld_rng=0, splitk=1, sCsplit=0,
-         rowsum=None, ld_rowsum=0, red_out=None, red_bias=None, red_cnt=None):
+         rowsum=None, ld_rowsum=0, red_out=None, red_bias=None, red_cnt=None, mask=None):
     a = GemmArgs()
     a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
     a.M, a.N, a.K = int(M), int(N), int(K)
@@ -85,6 +85,9 @@ def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv
     if red_cnt is not None:
         a.red_out, a.ld_red_out = red_out.data_ptr(), int(red_out.stride(0))
         a.red_bias, a.red_cnt = _p(red_bias), red_cnt.data_ptr()
+    if mask is not None:   # 1-bit ReLU/dropout activity mask (relu_mask_alloc), written or read
+        assert mask.dtype == torch.uint8 and mask.shape[0] >= (M + 63) // 64 * 64 and mask.stride(1) == 1
+        a.mask, a.ld_mask = mask.data_ptr(), int(mask.stride(0))
     ws = None
     if splitk == 1 and epi != EPI_F32 and batch == 1 and rowsum is None and _SPLITK_FIX:
         s = _fixup_splits(M, N, K)
@@ -216,9 +219,26 @@ def gemm_profile_durations(buf, n):
     return out
 
 
+def relu_mask_alloc(M, N, device):
+    """Buffer of the 1-bit ReLU/dropout activity mask of an [M, N] output (N % 8 == 0): N/8 byte
+    columns, rows padded to 64 (gemm.hip mask_byte: 64-row blocks, 8 rows of one column group per
+    8-byte word)."""
+    return torch.empty((M + 63) // 64 * 64, N // 8, dtype=torch.uint8, device=device)
+
+
+def relu_mask_unpack(mask, M, N):
+    """bool [M, N] from a relu_mask_alloc buffer (tests)."""
+    ld = N // 8
+    b = mask.reshape(-1, ld, 8, 8)                  # [m/64][n/8][m%8][(m%64)/8]
+    b = b.permute(0, 3, 2, 1).reshape(-1, ld)[:M]    # rows m = 64*blk + 8*(m%64/8) + m%8
+    bits = torch.stack([(b >> i) & 1 for i in range(8)], dim=-1)
+    return bits.reshape(M, N).bool()
+
+
 def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
-           ldc=None, alpha=1.0):
-    """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue)."""
+           ldc=None, alpha=1.0, mask=None):
+    """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue).
+    mask: uint8 [M, N/8] written with EPI_RELU_DROP (bit n%8 of byte n/8 = out[m, n] > 0)."""
     M, K = x.shape
     N = W.shape[0]
     assert W.shape[1] == K, (W.shape, x.shape)
@@ -230,7 +250,7 @@ def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0
     gemm(x, W, out, M, N, K, lda=x.stride(0), ldb=W.stride(0), ldc=ldc or out.stride(0), epi=epi,
          bias=bias, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), out2=out2,
          ldo2=(out2.stride(0) if out2 is not None else 0), p=p, seed=seed, offset=off, ld_rng=N,
-         alpha=alpha)
+         alpha=alpha, mask=mask)
     return out
 
 
@@ -294,10 +314,11 @@ class TransposedWeights:
         return self.flatT[off:off + W.numel()].view(W.shape[1], W.shape[0])
 
 
-def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None):
+def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None, mask=None):
     """dx[M,K] = dy[M,N] @ W[N,K]  (W row-major, reduction over N).  Reads the W^T image when one
     is registered (TransposedWeights), else W itself through transposed fragment reads.
-    drop=(seed, offset): the forward dropout mask of the [M, K] output (EPI_GELU_DROP_BWD)."""
+    drop=(seed, offset): the forward dropout mask of the [M, K] output (EPI_GELU_DROP_BWD).
+    mask: EPI_RELU_DROP_BWD reads the forward's 1-bit activity mask instead of aux."""
     M, N = dy.shape
     K = W.shape[1]
     if out is None:
@@ -309,11 +330,11 @@ def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=Fa
     if WT is not None:
         gemm(dy, WT, out, M, K, N, a_kc=True, b_kc=True, lda=dy.stride(0), ldb=WT.stride(0),
              ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p,
-             seed=seed, offset=off, ld_rng=K)
+             seed=seed, offset=off, ld_rng=K, mask=mask)
         return out
     gemm(dy, W, out, M, K, N, a_kc=True, b_kc=False, lda=dy.stride(0), ldb=W.stride(0),
          ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p,
-         seed=seed, offset=off, ld_rng=K)
+         seed=seed, offset=off, ld_rng=K, mask=mask)
     return out
 
 

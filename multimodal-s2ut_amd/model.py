@@ -34,6 +34,11 @@ from .kernels import F16, round_up
 # encoder backward: enqueue each dgrad (main stream, critical path) before the weight gradient
 # (side stream) that reads the same dy; MMS2UT_DGRAD_FIRST=0 restores wgrad-first (A/B)
 DGRAD_FIRST = os.environ.get("MMS2UT_DGRAD_FIRST", "1") != "0"
+# MMS2UT_RELU_MASK=1: the fc1 forward also writes a 1-bit activity mask of its ReLU+dropout output
+# (K.relu_mask_alloc) and the fc2 dgrad epilogue reads it instead of the fp16 activation (1/16 of
+# those bytes, bit-identical output).  Measured 0.6 % slower per step than reading the activation
+# (18.67 vs 18.56 ms, two interleaved pairs, profiles/round2_v3_relu_mask_ab.txt), so opt-in.
+RELU_MASK = os.environ.get("MMS2UT_RELU_MASK", "0") == "1"
 
 
 def default_cfg(**over):
@@ -707,8 +712,10 @@ class MMS2UTModel:
         c["h2"] = h2
         pact = self._p("activation_dropout")
         c["drop_act"] = self._drop(pact, R * cfg["encoder_ffn_embed_dim"])
+        F_ = cfg["encoder_ffn_embed_dim"]
+        c["f1m"] = K.relu_mask_alloc(R, F_, h2.device) if RELU_MASK and F_ % 8 == 0 else None
         f1 = K.linear(h2, self.P(p + ".fc1.weight"), self.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP,
-                      p=pact, drop=c["drop_act"])
+                      p=pact, drop=c["drop_act"], mask=c["f1m"])
         c["f1"] = f1
         c["drop2"] = self._drop(pd, R * d)
         x3 = K.linear(f1, self.P(p + ".fc2.weight"), self.P(p + ".fc2.bias"), epi=K.EPI_DROP_RESID,
@@ -734,7 +741,8 @@ class MMS2UTModel:
         # that reads the same dy, so its blocks are dispatched first
         if not DGRAD_FIRST:
             K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"), db=self.G(p + ".fc2.bias"))
-        df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
+        df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD,
+                             aux=c["f1"] if c.get("f1m") is None else None, mask=c.get("f1m"), p=pact)
         if DGRAD_FIRST:
             K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"), db=self.G(p + ".fc2.bias"))
         else:
@@ -1150,8 +1158,9 @@ class MMS2UTModel:
         h3, c["m3"], c["r3"] = K.layernorm(x3, self.P(p + ".final_layer_norm.weight"), self.P(p + ".final_layer_norm.bias"))
         c["h3"] = h3
         c["drop_act"] = self._drop(pact, R * spec.F)
+        c["f1m"] = K.relu_mask_alloc(R, spec.F, h3.device) if RELU_MASK and spec.F % 8 == 0 else None
         f1 = K.linear(h3, self.P(p + ".fc1.weight"), self.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP, p=pact,
-                      drop=c["drop_act"])
+                      drop=c["drop_act"], mask=c["f1m"])
         c["f1"] = f1
         c["drop3"] = self._drop(pd, R * d)
         x4 = K.linear(f1, self.P(p + ".fc2.weight"), self.P(p + ".fc2.bias"), epi=K.EPI_DROP_RESID, aux=x3,
@@ -1172,7 +1181,8 @@ class MMS2UTModel:
             dy3 = K.dropout(dx4, pd, c["drop3"], out=torch.empty_like(dx4)) if pd > 0 else dx4
         K.linear_wgrad(dy3, c["f1"], self.G(p + ".fc2.weight"),
                        db=self.G(p + ".fc2.bias"))
-        df1 = K.linear_dgrad(dy3, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
+        df1 = K.linear_dgrad(dy3, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD,
+                             aux=c["f1"] if c.get("f1m") is None else None, mask=c.get("f1m"), p=pact)
         K.linear_wgrad(df1, c["h3"], self.G(p + ".fc1.weight"),
                        db=self.G(p + ".fc1.bias"))
         dh3 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))

@@ -123,3 +123,26 @@ def test_tail_split_matches_single_launch(M, N, K):
         assert torch.equal(outs[1][:M1], outs[0][:M1]), name        # the head is the same launch
         if name == "relu_drop_open":
             assert torch.equal(outs[1] == 0, outs[0] == 0)
+
+
+@pytest.mark.parametrize("M", [4096, 470, 1003])
+def test_relu_mask_roundtrip(M):
+    """fc1 forward writes the 1-bit ReLU+dropout activity mask (bit n%8 of byte n/8 = out > 0) and
+    the fc2 dgrad epilogue reading it is bit-identical to reading the fp16 activation — on the
+    LDS-staged fast path, the short-M split-K fixup path and an odd M."""
+    K = pkg().kernels
+    torch.manual_seed(0)
+    F, d = 3072, 768
+    x = torch.randn(M, d, device="cuda").half()
+    W1 = (0.05 * torch.randn(F, d, device="cuda")).half()
+    b1 = torch.randn(F, device="cuda").half()
+    mask = K.relu_mask_alloc(M, F, "cuda").fill_(0xAA)
+    f1 = K.linear(x, W1, b1, epi=K.EPI_RELU_DROP, p=0.1, drop=(11, 4096), mask=mask)
+    assert torch.equal(K.relu_mask_unpack(mask, M, F), f1 > 0)
+    f1b = K.linear(x, W1, b1, epi=K.EPI_RELU_DROP, p=0.1, drop=(11, 4096))
+    assert torch.equal(f1, f1b)          # writing the mask does not change the activation
+    dy = torch.randn(M, d, device="cuda").half()
+    W2 = (0.05 * torch.randn(d, F, device="cuda")).half()
+    ref = K.linear_dgrad(dy, W2, epi=K.EPI_RELU_DROP_BWD, aux=f1, p=0.1)
+    got = K.linear_dgrad(dy, W2, epi=K.EPI_RELU_DROP_BWD, mask=mask, p=0.1)
+    assert torch.equal(ref, got)
