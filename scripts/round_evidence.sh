@@ -13,4 +13,5 @@ step bench 240 python bench.py
 B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-gemm-timing"
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $B
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $B
+step dp2 300 scripts/_dp2_rehearsal.sh
 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
