@@ -147,7 +147,9 @@ def test_layernorm_padded_dropout(K, extra):
 def test_layernorm_fwd_bwd(K, ln16, monkeypatch):
     """ln16=1: D % 256 == 0 takes the 16-B half-wave-per-row backward; 0 forces the 8-B one."""
     monkeypatch.setenv("MMS2UT_LN16", ln16)
-    for R, D in ((1000, 768), (37, 256), (5, 96), (3, 1024)):
+    # 46160 rows (the image LayerNorm of a 80-utterance ViT batch): each 16-B-path block folds
+    # several 8-row groups into one dgamma / dbeta partial row (ops.hip ln16_iters)
+    for R, D in ((1000, 768), (37, 256), (5, 96), (3, 1024), (46160, 768)):
         x = (3 * torch.randn(R, D, device="cuda") + 1).half()
         g = (1 + 0.1 * torch.randn(D, device="cuda")).half()
         b = (0.1 * torch.randn(D, device="cuda")).half()
@@ -172,7 +174,10 @@ def test_layernorm_fwd_bwd(K, ln16, monkeypatch):
         assert torch.equal(dx2, dx)
         ref = torch.where(keep, dx.float() / 0.9, torch.zeros_like(dx.float()))
         assert (dxd.float() - ref).abs().max().item() <= 2e-3 * ref.abs().max().item() + 1e-3
-        assert torch.equal(dxd == 0, ~keep | (dx == 0))
+        # zero exactly where dropped or dx == 0 — up to elements at the fp16 underflow edge, where the
+        # fp32 value behind dx rounds to 0 but its /(1-p) copy does not (or vice versa)
+        mism = (dxd == 0) != (~keep | (dx == 0))
+        assert (dx.float().abs()[mism] < 1e-6).all() and (dxd.float().abs()[mism] < 1e-6).all()
         # parameter-grad-only mode (image LN: no dx)
         dgb2 = torch.empty_like(dgb)
         assert K.layernorm_bwd(dy, x, g, mean, rstd, dgb2, want_dx=False) is None
