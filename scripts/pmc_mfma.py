@@ -1,6 +1,9 @@
 """MFMA utilisation of the training step's kernels from one rocprofv3 PMC pass over bench.py
 (counters SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE, SQ_BUSY_CYCLES — one pass, within the SQ /
-GRBM slot limits of MI355X_MICROARCH.md).  One full training step (fbank launch to fbank launch).
+GRBM slot limits of MI355X_MICROARCH.md).  Windows are fbank launch to fbank launch (one training
+step each); bench.py cycles through its resident batches (a K=3 window holds 3 batches, one of
+them the dataset's short tail batch), so the figures aggregate the last complete cycle of
+--cycle windows (default 3), and each window is reported on its own.
 
   MFMA utilisation of a kernel = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs × 256 CUs × 4 SIMDs)
 
@@ -27,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("pmc")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--cycle", type=int, default=3)
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.pmc + "/run_counter_collection.csv")))
     per = defaultdict(dict)
@@ -37,7 +41,20 @@ def main():
         names[d] = r["Kernel_Name"]
     order = sorted(per)
     starts = [d for d in order if "fbank_kernel" in names[d]]
-    step = [d for d in order if starts[-2] <= d < starts[-1]]
+    lo, hi = starts[-1 - a.cycle], starts[-1]
+    step = [d for d in order if lo <= d < hi]
+    windows = []
+    for w0, w1 in zip(starts[-1 - a.cycle:-1], starts[-a.cycle:]):
+        ds = [d for d in order if w0 <= d < w1]
+        b = sum(per[d].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for d in ds)
+        g = sum(per[d].get("GRBM_GUI_ACTIVE", 0.0) / 8 * 256 * 4 for d in ds)
+        gd = [d for d in ds if short(names[d]).startswith("gemm")]
+        gb = sum(per[d].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for d in gd)
+        gg = sum(per[d].get("GRBM_GUI_ACTIVE", 0.0) / 8 * 256 * 4 for d in gd)
+        windows.append({"dispatches": len(ds), "mfma_util": b / max(g, 1.0), "gemm_mfma_util": gb / max(gg, 1.0),
+                        "mfma_busy": b})
+        print(f"window {w0}: {len(ds)} dispatches, MFMA util {b / max(g, 1.0) * 100:.1f} % "
+              f"(GEMMs {gb / max(gg, 1.0) * 100:.1f} %)")
     agg = defaultdict(lambda: [0, 0.0, 0.0])
     tot = [0.0, 0.0]
     for d in step:
@@ -50,9 +67,10 @@ def main():
         tot[0] += busy
         tot[1] += gui / 8 * 256 * 4
     out = {"source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES of "
-                     "`python bench.py --steps 3 --warmup 1 --no-gemm-timing`; one training step",
+                     "`python bench.py --steps 3 --warmup 1 --no-gemm-timing`; the last cycle of "
+                     f"{a.cycle} training steps (bench's resident batches)",
            "formula": "MFMA_BUSY / (GRBM_GUI_ACTIVE/8 * 256 CU * 4 SIMD)",
-           "step_mfma_util": tot[0] / max(tot[1], 1.0), "per_kernel": {}}
+           "step_mfma_util": tot[0] / max(tot[1], 1.0), "windows": windows, "per_kernel": {}}
     gemm = [0.0, 0.0]
     for k, (n, b, g) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
         out["per_kernel"][k] = {"launches": n, "mfma_util": b / max(g, 1.0), "simd_cycles": g}
