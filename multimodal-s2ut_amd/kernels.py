@@ -3,6 +3,7 @@
 Every function enqueues HIP kernels on PyTorch's current stream through libmms2ut_hip.so.
 Tensors are fp16 (``torch.float16``) unless stated; shapes are checked before the call.
 """
+import ctypes
 import math
 import os
 
@@ -64,43 +65,38 @@ def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv
          sA=(0, 0), sB=(0, 0), sC=(0, 0), epi=EPI_F16, alpha=1.0, bias=None, aux=None, ldaux=0,
          sX=(0, 0), out2=None, ldo2=0, p=0.0, seed=0, offset=0, ld_rng=0, splitk=1, sCsplit=0,
          rowsum=None, ld_rowsum=0, red_out=None, red_bias=None, red_cnt=None, mask=None):
-    a = GemmArgs()
-    a.A, a.B, a.C = A.data_ptr(), B.data_ptr(), C.data_ptr()
-    a.M, a.N, a.K = int(M), int(N), int(K)
-    a.a_kcontig, a.b_kcontig = int(a_kc), int(b_kc)
-    a.lda, a.ldb, a.ldc = int(lda), int(ldb), int(ldc)
-    a.batch, a.bdiv = int(batch), int(bdiv)
-    a.sA1, a.sA2 = sA
-    a.sB1, a.sB2 = sB
-    a.sC1, a.sC2 = sC
-    a.splitk, a.sCsplit = int(splitk), int(sCsplit)
-    a.epi, a.alpha = int(epi), float(alpha)
-    a.bias = _p(bias)
-    a.aux = _p(aux)
-    a.ldaux = int(ldaux)
-    a.sX1, a.sX2 = sX
-    a.out2, a.ldo2 = _p(out2), int(ldo2)
-    a.dropout_p, a.seed, a.offset, a.ld_rng = float(p), int(seed), int(offset), int(ld_rng)
-    a.rowsum, a.ld_rowsum = _p(rowsum), int(ld_rowsum)
-    if red_cnt is not None:
-        a.red_out, a.ld_red_out = red_out.data_ptr(), int(red_out.stride(0))
-        a.red_bias, a.red_cnt = _p(red_bias), red_cnt.data_ptr()
-    if mask is not None:   # 1-bit ReLU/dropout activity mask (relu_mask_alloc), written or read
-        assert mask.dtype == torch.uint8 and mask.shape[0] >= (M + 63) // 64 * 64 and mask.stride(1) == 1
-        a.mask, a.ld_mask = mask.data_ptr(), int(mask.stride(0))
-    ws = None
+    """One mms2ut_gemm_f16 launch.  The argument block is packed in one struct call (_lib.GEMM_ARGS,
+    the C layout of mms2ut_gemm_args): this runs a few hundred times per training step."""
+    ws_p = ws_n = 0
+    tail = 0
     if splitk == 1 and epi != EPI_F32 and batch == 1 and rowsum is None and _SPLITK_FIX:
         s = _fixup_splits(M, N, K)
         if s > 1:
             ws = _workspace("splitk_fix", s * M * N, C.device)
-            a.splitk, a.splitk_ws, a.splitk_ws_floats = s, ws.data_ptr(), ws.numel()
+            splitk, ws_p, ws_n = s, ws.data_ptr(), ws.numel()
         elif _TAIL_SPLIT:
-            M1 = _tail_split_rows(M, N, K)
-            if M1:
-                return _gemm_tail_split(a, M1, C.device)
-    call("mms2ut_gemm_f16", a, _s())
+            tail = _tail_split_rows(M, N, K)
+    red_p = ld_red = red_b = red_c = 0
+    if red_cnt is not None:
+        red_p, ld_red = red_out.data_ptr(), red_out.stride(0)
+        red_b, red_c = (0 if red_bias is None else red_bias.data_ptr()), red_cnt.data_ptr()
+    mask_p = ld_mask = 0
+    if mask is not None:   # 1-bit ReLU/dropout activity mask (relu_mask_alloc), written or read
+        assert mask.dtype == torch.uint8 and mask.shape[0] >= (M + 63) // 64 * 64 and mask.stride(1) == 1
+        mask_p, ld_mask = mask.data_ptr(), mask.stride(0)
+    buf = _GEMM_PACK(
+        A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, a_kc, b_kc, lda, ldb, ldc, batch, bdiv,
+        sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], splitk, sCsplit, epi, alpha,
+        0 if bias is None else bias.data_ptr(), 0 if aux is None else aux.data_ptr(), ldaux, sX[0], sX[1],
+        0 if out2 is None else out2.data_ptr(), ldo2, p, seed, offset, ld_rng,
+        0 if rowsum is None else rowsum.data_ptr(), ld_rowsum, ws_p, ws_n, red_p, ld_red, red_b, red_c,
+        mask_p, ld_mask)
+    if tail:
+        return _gemm_tail_split(GemmArgs.from_buffer_copy(buf), tail, C.device)
+    call("mms2ut_gemm_f16", buf, _s())
 
 
+_GEMM_PACK = _lib.GEMM_ARGS.pack
 _SPLITK_FIX = os.environ.get("MMS2UT_SPLITK_FIX", "1") != "0"
 # Tail split (below) measured slower in the training step (19.03 vs 18.46 ms over three interleaved
 # pairs) although faster in isolation: opt-in, MMS2UT_GEMM_TAILSPLIT=1.
@@ -133,7 +129,7 @@ def _gemm_tail_split(a, M1, device):
     M = a.M
     t = GemmArgs.from_buffer_copy(a)
     a.M = M1
-    call("mms2ut_gemm_f16", a, _s())
+    call("mms2ut_gemm_f16", ctypes.byref(a), _s())
     M2 = M - M1
     t.M = M2
     t.A = a.A + 2 * M1 * (a.lda if a.a_kcontig else 1)
@@ -146,7 +142,7 @@ def _gemm_tail_split(a, M1, device):
     s = max(2, _fixup_splits(M2, a.N, a.K))
     ws = _workspace("splitk_fix", s * M2 * a.N, device)
     t.splitk, t.splitk_ws, t.splitk_ws_floats = s, ws.data_ptr(), ws.numel()
-    call("mms2ut_gemm_f16", t, _s())
+    call("mms2ut_gemm_f16", ctypes.byref(t), _s())
 
 
 def _fixup_splits(M, N, K):
@@ -635,19 +631,11 @@ FLASH_HD = (64, 96, 128)
 
 def _attn_args(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len, causal, p, drop, lse,
                sq=0, sk=0, sv=0, so=0):
-    from ._lib import AttnArgs
-    a = AttnArgs()
-    a.q, a.k, a.v, a.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
-    a.ldq, a.ldk, a.ldv, a.ldo = int(ldq), int(ldk), int(ldv), int(ldo)
-    a.sqb, a.skb, a.svb, a.sob = int(sq), int(sk), int(sv), int(so)
-    a.B, a.H, a.Tq, a.Tk, a.hd = int(B), int(H), int(Tq), int(Tk), int(hd)
-    a.key_len = _p(key_len)
-    a.causal = int(causal)
-    a.scale = float(scale)
+    """mms2ut_attn_args packed in one struct call (_lib.ATTN_ARGS, fields in AttnArgs order)."""
     seed, off = drop if p > 0 else (0, 0)
-    a.p, a.seed, a.offset = float(p), int(seed), int(off)
-    a.lse = lse.data_ptr()
-    return a
+    return _lib.ATTN_ARGS.pack(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), ldq, ldk, ldv, ldo,
+                               sq, sk, sv, so, B, H, Tq, Tk, hd, 0 if key_len is None else key_len.data_ptr(),
+                               int(causal), scale, p, seed, off, lse.data_ptr())
 
 
 def mha_fwd(q, k, v, o, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len=None, causal=False,

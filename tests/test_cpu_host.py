@@ -39,7 +39,20 @@ def test_library_error_path_without_gpu():
     a = mm._lib.GemmArgs()
     a.M, a.N, a.K, a.batch, a.lda, a.ldb = 4, 4, 4, 1, 3, 8
     with pytest.raises(mm._lib.HipError, match="multiples of 8"):
-        mm._lib.call("mms2ut_gemm_f16", a, None)
+        mm._lib.call("mms2ut_gemm_f16", ctypes.byref(a), None)
+    b = mm._lib.GEMM_ARGS.pack(*[getattr(a, f) or 0 for f, _ in a._fields_])
+    with pytest.raises(mm._lib.HipError, match="multiples of 8"):
+        mm._lib.call("mms2ut_gemm_f16", b, None)
+
+
+def test_gemm_args_pack_layout():
+    """_lib.GEMM_ARGS / ATTN_ARGS (the struct-packed argument blocks kernels.gemm / _attn_args pass)
+    have GemmArgs' / AttnArgs' layout: every field lands at its ctypes offset."""
+    mm = pkg()
+    for G, S in ((mm._lib.GemmArgs, mm._lib.GEMM_ARGS), (mm._lib.AttnArgs, mm._lib.ATTN_ARGS)):
+        vals = [(i + 1) * (3 if t is not ctypes.c_float else 0.5) for i, (_, t) in enumerate(G._fields_)]
+        g = G.from_buffer_copy(S.pack(*vals))
+        assert [getattr(g, f) for f, _ in G._fields_] == vals, G
 
 
 def test_param_layout_matches_reference_state_dict():
