@@ -313,6 +313,8 @@ def main():
                 step(i, draws=[dr])
         n_graphs = len(tr.graphs)
     base = args.warmup   # the timed batch sequence does not depend on how many settling steps ran
+    host_cpu = [0.0]   # CPU seconds of the issuing threads (main + autograd backward) in the last window
+
     def timed(profile):
         """K steps between barrier + synchronize on both sides -> (seconds, host issue seconds, GEMM stats).
         profile=True: the roofline pass — every GEMM kernel's workgroups store their start / end
@@ -341,10 +343,12 @@ def main():
             bprof = cProfile.Profile()
             runtime._BWD_PROFILE = bprof
             prof.enable()
+        c0, b0 = time.thread_time(), runtime.BWD_CPU_S[0]
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(base + i, eager=profile)
         t_issue = time.perf_counter()  # host finished enqueueing (host-bound if ~ t1)
+        host_cpu[0] = time.thread_time() - c0 + runtime.BWD_CPU_S[0] - b0
         if prof is not None:
             import pstats
             prof.disable()
@@ -373,6 +377,7 @@ def main():
     # the throughput region runs uninstrumented; the same K steps are then re-run serially with the
     # library's in-kernel workgroup stamps for the roofline
     t_run, t_issue_run, _, _ = timed(False)
+    host_cpu_run = host_cpu[0]
     t_prof = None
     gemm_ms, n_launch, launched_flops, gemm_bytes = 0.0, 0, 0.0, 0.0
     classes, templates = {}, {}
@@ -466,6 +471,10 @@ def main():
                          "classes": class_lines,
                          "kernels": tmpl_lines,
                          "host_issue_ms_per_step": 1e3 * (t_issue - t0) / args.steps,
+                         # CPU time of the two issuing threads (main: forward, loss, optimizer;
+                         # autograd's: the hand-written backward) — the host's own cost per step,
+                         # without the waits on the runtime the wall-clock issue time includes
+                         "host_cpu_ms_per_step": 1e3 * host_cpu_run / args.steps,
                          "hip_graph": {"enabled": graph, "graphs": n_graphs},
                          "roofline_pass_ms_per_step": (1e3 * t_prof / args.steps) if t_prof else None,
                          "note": "achieved = SURVEY §8d algorithmic GEMM FLOPs (true lengths, 3x fwd, "

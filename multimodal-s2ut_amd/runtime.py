@@ -5,6 +5,7 @@ The autograd graph has exactly two nodes per step — the whole model and the lo
 model's backward is hand-written (model.py); PyTorch only carries the upstream loss-scale
 gradient between them.
 """
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -157,6 +158,7 @@ class _ModelFn(torch.autograd.Function):
         if dlogits is None:    # only the multitask losses were differentiated
             dlogits = torch.zeros(dctx["B"] * dctx["Tt"], dctx["Vp"], dtype=F16, device=enc.device)
         prof = _BWD_PROFILE
+        t_cpu = time.thread_time()
         if prof is not None:
             prof.enable()
         model.decoder_backward(dctx, dlogits.contiguous(), enc, denc, dinner=dinner)
@@ -166,12 +168,17 @@ class _ModelFn(torch.autograd.Function):
         K.side_join()  # weight gradients (side stream) complete before anyone reads them
         if prof is not None:
             prof.disable()
+        BWD_CPU_S[0] += time.thread_time() - t_cpu
         return None, None, None
 
 
 # host-side profile of the hand-written backward (it runs on the autograd engine's thread, which a
 # profiler enabled on the main thread does not see): bench.py sets a cProfile.Profile here
 _BWD_PROFILE = None
+# CPU time the backward's issuing thread spent (seconds, summed over calls): bench.py adds it to the
+# main thread's CPU time for the host cost per step, which — unlike the wall time to enqueue — does
+# not count the host's waits on the runtime
+BWD_CPU_S = [0.0]
 
 
 def model_outputs(model, batch):

@@ -12,6 +12,6 @@ import json, sys
 line = [l for l in open(sys.argv[2]) if l.startswith("{")][-1]
 d = json.loads(line)
 r = d["roofline"]
-print(f"[{sys.argv[1]:14s}] {d['ms_per_step']:7.2f} ms/step  {d['value']/1e6:6.3f} Mframes/s  gemm {r['gemm_ms_per_step']:6.2f} ms  ach {r['achieved']:6.1f} TF  issue {r['host_issue_ms_per_step']:5.2f} ms", flush=True)
+print(f"[{sys.argv[1]:14s}] {d['ms_per_step']:7.2f} ms/step  {d['value']/1e6:6.3f} Mframes/s  gemm {r['gemm_ms_per_step']:6.2f} ms  ach {r['achieved']:6.1f} TF  issue {r['host_issue_ms_per_step']:5.2f} ms  host cpu {r.get('host_cpu_ms_per_step', float('nan')):5.2f} ms", flush=True)
 PY
 done
