@@ -758,6 +758,51 @@ __global__ void im2col_kernel(const h16* __restrict__ x, h16* __restrict__ col, 
   }
 }
 
+// im2col with 8 consecutive columns of one row per thread (one 16-B store) and 32-bit index math
+// (the generic kernel's 64-bit div/mod per element dominated it): ldcol % 8 == 0, col 16-B aligned,
+// B*Tout*ldcol < 2^31.  The x gathers of a row's 8 columns hit at most 2 channel positions x k taps.
+__global__ void im2col8_kernel(const h16* __restrict__ x, h16* __restrict__ col, int rows, int Tin, int Tout,
+                               int C, int k, int stride, int pad, int ldcol) {
+  const int W = C * k, n8 = ldcol >> 3, total = rows * n8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int bt = i / n8, r8 = (i - bt * n8) << 3;
+    const int b = bt / Tout, t = bt - b * Tout;
+    const int t0 = t * stride - pad;
+    const h16* xb = x + (long)b * Tin * C;
+    int c = r8 / k, kk = r8 - c * k;
+    h16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int ti = t0 + kk;
+      v[e] = (r8 + e < W && ti >= 0 && ti < Tin) ? xb[ti * C + c] : (h16)0.f;
+      if (++kk == k) { kk = 0; ++c; }
+    }
+    *reinterpret_cast<h16x8*>(col + (long)bt * ldcol + r8) = v;
+  }
+}
+
+// col2im with 4 consecutive channels per thread (one 8-B store), 32-bit index math: C % 4 == 0,
+// B*Tin*C < 2^31.  Same summation order as col2im_kernel (taps kk ascending, fp32).
+__global__ void col2im4_kernel(const h16* __restrict__ dcol, h16* __restrict__ dx, int rows_in, int Tin,
+                               int Tout, int C, int k, int stride, int pad) {
+  const int C4 = C >> 2, total = rows_in * C4, W = C * k;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int bt = i / C4, c = (i - bt * C4) << 2;
+    const int b = bt / Tin, ti = bt - b * Tin;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < k; ++kk) {
+      const int num = ti + pad - kk;
+      if (num < 0 || num % stride) continue;
+      const int t = num / stride;
+      if (t >= Tout) continue;
+      const h16* src = dcol + (long)(b * Tout + t) * W + c * k + kk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[e] += (float)src[e * k];
+    }
+    *reinterpret_cast<h16x4*>(dx + (long)bt * C + c) = h16x4{(h16)s[0], (h16)s[1], (h16)s[2], (h16)s[3]};
+  }
+}
+
 __global__ void col2im_kernel(const h16* __restrict__ dcol, h16* __restrict__ dx, int B, int Tin,
                               int Tout, int C, int k, int stride, int pad) {
   const long n = (long)B * Tin * C;
@@ -1134,6 +1179,11 @@ extern "C" int mms2ut_im2col_ld(const h16* x, h16* col, int B, int Tin, int Tout
   MMS_REQUIRE(ldcol >= C * k, "im2col: ldcol < C*k");
   const long n = (long)B * Tout * ldcol;
   if (n == 0) return 0;
+  if (ldcol % 8 == 0 && ((uintptr_t)col & 15) == 0 && n < (1L << 31)) {
+    hipLaunchKernelGGL(im2col8_kernel, dim3(grid_for(n / 8, 256)), dim3(256), 0, s, x, col, B * Tout, Tin, Tout,
+                       C, k, stride, pad, ldcol);
+    return mms::check_launch("im2col");
+  }
   hipLaunchKernelGGL(im2col_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, col, B, Tin, Tout, C, k,
                      stride, pad, ldcol);
   return mms::check_launch("im2col");
@@ -1148,6 +1198,11 @@ extern "C" int mms2ut_col2im(const h16* dcol, h16* dx, int B, int Tin, int Tout,
                              int pad, hipStream_t s) {
   const long n = (long)B * Tin * C;
   if (n == 0) return 0;
+  if (C % 4 == 0 && ((uintptr_t)dx & 7) == 0 && n < (1L << 31) && (long)B * Tout * C * k < (1L << 31)) {
+    hipLaunchKernelGGL(col2im4_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, s, dcol, dx, B * Tin, Tin, Tout,
+                       C, k, stride, pad);
+    return mms::check_launch("col2im");
+  }
   hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, dcol, dx, B, Tin, Tout, C, k,
                      stride, pad);
   return mms::check_launch("col2im");

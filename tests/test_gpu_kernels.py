@@ -355,6 +355,28 @@ def test_ls_xent(K):
     assert torch.equal(dz[:, V:], torch.zeros_like(dz[:, V:]))  # pad columns zeroed
 
 
+@pytest.mark.parametrize("B,Tin,C,k,ldcol", [(3, 41, 80, 5, 448), (2, 37, 512, 5, None), (2, 23, 6, 5, None),
+                                             (4, 250, 80, 5, 400)])
+def test_im2col_col2im_exact(K, B, Tin, C, k, ldcol):
+    """im2col is a pure gather: bit-exact against torch unfold (zero pad columns past C*k); col2im
+    sums <= ceil(k/stride) taps in fp32: against the fp32 fold, one fp16 rounding apart.  Covers the
+    vectorised kernels (ldcol % 8 == 0, C % 4 == 0) and the generic ones (C = 6, ldcol = 30)."""
+    Tout = (Tin - 1) // 2 + 1
+    x = torch.randn(B * Tin, C, device="cuda").half()
+    col = K.im2col(x, B, Tin, Tout, C, k, ldcol=ldcol)
+    ref = torch.nn.functional.unfold(x.view(B, Tin, C).transpose(1, 2).unsqueeze(-1).float(), (k, 1),
+                                     padding=(2, 0), stride=(2, 1)).transpose(1, 2).reshape(B * Tout, C * k)
+    W = C * k
+    assert torch.equal(col[:, :W].float(), ref)
+    if col.shape[1] > W:
+        assert torch.equal(col[:, W:], torch.zeros_like(col[:, W:]))
+    dcol = torch.randn(B * Tout, W, device="cuda").half()
+    dx = K.col2im(dcol, B, Tin, Tout, C, k)
+    fold = torch.nn.functional.fold(dcol.float().view(B, Tout, W).transpose(1, 2), (Tin, 1), (k, 1),
+                                    padding=(2, 0), stride=(2, 1)).view(B, C, Tin).transpose(1, 2).reshape(B * Tin, C)
+    assert torch.equal(dx, fold.half())
+
+
 def test_glu_im2col_col2im(K):
     B, Tin, C, k = 2, 23, 16, 5
     Tout = (Tin - 1) // 2 + 1
