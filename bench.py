@@ -238,6 +238,38 @@ def decode_main(args):
         "cpu_baseline": cpu}), flush=True)
 
 
+def launch_ranks(args):
+    """``--gpus N`` without a torch.distributed launcher around us: start ``torch.distributed.run
+    --nproc-per-node N`` over this same script as a CHILD process (this process has not touched the
+    GPU: nothing above this point initialises HIP) and exit with its return code; rank 0's JSON line
+    reaches stdout through the inherited file descriptors.  Under a launcher (WORLD_SIZE set), the
+    launcher's world size must equal --gpus: a mismatch fails loudly instead of timing a different
+    node size than the one asked for.  Returns only when this process is itself a rank."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    backend = os.environ.get("MMS2UT_DIST_BACKEND", "")
+    ndev = torch.cuda.device_count()       # does not initialise the GPU on this image
+    if backend != "gloo" and ndev < args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but {ndev} visible GPUs (RCCL needs one GPU per rank; "
+                         f"MMS2UT_DIST_BACKEND=gloo rehearses N ranks on fewer devices)")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    rc = subprocess.call(cmd, env=env)
+    sys.exit(rc)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,8 +295,11 @@ def main():
     args = ap.parse_args()
     if args.decode:
         return decode_main(args)
+    launch_ranks(args)
 
     rank, world, local = parallel.init_from_env()
+    if world > 1:
+        world = dist.get_world_size()          # n_gpus as the process group sees it
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     detr = args.image_feats == "detr"
@@ -424,6 +459,15 @@ def main():
         frames_all, flops_all, gemm_all, nl_all = float(frames), float(alg_flops), gemm_ms, float(n_launch)
         total_flops_all = float(total_flops)
     ost = dict(tr.opt.stats(), untimed_scale_settling_steps=settle)
+    # fp32 master checksum after every step above: equal on all ranks (DP keeps replicas identical)
+    # and, for a fixed step sequence, independent of --bucket-mb (scripts/_dp2_rehearsal.sh)
+    tr.sync()
+    ck = torch.tensor([float(tr.opt.master.double().sum())], dtype=torch.float64, device=device)
+    ost["master_checksum"] = float(ck)
+    if world > 1:
+        cks = [torch.zeros_like(ck) for _ in range(world)]
+        dist.all_gather(cks, ck)
+        ost["ranks_identical"] = all(float(c) == float(ck) for c in cks)
     traffic, traffic_src = gemm_pmc_traffic()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -84,6 +84,33 @@ class SpecAugment:
         return out
 
 
+_FRONTENDS = {}
+
+
+def wave_net_input_src(ni, device):
+    """fp16 [B, Tmax, 80] src_tokens for a sample whose net_input carries waveforms instead of
+    features (the fairseq-train drop-in's collater, fairseq_adapter.py): ``src_waves`` int32 [N]
+    = the fp32 samples' bit patterns (so fairseq's apply_half leaves them alone), ``src_wave_offsets``
+    int64 [B + 1], ``src_cmvn`` bool, optional ``src_specaugment`` {masks int32 [B, 2(nf + nt)],
+    n_freq, n_time, mask_value} drawn by the collater (CPU worker, as the reference's transform)."""
+    dev = torch.device(device)
+    cmvn = bool(ni.get("src_cmvn", True))
+    fe = _FRONTENDS.get((dev, cmvn))
+    if fe is None:
+        fe = _FRONTENDS[(dev, cmvn)] = FbankFrontend(dev, cmvn=cmvn)
+    w = ni["src_waves"]
+    if w.dtype != torch.int32:
+        raise TypeError(f"src_waves: int32 bit patterns of fp32 samples expected, got {w.dtype}")
+    wb = fe.from_device(w.to(dev).view(torch.float32), ni["src_wave_offsets"])
+    feats = K.fbank(wb["wave"], wb["wave_off"], wb["frame_off"], wb["total"], fe.banks, fe.mel_range, fe.num_bins)
+    out = K.cmvn_collate(feats, wb["frame_off"], wb["B"], wb["Tmax"], fe.num_bins, cmvn)
+    sa = ni.get("src_specaugment")
+    if sa is not None and sa["n_freq"] + sa["n_time"] > 0:
+        K.specaugment(out, wb["frame_off"], sa["masks"].to(dev, torch.int32).contiguous(), int(sa["n_freq"]),
+                      int(sa["n_time"]), sa.get("mask_value"))
+    return out
+
+
 class FbankFrontend:
     def __init__(self, device="cuda", num_bins=80, cmvn=True, specaugment=None):
         self.device = torch.device(device)
@@ -133,6 +160,18 @@ class FbankFrontend:
             masks = torch.from_numpy(m).pin_memory().to(self.device, non_blocking=True)
             K.specaugment(out, wb["frame_off"], masks, sa.fn, sa.tn, sa.mask_value)
         return out
+
+    def from_device(self, waves, wave_off):
+        """A wave batch from samples already in HBM: ``waves`` fp32 [N] (utterances back to back, in
+        the collater's frame-descending order), ``wave_off`` int64 [B + 1] sample offsets."""
+        off = wave_off.cpu().numpy().astype(np.int64)
+        fr = np.array([n_frames(int(n)) for n in np.diff(off)], dtype=np.int64)
+        if len(fr) == 0 or np.any(fr <= 0) or np.any(np.diff(fr) > 0):
+            raise ValueError(f"wave batch: frames {fr.tolist()} (need >= 1 frame each, descending order)")
+        frame_off = np.concatenate([[0], np.cumsum(fr)]).astype(np.int32)
+        return {"wave": waves.contiguous(), "wave_off": wave_off.to(self.device, torch.int64).contiguous(),
+                "frame_off": torch.from_numpy(frame_off).to(self.device), "n_frames": torch.from_numpy(fr),
+                "total": int(fr.sum()), "Tmax": int(fr.max()), "B": len(fr), "order": list(range(len(fr)))}
 
     def features_f32(self, wb):
         """Raw log-mel features [total_frames, nbins] fp32 (no CMVN) — for parity tests."""

@@ -235,7 +235,10 @@ class MultiModalSpeechToSpeechTask:
             self.datasets = {}
         self.datasets[split] = M.MultiModalS2SManifest(
             a.data, split, M.UnitDictionary.for_codes(self.vocab_size - 4), data_cfg=data_cfg,
-            image_feat_path=feat, is_train=split.startswith("train"))
+            image_feat_path=feat, is_train=split.startswith("train"),
+            max_source_positions=getattr(a, "max_source_positions", None) or 6000,
+            max_target_positions=getattr(a, "max_target_positions", None) or 1024,
+            multitask=self.multitask_tasks or None)
         return self.datasets[split]
 
     def build_generator(self, models, args, **kw):
@@ -445,8 +448,10 @@ class MM_S2UTTransformerModel:
         return self.cfg["max_target_positions"]
 
     def _batch(self, src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target=None,
-               multitask=None):
-        sample = {"net_input": {"src_tokens": src_tokens, "src_lengths": src_lengths,
+               multitask=None, extra_input=None):
+        """extra_input: further net_input keys (the waveform front-end fields, frontend.wave_net_input_src)."""
+        ni = {k: v for k, v in (extra_input or {}).items() if k.startswith("src_")}
+        sample = {"net_input": {**ni, "src_tokens": src_tokens, "src_lengths": src_lengths,
                                 "prev_output_tokens": prev_output_tokens, "imgs_list": list(imgs_list or []),
                                 "img_masks_list": list(img_masks_list or [])},
                   "target": target if target is not None else prev_output_tokens,
@@ -491,7 +496,7 @@ class MM_S2UTTransformerModel:
         if tgt_speaker is not None:
             raise NotImplementedError("target speaker embeddings (spk_emb_proj) are out of scope")
         batch = self._batch(src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list, target,
-                            multitask)
+                            multitask, extra_input=kwargs)
         stash = {}
         if return_all_hiddens:
             self.net.encoder_hook = stash.__setitem__

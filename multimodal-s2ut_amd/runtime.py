@@ -50,6 +50,9 @@ def prepare_batch(sample, cfg, device="cuda", src_override=None):
     ni = sample["net_input"]
     lens = ni["src_lengths"].cpu().numpy()
     nl = len(cfg["conv_kernel_sizes"])
+    if src_override is None and ni.get("src_tokens") is None and ni.get("src_waves") is not None:
+        from .frontend import wave_net_input_src      # waveforms in the sample: GPU fbank front end
+        src_override = wave_net_input_src(ni, dev)
     if src_override is not None:
         src = src_override
     else:
@@ -123,12 +126,25 @@ def decoder_batch(prev_output_tokens, cfg):
     return DecoderBatch(prev=prev_output_tokens.contiguous(), tgt_mask=tm, tgt_len32=tl)
 
 
+def _add_state_grads(out, grads):
+    """Merge {index: gradient} from the model's exposed hidden-state outputs into ``out``."""
+    for j, g in grads.items():
+        g = g.to(F16).contiguous()
+        out[j] = g if j not in out else K.add_f16(out[j], g)
+    return out
+
+
 class _ModelFn(torch.autograd.Function):
-    """Outputs (padded logits, weighted multitask loss fp32 [1]); the backward is hand-written:
-    multitask heads on decoder states -> unit decoder -> heads on encoder states -> encoder."""
+    """Outputs (padded logits, weighted multitask loss fp32 [1]) and, with ``states=True``, the
+    hidden states fairseq's ``return_all_hiddens`` exposes as further outputs: the L_e encoder layer
+    outputs ([B*Te, d] batch-major; fairseq ``encoder_states``), then the L_d + 1 decoder
+    ``inner_states`` ([B*Tt, d]).  Gradients reaching those outputs (e.g. from multitask heads that
+    live outside the HIP model, fairseq_adapter.py) enter the hand-written backward where the state
+    is produced.  The backward is hand-written: multitask heads on decoder states -> unit decoder ->
+    heads on encoder states -> encoder."""
 
     @staticmethod
-    def forward(fctx, anchor, model, batch):
+    def forward(fctx, anchor, model, batch, states=False):
         from . import multitask as MT
         enc, len32, Te, ectx = model.encoder_forward(batch)
         if getattr(model, "encoder_hook", None) is not None:   # return_all_hiddens (plugins.py)
@@ -139,12 +155,20 @@ class _ModelFn(torch.autograd.Function):
         model.last_aux_losses = alog
         fctx.model = model
         fctx.saved = (ectx, dctx, enc, batch, actx, Te)
+        # an anchor other than the model's own leaf comes from fairseq_adapter's parameter bridge,
+        # whose backward (handing out the flat gradient per parameter) must be reached
+        fctx.bridged = anchor is not model.anchor
         if aux is None:
             aux = torch.zeros(1, dtype=torch.float32, device=logits.device)
-        return logits, aux.reshape(())
+        if not states:
+            return logits, aux.reshape(())
+        fctx.set_materialize_grads(False)
+        es, ins = model.encoder_states(ectx), model.inner_states(dctx)
+        fctx.n_enc = len(es)
+        return (logits, aux.reshape(()), *es, *ins)
 
     @staticmethod
-    def backward(fctx, dlogits, daux):
+    def backward(fctx, dlogits, daux, *dhidden):
         from . import multitask as MT
         model = fctx.model
         ectx, dctx, enc, batch, actx, Te = fctx.saved
@@ -154,22 +178,26 @@ class _ModelFn(torch.autograd.Function):
         use_aux = bool(actx) and daux is not None
         if use_aux:
             daux = daux.reshape(1).to(torch.float32).contiguous()
-        dinner = MT.aux_backward_decoder_heads(model, actx, daux) if use_aux else None
-        if dlogits is None:    # only the multitask losses were differentiated
+        dinner = MT.aux_backward_decoder_heads(model, actx, daux) if use_aux else {}
+        n_enc = getattr(fctx, "n_enc", 0)
+        _add_state_grads(dinner, {j: g for j, g in enumerate(dhidden[n_enc:]) if g is not None})
+        if dlogits is None:    # only the multitask losses / hidden states were differentiated
             dlogits = torch.zeros(dctx["B"] * dctx["Tt"], dctx["Vp"], dtype=F16, device=enc.device)
         prof = _BWD_PROFILE
         t_cpu = time.thread_time()
         if prof is not None:
             prof.enable()
-        model.decoder_backward(dctx, dlogits.contiguous(), enc, denc, dinner=dinner)
+        model.decoder_backward(dctx, dlogits.contiguous(), enc, denc, dinner=dinner or None)
         del dctx
-        dstates = MT.aux_backward_encoder_heads(model, actx, daux, batch.prev.shape[0], Te) if use_aux else None
-        model.encoder_backward(ectx, denc, dstates)
+        dstates = MT.aux_backward_encoder_heads(model, actx, daux, batch.prev.shape[0], Te) if use_aux else {}
+        _add_state_grads(dstates, {j: g for j, g in enumerate(dhidden[:n_enc]) if g is not None})
+        model.encoder_backward(ectx, denc, dstates or None)
         K.side_join()  # weight gradients (side stream) complete before anyone reads them
         if prof is not None:
             prof.disable()
         BWD_CPU_S[0] += time.thread_time() - t_cpu
-        return None, None, None
+        danchor = torch.zeros(1, dtype=torch.float32, device=enc.device) if fctx.bridged else None
+        return danchor, None, None, None
 
 
 # host-side profile of the hand-written backward (it runs on the autograd engine's thread, which a
@@ -181,10 +209,11 @@ _BWD_PROFILE = None
 BWD_CPU_S = [0.0]
 
 
-def model_outputs(model, batch):
+def model_outputs(model, batch, states=False):
     """(padded logits [B*Tt, round64(V)] fp16, weighted multitask loss fp32 0-dim) — both
-    autograd-connected through the hand-written backward."""
-    return _ModelFn.apply(model.anchor, model, batch)
+    autograd-connected through the hand-written backward.  states=True appends the encoder_states
+    and decoder inner_states outputs (see _ModelFn)."""
+    return _ModelFn.apply(model.anchor, model, batch, states)
 
 
 def model_logits(model, batch):

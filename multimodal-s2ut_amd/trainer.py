@@ -73,6 +73,7 @@ class Trainer:
         self.world = world_size
         self.acc = None   # fp32 gradient accumulator (update_freq > 1), allocated on first use
         self.log = torch.zeros(5, dtype=torch.float32, device=model.params.flat.device)
+        self.grad_tap = None   # optional callable(flat fp16 grad) run right before the optimizer (tests)
         # The step's critical path (forward, dgrad chain, optimizer) runs on a high-priority stream
         # so the hardware dispatcher prefers its workgroups over the weight-gradient side stream's
         # (lowest priority), which only fills the CUs the critical path leaves idle.
@@ -229,6 +230,10 @@ class Trainer:
         self.log[LOG_NSENT].fill_(float(sum(int(b.nsentences) for b in batches)))
         self.log[LOG_SS_OVER_WORLD].fill_(float(ntok) / self.world)
         all_reduce_scalars(self.log)
+        if self.grad_tap is not None:
+            # the final (reduced, accumulated) fp16 gradient, in stream order before the optimizer
+            # consumes and (deferred path) zeroes it
+            self.grad_tap(m.params.grad)
         # DDP-averaged gradients (sum / world): multiply factor world / (scale * sample_size)
         self.opt.step(self.log[LOG_SS_OVER_WORLD:LOG_SS_OVER_WORLD + 1], check=self.norm_check)
         return self.log

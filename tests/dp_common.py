@@ -6,7 +6,10 @@ def model_cfg(mm):
     return mm.default_cfg(**R.no_dropout(R.tiny_config(conv_channels=256)))
 
 
-SHAPES = (([120, 90], [30, 22]), ([100, 77, 60], [25, 20, 15]))
+# gradient bucket sizes of the DP test: many small buckets (overlap path) + SURVEY §8e's sweep
+BUCKETS_MB = (0.25, 8, 25, 64, 128)
+
+SHAPES =(([120, 90], [30, 22]), ([100, 77, 60], [25, 20, 15]))
 
 
 def samples(mm):

@@ -3,6 +3,7 @@ parameter layout/state-dict names, fbank oracle cross-check, optimizer restateme
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -233,3 +234,36 @@ def test_deal_batches_balanced_and_round_robin():
     order = np.random.RandomState(4).permutation(len(batches)).tolist()
     order = order[: len(order) // 2 * 2]
     assert D.deal_batches(costs, 2, seed=1, epoch=3, balanced=False) == [order[0::2], order[1::2]]
+
+
+def test_bench_gpus_flag_launches_ranks(monkeypatch):
+    """`bench.py --gpus N` starts N ranks itself (torch.distributed.run as a
+    child process) when no launcher is around it, and fails loudly when a launcher's WORLD_SIZE
+    disagrees with --gpus."""
+    import argparse
+    import subprocess
+    import bench
+    calls = []
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: calls.append((cmd, env)) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("MMS2UT_DIST_BACKEND", "gloo")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "4"])
+    with pytest.raises(SystemExit) as e:
+        bench.launch_ranks(argparse.Namespace(gpus=2))
+    assert e.value.code == 0 and len(calls) == 1
+    cmd, env = calls[0]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"] and "--nproc-per-node=2" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and env["MASTER_ADDR"] == "127.0.0.1"
+    assert cmd[-4:] == [bench.__file__.replace(".pyc", ".py"), "--gpus", "2", "--steps", "4"][-4:]
+    # one GPU: nothing to launch
+    assert bench.launch_ranks(argparse.Namespace(gpus=1)) is None
+    # under a launcher, the sizes must agree
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    with pytest.raises(SystemExit, match="WORLD_SIZE=4"):
+        bench.launch_ranks(argparse.Namespace(gpus=8))
+    assert bench.launch_ranks(argparse.Namespace(gpus=4)) is None
+    # RCCL needs a GPU per rank
+    monkeypatch.delenv("WORLD_SIZE")
+    monkeypatch.delenv("MMS2UT_DIST_BACKEND")
+    with pytest.raises(SystemExit, match="visible GPUs"):
+        bench.launch_ranks(argparse.Namespace(gpus=2))

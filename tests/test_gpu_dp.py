@@ -7,6 +7,9 @@ Trainer on its own batch.  Checks:
   * both ranks hold bit-identical gradients, parameters, fp32 masters and optimizer state after 3
     updates, and the cross-rank grad-norm check (fairseq Trainer._check_grad_norms) stays clean;
   * the DP run's parameters after 3 updates match the single-process --update-freq 2 run's.
+The children run the default configuration: deferred chunked Adam and the gradient zeroing on
+the side stream (the gradient is taken right before the optimizer, Trainer.grad_tap), once per
+bucket size in dp_common.BUCKETS_MB; every bucket size must give bit-identical results.
 Children are spawned (never exec'd over a GPU process) and bounded by a timeout."""
 import os
 import socket
@@ -18,7 +21,7 @@ import pytest
 import torch
 
 from conftest import ROOT, pkg
-from dp_common import batches, model_cfg
+from dp_common import BUCKETS_MB, batches, model_cfg
 
 pytestmark = pytest.mark.gpu
 
@@ -45,39 +48,39 @@ def dp_run(tmp_path_factory):
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), MMS2UT_DIST_BACKEND="gloo", MMS2UT_DEFER_ADAM="0")
+                   MASTER_PORT=str(port), MMS2UT_DIST_BACKEND="gloo")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dp_child.py"), str(out)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=240)
+            o, _ = p.communicate(timeout=420)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
             raise
         logs.append(o.decode(errors="replace")[-3000:])
     assert all(p.returncode == 0 for p in procs), logs
-    return [dict(np.load(out / f"rank{r}.npz")) for r in range(2)]
+    return {mb: [dict(np.load(out / f"rank{r}_b{mb:g}.npz")) for r in range(2)] for mb in BUCKETS_MB}
 
 
 @pytest.fixture(scope="module")
 def single_run():
     mm = pkg()
     cfg = model_cfg(mm)
-    os.environ["MMS2UT_DEFER_ADAM"] = "0"
-    try:
-        model = mm.MMS2UTModel(cfg, device="cuda").init_params(seed=5)
-        tr = mm.trainer.Trainer(model, lr=1e-3, world_size=1, init_scale=8.0, warmup_updates=0, update_freq=2)
-    finally:
-        os.environ.pop("MMS2UT_DEFER_ADAM")
+    model = mm.MMS2UTModel(cfg, device="cuda").init_params(seed=5)
+    tr = mm.trainer.Trainer(model, lr=1e-3, world_size=1, init_scale=8.0, warmup_updates=0, update_freq=2)
+    assert tr.opt.defer
+    taps = []
+    tr.grad_tap = lambda g: taps.append(g.clone()) if not taps else None
     bs = batches(mm, cfg)
     out = {}
     for step in range(3):
         tr.train_step(bs)
-        torch.cuda.synchronize()
         if step == 0:
-            out["grad0"] = model.params.grad.float().cpu().numpy()
+            torch.cuda.synchronize()
+            out["grad0"] = taps[0].float().cpu().numpy()
+            tr.sync()
             out["ost0"] = tr.opt.ost.cpu().numpy()
     tr.sync()
     torch.cuda.synchronize()
@@ -86,8 +89,9 @@ def single_run():
     return out
 
 
-def test_dp_ranks_bit_identical(dp_run):
-    r0, r1 = dp_run
+@pytest.mark.parametrize("mb", BUCKETS_MB)
+def test_dp_ranks_bit_identical(dp_run, mb):
+    r0, r1 = dp_run[mb]
     for k in ("grad0", "params", "master", "ost"):
         assert np.array_equal(r0[k], r1[k]), k
     assert not bool(r0["inconsistent"]) and not bool(r1["inconsistent"])
@@ -95,8 +99,18 @@ def test_dp_ranks_bit_identical(dp_run):
     assert r0["ost"][K.OST_STEP] == 3 and r0["ost"][K.OST_FATAL] == 0
 
 
+def test_dp_bucket_size_invariant(dp_run):
+    """The same sums whatever the bucket cut: every size gives the 0.25 MB run's bits."""
+    ref = dp_run[BUCKETS_MB[0]][0]
+    assert int(ref["nbuckets"]) > 1 and int(dp_run[BUCKETS_MB[-1]][0]["nbuckets"]) == 1
+    for mb in BUCKETS_MB[1:]:
+        for k in ("grad0", "params", "master", "ost"):
+            assert np.array_equal(dp_run[mb][0][k], ref[k]), (mb, k)
+
+
 def test_dp_gradient_equals_accumulated_union(dp_run, single_run):
     K = pkg("kernels")
+    dp_run = dp_run[BUCKETS_MB[0]]
     dp = dp_run[0]["grad0"] * 2.0              # DDP average -> sum
     assert _rel(dp, single_run["grad0"]) < 1e-3
     # same multiply factor: world / (scale * sample_size) on the average == 1 / (scale * size) on the sum

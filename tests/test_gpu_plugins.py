@@ -293,3 +293,101 @@ def test_cli_trains_on_manifest_with_multitask(tmp_path, capsys):
               "target_ctc_decoder.proj.weight", "decoder_ctc_decoder.proj.bias"):
         assert k in ck["model"], k
     assert tuple(ck["model"]["source_letter_decoder.layers.0.encoder_attn.k_proj.weight"].shape) == (256, 256)
+
+
+FUSION_NODROP = FUSION_YAML.replace("SA_image_dropout: 0.1", "SA_image_dropout: 0.0")
+
+
+def _rel_all(ga, gb, names):
+    num = sum(float((ga[n].float() - gb[n].float()).norm() ** 2) for n in names)
+    den = sum(float(gb[n].float().norm() ** 2) for n in names)
+    return (num / max(den, 1e-30)) ** 0.5
+
+
+def test_fairseq_dropin_trains_like_native(monkeypatch, tmp_path):
+    """fairseq-train's call sequence (stub fairseq restating its behaviour,
+    tests/fairseq_stub.py) drives setup_task -> load_dataset -> build_model -> build_criterion ->
+    criterion(model, sample) -> backward through the adapter.  With the stub's built-in
+    speech_to_unit (the reference's criterion: model(**net_input, return_all_hiddens=True), then
+    compute_loss(model, [net_output], sample) -> get_normalized_probs -> label_smoothed_nll_loss
+    in torch fp32) the loss equals the native path's to 1e-5 and the per-parameter gradients to
+    5e-3 (the two LS-CE implementations round dlogits to fp16 differently); through the adapter's
+    own alias criterion (HIP LS-CE) both are bit-identical to the native path.  Dropout is on
+    (p = 0.1 everywhere); each run restarts the dropout stream from the same seed."""
+    import fairseq_stub
+    fs, regs, args, c, _ = fairseq_stub.dropin_setup(monkeypatch, tmp_path, FUSION_NODROP)
+    P = pkg("plugins")
+    task = fs.tasks.setup_task(args)
+    task.load_dataset("train")
+    model = task.build_model(args).half()          # fairseq Trainer: model.half() for --fp16
+    crit = task.build_criterion(args)
+    alias = regs["criterion"]["speech_to_unit_v2"].build_criterion(args, task)
+    batches = task.get_batch_iterator(task.dataset("train"), max_tokens=450, max_positions=task.max_positions())
+    sample = fs.utils.apply_half(fs.utils.move_to_cuda(batches[0]))
+    net = model.impl.net
+    names = [n for n, _ in model.named_parameters()]
+    model.train()
+    runs = {}
+    for kind in ("fairseq", "alias", "native"):
+        model.zero_grad(set_to_none=True)
+        net.drop.reset(7)
+        if kind == "native":
+            net.params.grad.zero_()                # as the native Trainer does per micro-batch
+            loss, ss, log = P.SpeechToUnitCriterion(task.impl, 0.2)(model.impl, sample)
+            loss.backward()
+            torch.cuda.synchronize()
+            g = {n: net.params.g[n if n != "decoder.output_projection.weight" else "decoder.embed_tokens.weight"].clone()
+                 for n in names}
+        else:
+            loss, ss, log = (crit if kind == "fairseq" else alias)(model, sample)
+            loss.backward()
+            torch.cuda.synchronize()
+            g = {n: p.grad.clone() for n, p in model.named_parameters()}
+        assert ss == sample["ntokens"] and log["nsentences"] == sample["target"].size(0)
+        runs[kind] = (float(loss), g)
+    ln, gn = runs["native"]
+    la, ga = runs["alias"]
+    lf, gf = runs["fairseq"]
+    assert la == ln and all(torch.equal(ga[n], gn[n]) for n in names)
+    assert abs(lf - ln) / abs(ln) < 1e-5, (lf, ln)
+    assert _rel_all(gf, gn, names) < 5e-3
+    for n in ("encoder.subsample.conv_layers.0.weight", "encoder.multimodal_attns.0.in_proj_weight",
+              "decoder.embed_tokens.weight"):
+        assert _rel_all(gf, gn, [n]) < 1e-2, n
+
+
+def test_fairseq_dropin_multitask_ctc_matches_native(monkeypatch, tmp_path):
+    """The reference recipe's multitask head through the drop-in: fairseq's own CTC decoder
+    (stub CTCDecoder = Linear) reads extra["encoder_states"][0] from the HIP model's forward and
+    the stub's MultitaskCriterion / CtcCriterion compute its loss in torch; the gradient it puts on
+    the encoder state enters the hand-written backward.  Against the native path (HIP CTC head in
+    the flat buffer, same weights): total loss to 1e-3, encoder gradients to 1e-2."""
+    import fairseq_stub
+    fs, regs, args, c, _ = fairseq_stub.dropin_setup(monkeypatch, tmp_path, FUSION_NODROP, multitask=True,
+                                                     extra="--dropout 0 --attention-dropout 0 --relu-dropout 0")
+    P = pkg("plugins")
+    task = fs.tasks.setup_task(args)
+    task.load_dataset("train")
+    model = task.build_model(args).half()
+    crit = task.build_criterion(args)
+    native = P.MM_S2UTTransformerModel.build_model(args, task.impl)
+    sd = {k: v for k, v in model.state_dict().items()}
+    native.load_state_dict({k: v for k, v in sd.items() if k in native.net.params.offsets or k in native.net.params.unused})
+    batches = task.get_batch_iterator(task.dataset("train"), max_tokens=450, max_positions=task.max_positions())
+    sample = fs.utils.apply_half(fs.utils.move_to_cuda(batches[0]))
+    model.train()
+    native.train()
+    loss_f, _, log = crit(model, sample)
+    loss_f.backward()
+    loss_n, _, logn = P.SpeechToUnitCriterion(task.impl, 0.2)(native, sample)
+    loss_n.backward()
+    torch.cuda.synchronize()
+    assert "target_ctc" in log["multitask"] and float(log["multitask"]["target_ctc"]["loss"]) > 0
+    assert abs(float(loss_f) - float(loss_n)) / abs(float(loss_n)) < 1e-3
+    gf = {n: p.grad for n, p in model.named_parameters()}
+    gn = {n: native.net.params.g[n] for n in native.net.params.offsets}
+    enc = [n for n in gn if n.startswith("encoder.transformer_layers.0.")]
+    assert _rel_all(gf, gn, enc) < 1e-2
+    assert _rel_all(gf, gn, ["target_ctc_decoder.proj.weight"]) < 1e-2
+    # the head's gradient reached the encoder: without it layer 0 would see only the main loss
+    assert float(gf["encoder.transformer_layers.0.fc1.weight"].float().norm()) > 0

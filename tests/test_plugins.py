@@ -3,8 +3,10 @@
 fairseq is not importable here: the adapter is checked against a stub registry that mimics the
 decorator API of fairseq.tasks / fairseq.models / fairseq.criterions.
 """
-import sys
+import sys  # noqa: F401
 import types
+
+import numpy as np
 
 import pytest
 import torch
@@ -128,60 +130,86 @@ def test_cli_rejects_non_fp16_and_missing_data():
         cli.main(["/d", "--fp16", "--criterion", "cross_entropy", "--synthetic"])
 
 
-def _stub_fairseq(monkeypatch, preexisting_criteria=("speech_to_unit",)):
-    regs = {"task": {}, "model": {}, "arch": {}, "criterion": {c: object for c in preexisting_criteria}}
-
-    def deco(kind):
-        def reg(name):
-            def d(cls):
-                assert name not in regs[kind], f"duplicate {kind} {name}"
-                regs[kind][name] = cls
-                return cls
-            return d
-        return reg
-
-    def reg_arch(model_name, arch_name):
-        def d(fn):
-            regs["arch"][arch_name] = (model_name, fn)
-            return fn
-        return d
-
-    class FairseqTask:
-        def __init__(self, args):
-            self.args = args
-
-    class FairseqCriterion(torch.nn.Module):
-        def __init__(self, task):
-            super().__init__()
-            self.task = task
-
-    fs = types.ModuleType("fairseq")
-    tasks = types.ModuleType("fairseq.tasks")
-    tasks.FairseqTask, tasks.register_task = FairseqTask, deco("task")
-    models = types.ModuleType("fairseq.models")
-    models.BaseFairseqModel = torch.nn.Module
-    models.register_model, models.register_model_architecture = deco("model"), reg_arch
-    crit = types.ModuleType("fairseq.criterions")
-    crit.FairseqCriterion, crit.register_criterion = FairseqCriterion, deco("criterion")
-    crit.CRITERION_REGISTRY = regs["criterion"]
-    for name, m in (("fairseq", fs), ("fairseq.tasks", tasks), ("fairseq.models", models),
-                    ("fairseq.criterions", crit)):
-        monkeypatch.setitem(sys.modules, name, m)
-    return fs, regs
-
-
 def test_fairseq_adapter_registers_reference_names(monkeypatch):
-    fs, regs = _stub_fairseq(monkeypatch)
-    task, model, crits = pkg("fairseq_adapter").register(fs)
+    import fairseq_stub
+    fs, regs = fairseq_stub.install(monkeypatch)
+    task, model, crits, _ = pkg("fairseq_adapter").register(fs)
     assert regs["task"]["multimodal_speech_to_speech"] is task
     assert regs["model"]["mm_s2ut_transformer"] is model
-    assert regs["arch"]["mm_s2ut_transformer"][0] == "mm_s2ut_transformer"
+    assert regs["arch"]["mm_s2ut_transformer"] is model
     # fairseq's built-in speech_to_unit keeps its name; the free aliases are ours
-    assert regs["criterion"]["speech_to_unit"] is object
+    assert regs["criterion"]["speech_to_unit"].__name__ == "SpeechToUnit"    # the stub's built-in
     assert set(crits) == {"speech_to_speech", "speech_to_unit_v2"}
     ns = types.SimpleNamespace()
-    regs["arch"]["mm_s2ut_transformer"][1](ns)
+    regs["arch_cfg"]["mm_s2ut_transformer"](ns)
     assert ns.encoder_embed_dim == 512 and ns.decoder_layers == 6 and ns.conv_channels == 1024
+
+
+def test_fairseq_dropin_task_dataset_model_cpu(monkeypatch, tmp_path):
+    """fairseq-train's call sequence against the adapter, up to the model's forward (which needs
+    the GPU; tests/test_gpu_plugins.py runs the rest): setup_task -> load_dataset -> batches ->
+    build_model -> build_criterion, with the reference's contracts checked at each step
+    (criterions/speech_to_speech_criterion.py:56,73-76; tasks/speech_to_speech.py:83-123)."""
+    import fairseq_stub
+    fs, regs, args, c, _ = fairseq_stub.dropin_setup(monkeypatch, tmp_path, FUSION_YAML, multitask=True)
+    base = fs.tasks.LegacyFairseqTask(args)     # the stub base restates fairseq's abstract members
+    with pytest.raises(NotImplementedError):
+        base.load_dataset("train")
+    with pytest.raises(NotImplementedError):
+        base.target_dictionary
+    task = fs.tasks.setup_task(args)
+    assert len(task.target_dictionary) == 1004 and task.target_dictionary.pad() == 1
+    assert task.source_dictionary is None
+    assert set(task.multitask_tasks) == {"target_ctc"}
+    mt = task.multitask_tasks["target_ctc"]
+    assert (mt.args.input_from, mt.args.input_layer, mt.args.decoder_type) == ("encoder", 0, "ctc")
+    ds = task.load_dataset("train")
+    assert task.dataset("train") is ds and len(ds) == 6
+    batches = task.get_batch_iterator(ds, max_tokens=450, max_positions=task.max_positions())
+    seen = []
+    for sample in batches:
+        ni = sample["net_input"]
+        ids = sample["id"].tolist()
+        seen += ids
+        assert ni["src_tokens"] is None and ni["src_lengths"].tolist() == sorted(ni["src_lengths"].tolist(), reverse=True)
+        # the waveforms travel as the int32 bit patterns of the fp32 samples (apply_half-proof)
+        assert ni["src_waves"].dtype == torch.int32
+        off = ni["src_wave_offsets"].tolist()
+        for j, i in enumerate(ids):
+            w = ni["src_waves"][off[j]:off[j + 1]].view(torch.float32).numpy()
+            assert np.array_equal(w, c["waves"][i])
+        assert fs.utils.apply_half(sample)["net_input"]["src_waves"].dtype == torch.int32
+        assert ni["imgs_list"][0].shape[1:] == (12, 768) and ni["img_masks_list"][0].dtype == torch.bool
+        assert sample["target"][:, -1].tolist() == [2 if t == sample["target"].shape[1] else 1
+                                                    for t in sample["target_lengths"].tolist()]
+        assert set(sample["multitask"]) == {"target_ctc"}
+        assert sample["multitask"]["target_ctc"]["target"].shape[0] == len(ids)
+    assert sorted(seen) == list(range(6))
+    model = task.build_model(args)
+    # the reference model's state-dict keys (fairseq module tree), every parameter a view of the
+    # flat HIP buffer; the multitask head is fairseq's own module under {task}_decoder.*
+    sd = model.state_dict()
+    ref_keys = set(model.impl.net.params.state_dict())
+    assert ref_keys <= set(sd) and "decoder.output_projection.weight" in sd
+    assert "encoder.proj_768_to_512.weight" in sd and "target_ctc_decoder.proj.weight" in sd
+    assert "flat" not in sd
+    flat = model.impl.net.params.flat
+    lo, hi = flat.data_ptr(), flat.data_ptr() + 2 * flat.numel()
+    named = dict(model.named_parameters())
+    assert all(lo <= p.data_ptr() < hi for n, p in named.items() if not n.startswith("target_ctc_decoder"))
+    assert model.get_parameter("decoder.output_projection.weight") is model.get_parameter("decoder.embed_tokens.weight")
+    assert set(model.multitask_decoders) == {"target_ctc"}
+    # a checkpoint round trip through the fairseq key names writes the flat buffer
+    sd2 = {k: v.clone() for k, v in sd.items()}
+    sd2["encoder.layer_norm.weight"].fill_(0.5)
+    model.load_state_dict(sd2, strict=True)
+    assert torch.all(model.impl.net.params.p["encoder.layer_norm.weight"] == 0.5)
+    # get_normalized_probs on the criterion's one-element list (compute_loss(model, [net_output]))
+    lg = torch.randn(2, 3, 1004)
+    lp = model.get_normalized_probs([lg], log_probs=True)
+    assert torch.allclose(lp.exp().sum(-1), torch.ones(2, 3), atol=1e-5)
+    crit = task.build_criterion(args)
+    assert type(crit).__name__ == "SpeechToUnit" and crit.eps == 0.2 and set(crit.multitask_criterion) == {"target_ctc"}
 
 
 def _reducer_worker(rank, world, port, q):
