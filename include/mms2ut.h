@@ -357,8 +357,9 @@ int mms2ut_ctc_loss_bwd(const mms2ut_half* logits, int64_t ld, int B, int T, int
                         hipStream_t stream);
 /* fairseq Trainer._check_grad_norms on device.  stage 0: buf[0..world) = 0 except
  * buf[rank] = ost[MMS_OST_GNORM]; the caller SUM-all-reduces buf; stage 1: ost[MMS_OST_INCONSISTENT]
- * = 1 when the norms are finite and max|n_r - n_0| / (n_0 + 1e-6) >= 1e-6 — optim_prepare then
- * sets MMS_OST_FATAL and no rank updates (the host raises FloatingPointError at its next read). */
+ * = 1 when the norms are finite and max|n_r - n_0| / (n_0 + 1e-6) >= 1e-6 (sticky: never cleared)
+ * — optim_prepare then sets MMS_OST_FATAL, which is sticky as well: from that step on no rank
+ * updates anything (the host raises FloatingPointError on every rank at its next check).        */
 int mms2ut_grad_norm_check(float* buf, int world, int rank, float* ost, int stage, hipStream_t stream);
 /* x *= alpha in place (fp16, n % 8 == 0): the data-parallel gradient pre-division by world size
  * (torch DDP's allreduce hook divides each bucket before its SUM all-reduce)                    */

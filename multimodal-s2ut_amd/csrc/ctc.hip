@@ -13,8 +13,11 @@
 // recursion the same way and emits the logits gradient of row t as soon as beta_t is known:
 //   dlogit[t][v] = g * (exp(lp[t][v]) - exp(LSE_{s: l'(s)=v}(alpha_t(s) + beta_t(s)) - lp[t][v] + loss))
 // (alpha and beta both include the emission at t; PyTorch's ctc_loss backward formula).  The
-// per-label log-sum-exp is segmented through LDS: a max pass (integer atomicMax on the
-// order-preserving bit pattern) and a sum-of-exp pass (LDS float atomicAdd).
+// per-label log-sum-exp is deterministic and independent of the vocabulary size: the distinct
+// labels of the extended sequence are ranked once per utterance (ascending, <= S + 1 of them, in
+// LDS, with each position's rank); per time step one thread per distinct label reduces its
+// positions in ascending order (max, then sum of exp), and the gradient loop over v finds v's
+// rank by binary search.  The summed loss is reduced over utterances in a fixed order.
 // All arithmetic fp32; the work is tiny (B x T x 2S) and latency-bound, so it is sized for one
 // launch per head per step, not for throughput.
 #include <math.h>
@@ -38,13 +41,6 @@ MMS_DEV float lse3(float a, float b, float c) {
   if (m == NEG_INF) return NEG_INF;
   return m + logf(expf(a - m) + expf(b - m) + expf(c - m));
 }
-
-// order-preserving float <-> int for atomicMax
-MMS_DEV int f2o(float f) {
-  const int i = __float_as_int(f);
-  return i >= 0 ? i : i ^ 0x7fffffff;
-}
-MMS_DEV float o2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
 
 // row log-sum-exp of the logits (fp32), one wave per row
 __global__ void ctc_lse_kernel(const h16* __restrict__ logits, long ld, long rows, int V, float* __restrict__ lse) {
@@ -107,8 +103,15 @@ __global__ void __launch_bounds__(CTC_NT) ctc_alpha_kernel(const h16* __restrict
     float loss = -ll;
     if (!isfinite(loss) && zero_inf) loss = 0.f;
     loss_b[b] = loss;
-    atomicAdd(loss_sum, loss);
   }
+}
+
+// loss_sum[0] += sum_b loss_b[b], one wave, fixed order (bit-reproducible; no float atomics)
+__global__ void ctc_loss_sum_kernel(const float* __restrict__ loss_b, int B, float* __restrict__ loss_sum) {
+  float s = 0.f;
+  for (int b = threadIdx.x; b < B; b += 64) s += loss_b[b];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) loss_sum[0] += s;
 }
 
 __global__ void __launch_bounds__(CTC_NT) ctc_beta_grad_kernel(const h16* __restrict__ logits, long ld, int T, int V,
@@ -119,7 +122,7 @@ __global__ void __launch_bounds__(CTC_NT) ctc_beta_grad_kernel(const h16* __rest
                                                              const float* __restrict__ loss_b,
                                                              const float* __restrict__ grad_scale, h16* __restrict__ dlogits,
                                                              long ldd) {
-  extern __shared__ float sh[];   // 2 x S2max beta rows | V maxima (int) | V sums
+  extern __shared__ float sh[];   // 2 x S2max beta rows | S2max ranks (int) | S2max labels (int) | S2max gammas
   const int b = blockIdx.x;
   const int Tb = min(in_len[b], T), Sb = tgt_len[b];
   const int S2 = 2 * Sb + 1;
@@ -130,10 +133,42 @@ __global__ void __launch_bounds__(CTC_NT) ctc_beta_grad_kernel(const h16* __rest
   h16* D = dlogits + (long)b * T * ldd;
   float* cur = sh;
   float* nxt = sh + S2max;
-  int* vmax = reinterpret_cast<int*>(sh + 2 * S2max);
-  float* vsum = sh + 2 * S2max + V;
+  int* own = reinterpret_cast<int*>(sh + 2 * S2max);   // [S2] rank of position s's label
+  int* lab = own + S2max;                              // [U] distinct labels, ascending
+  float* gam = reinterpret_cast<float*>(lab + S2max);  // [U] log-sum-exp of alpha + beta per label
+  __shared__ int U;
   const float g = grad_scale[0];
   auto lp = [&](int t, int v) { return (float)X[(long)t * ld + v] - Lb[t]; };
+  // distinct labels: own[s] = 1 at a label's first position, then ranks by label value
+  if (threadIdx.x == 0) U = 0;
+  for (int s = threadIdx.x; s < S2; s += blockDim.x) {
+    const int l = ext_label(tgt, s, blank);
+    int first = 1;
+    for (int q = 0; q < s && first; ++q) first = ext_label(tgt, q, blank) != l;
+    own[s] = first;
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < S2; s += blockDim.x) {
+    if (!own[s]) continue;
+    const int l = ext_label(tgt, s, blank);
+    int r = 0;
+    for (int q = 0; q < S2; ++q) r += (own[q] && ext_label(tgt, q, blank) < l) ? 1 : 0;
+    lab[r] = l;
+    atomicAdd(&U, 1);
+  }
+  __syncthreads();
+  const int nU = U;
+  auto rank_of = [&](int v) {          // index of v in lab[0, nU) or -1
+    int lo = 0, hi = nU - 1;
+    while (lo <= hi) {
+      const int mid = (lo + hi) >> 1;
+      const int x = lab[mid];
+      if (x == v) return mid;
+      if (x < v) lo = mid + 1; else hi = mid - 1;
+    }
+    return -1;
+  };
+  for (int s = threadIdx.x; s < S2; s += blockDim.x) own[s] = rank_of(ext_label(tgt, s, blank));
   // padded time steps and padded columns: zero gradient
   for (int t = Tb; t < T; ++t)
     for (int v = threadIdx.x; v < (int)ldd; v += blockDim.x) D[(long)t * ldd + v] = (h16)0.f;
@@ -145,6 +180,7 @@ __global__ void __launch_bounds__(CTC_NT) ctc_beta_grad_kernel(const h16* __rest
   }
   const bool impossible = !(lastA > NEG_INF);
   (void)loss_b;
+  __syncthreads();
   for (int t = Tb - 1; t >= 0; --t) {
     float* tmp = nxt; nxt = cur; cur = tmp;
     for (int s = threadIdx.x; s < S2; s += blockDim.x) {
@@ -160,18 +196,20 @@ __global__ void __launch_bounds__(CTC_NT) ctc_beta_grad_kernel(const h16* __rest
       }
       cur[s] = bt;
     }
-    for (int v = threadIdx.x; v < V; v += blockDim.x) { vmax[v] = f2o(NEG_INF); vsum[v] = 0.f; }
     __syncthreads();
     const float* At = A + (long)t * S2max;
-    for (int s = threadIdx.x; s < S2; s += blockDim.x) {
-      const float ab = At[s] + cur[s];
-      if (ab > NEG_INF) atomicMax(&vmax[ext_label(tgt, s, blank)], f2o(ab));
-    }
-    __syncthreads();
-    for (int s = threadIdx.x; s < S2; s += blockDim.x) {
-      const float ab = At[s] + cur[s];
-      const int l = ext_label(tgt, s, blank);
-      if (ab > NEG_INF) atomicAdd(&vsum[l], expf(ab - o2f(vmax[l])));
+    for (int j = threadIdx.x; j < nU; j += blockDim.x) {
+      float m = NEG_INF;
+      for (int s = 0; s < S2; ++s)
+        if (own[s] == j) m = fmaxf(m, At[s] + cur[s]);
+      float acc = 0.f;
+      if (m > NEG_INF)
+        for (int s = 0; s < S2; ++s)
+          if (own[s] == j) {
+            const float ab = At[s] + cur[s];
+            if (ab > NEG_INF) acc += expf(ab - m);
+          }
+      gam[j] = (m > NEG_INF) ? m + logf(acc) : NEG_INF;
     }
     __syncthreads();
     for (int v = threadIdx.x; v < (int)ldd; v += blockDim.x) {
@@ -179,7 +217,8 @@ __global__ void __launch_bounds__(CTC_NT) ctc_beta_grad_kernel(const h16* __rest
       if (v < V && !impossible) {
         const float lpv = lp(t, v);
         d = expf(lpv);
-        if (vsum[v] > 0.f) d -= expf(logf(vsum[v]) + o2f(vmax[v]) - lpv - lastA);
+        const int j = rank_of(v);
+        if (j >= 0 && gam[j] > NEG_INF) d -= expf(gam[j] - lpv - lastA);
         d *= g;
       }
       D[(long)t * ldd + v] = (h16)d;
@@ -203,7 +242,8 @@ extern "C" int mms2ut_ctc_loss_fwd(const h16* logits, int64_t ld, int B, int T, 
   MMS_REQUIRE(V > 0 && ld >= V && blank >= 0 && blank < V && max_tgt_len >= 0 && tgt_ld >= max_tgt_len,
               "ctc_loss: bad shapes (V=%d ld=%ld blank=%d S=%d)", V, (long)ld, blank, max_tgt_len);
   const int S2 = 2 * max_tgt_len + 1;
-  MMS_REQUIRE((size_t)2 * S2 * sizeof(float) <= 64 * 1024, "ctc_loss: target too long (%d)", max_tgt_len);
+  MMS_REQUIRE((size_t)5 * S2 * sizeof(float) <= 64 * 1024, "ctc_loss: target too long (%d labels, max %d)",
+              max_tgt_len, (int)((64 * 1024 / (5 * sizeof(float)) - 1) / 2));
   if (B == 0 || T == 0) return 0;
   float* lse = work;
   float* alpha = work + (long)B * T;
@@ -213,6 +253,7 @@ extern "C" int mms2ut_ctc_loss_fwd(const h16* logits, int64_t ld, int B, int T, 
                      logits, (long)ld, rows, V, lse);
   hipLaunchKernelGGL(ctc_alpha_kernel, dim3(B), dim3(CTC_NT), 2 * S2 * sizeof(float), s, logits, (long)ld, T, V,
                      lse, targets, (long)tgt_ld, in_len, tgt_len, blank, zero_infinity, S2, alpha, loss_b, loss_sum);
+  hipLaunchKernelGGL(ctc_loss_sum_kernel, dim3(1), dim3(64), 0, s, loss_b, B, loss_sum);
   return mms::check_launch("ctc_loss_fwd");
 }
 
@@ -222,8 +263,9 @@ extern "C" int mms2ut_ctc_loss_bwd(const h16* logits, int64_t ld, int B, int T, 
                                    hipStream_t s) {
   MMS_REQUIRE(ldd >= V && ldd % 4 == 0, "ctc_loss_bwd: ldd must be >= V and a multiple of 4");
   const int S2 = 2 * max_tgt_len + 1;
-  const size_t lds = (2 * (size_t)S2 + 2 * (size_t)V) * sizeof(float);
-  MMS_REQUIRE(lds <= 64 * 1024, "ctc_loss_bwd: target/vocabulary too large for LDS");
+  const size_t lds = 5 * (size_t)S2 * sizeof(float);   // independent of the vocabulary size
+  MMS_REQUIRE(lds <= 64 * 1024, "ctc_loss_bwd: target too long for LDS (%d labels, max %d)", max_tgt_len,
+              (int)((64 * 1024 / (5 * sizeof(float)) - 1) / 2));
   if (B == 0 || T == 0) return 0;
   const float* lse = work;
   const float* alpha = work + (long)B * T;

@@ -137,6 +137,9 @@ __global__ void grad_norm_finalize_kernel(const float* __restrict__ part, int np
 __global__ void optim_prepare_kernel(float* ost, float lr_peak, float warmup_init_lr, float warmup_updates,
                                      float b1, float b2, float clip, float scale_window, float min_scale) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  // FATAL is sticky: fairseq raises (FloatingPointError) at the first fatal step, so no later step
+  // may update anything; every rank holds the same state vector and stops at the same step
+  if (ost[MMS_OST_FATAL] != 0.f) return;
   if (ost[MMS_OST_INCONSISTENT] != 0.f) {
     // fairseq Trainer._check_grad_norms raised: no update, the run is dead (FATAL for the host)
     ost[MMS_OST_FATAL] = 1.f;
@@ -196,7 +199,7 @@ __global__ void __launch_bounds__(256) adam_kernel(h16* __restrict__ param, cons
                                                    float* __restrict__ v, long n, const float* __restrict__ ost,
                                                    float b1, float b2, float eps, float wd) {
   // overflow: skip (FP16Optimizer OverflowError path); inconsistent grads across ranks: no update
-  if (ost[MMS_OST_OVERFLOW] != 0.f || ost[MMS_OST_INCONSISTENT] != 0.f) return;
+  if (ost[MMS_OST_OVERFLOW] != 0.f || ost[MMS_OST_INCONSISTENT] != 0.f || ost[MMS_OST_FATAL] != 0.f) return;
   const float lr = ost[MMS_OST_LR];
   const float mult = ost[MMS_OST_MULT] * ost[MMS_OST_CLIP_COEF];
   const float step_size = ost[MMS_OST_STEP_SIZE];
@@ -255,7 +258,8 @@ __global__ void grad_norm_check_kernel(float* buf, int world, int rank, float* o
     finite = finite && isfinite(buf[r]);
     dmax = fmaxf(dmax, fabsf(buf[r] - buf[0]));
   }
-  ost[MMS_OST_INCONSISTENT] = (finite && dmax / (buf[0] + 1e-6f) >= 1e-6f) ? 1.f : 0.f;
+  // sticky: once a step was inconsistent the flag stays set (the host reads it at its log cadence)
+  if (finite && dmax / (buf[0] + 1e-6f) >= 1e-6f) ost[MMS_OST_INCONSISTENT] = 1.f;
 }
 
 // x *= alpha (fp16, in place): DDP's pre-division of a gradient bucket by the world size

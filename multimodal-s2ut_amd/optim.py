@@ -95,6 +95,21 @@ class FP16Adam:
             ps.pending["__grad_zero__"] = ev
             ps.grad_zeroed = True
 
+    def check_fatal(self, st=None):
+        """Raise fairseq's FloatingPointError if the device state turned FATAL (sticky: an
+        inconsistent grad norm across ranks, Trainer._check_grad_norms, or the minimum loss scale
+        reached, DynamicLossScaler).  The state vector is identical on every rank, so every rank
+        calling this at the same step raises together."""
+        st = st or self.stats()
+        if st["inconsistent"]:
+            raise FloatingPointError("Fatal error: gradients are inconsistent between workers "
+                                     "(fairseq Trainer._check_grad_norms)")
+        if st["fatal"]:
+            raise FloatingPointError(f"Minimum loss scale reached ({self.min_loss_scale}). Your loss is probably "
+                                     "exploding. Try lowering the learning rate, using gradient clipping or "
+                                     "increasing the batch size.")
+        return st
+
     def stats(self):
         if hasattr(self.params, "await_all"):
             self.params.await_all()

@@ -59,7 +59,7 @@ class _ScriptedDraws:
 class Trainer:
     def __init__(self, model, lr=5e-4, betas=(0.9, 0.98), clip_norm=10.0, warmup_updates=10000,
                  warmup_init_lr=1e-7, init_scale=128.0, bucket_mb=64.0, world_size=1, update_freq=1,
-                 graph=False, device_seed=None):
+                 graph=False, device_seed=None, max_graphs=64):
         self.model = model
         self.cfg = model.cfg
         self.update_freq = int(update_freq)
@@ -98,6 +98,7 @@ class Trainer:
                 raise ValueError("graph mode: single process on a GPU (world size 1) only")
             self.opt.defer = False        # no cross-step event handoff: each replay is self-contained
             self.graphs = {}
+            self.max_graphs = int(max_graphs)
             self.pool = torch.cuda.graph_pool_handle()
             self.draws = _ScriptedDraws()
             model.np_rng = self.draws
@@ -163,6 +164,11 @@ class Trainer:
                     prologue()
                 log = self._train_step(batches)
             if not eager:
+                if len(self.graphs) >= self.max_graphs:
+                    # each graph pins its batches and every scratch buffer it baked in: graph mode is
+                    # for a fixed resident batch set (the bench), not a stream of fresh batches
+                    raise RuntimeError(f"graph mode: more than {self.max_graphs} distinct (batch set, modality "
+                                       "branch) keys; use eager mode for streamed batches")
                 self.draws.vals = vals
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self.pool, stream=self.stream):
@@ -249,23 +255,50 @@ class Trainer:
         return loss, nll
 
     # ------------------------------------------------------------------ checkpoints
+    def completed_updates(self):
+        """fairseq's num_updates: optimizer steps that were applied (fp16-overflow skips excluded),
+        read from the device state (a host sync)."""
+        self.sync()
+        return int(self.opt.ost[K.OST_STEP].item())
+
     def state_dict(self):
         """fairseq checkpoint layout (checkpoint_utils.save_checkpoint): model (fairseq keys),
-        last_optimizer_state (fp32 master / Adam moments / device optimizer state vector)."""
+        last_optimizer_state (fp32 master / Adam moments / device optimizer state vector, plus
+        FP16Optimizer's ``loss_scale``), optimizer_history, extra_state (num_updates and the
+        train iterator position ``train_iterator`` = {epoch, iterations_in_epoch})."""
         self.sync()
         o = self.opt
+        n = int(o.ost[K.OST_STEP].item())
+        pos = dict(getattr(self, "position", None) or {"epoch": 1, "iterations_in_epoch": 0})
         return {"model": {k: v.detach().cpu() for k, v in self.model.params.state_dict().items()},
                 "last_optimizer_state": {"master": o.master.cpu(), "exp_avg": o.exp_avg.cpu(),
-                                         "exp_avg_sq": o.exp_avg_sq.cpu(), "ost": o.ost.cpu()},
-                "extra_state": {"num_updates": int(o.ost[K.OST_STEP].item())}}
+                                         "exp_avg_sq": o.exp_avg_sq.cpu(), "ost": o.ost.cpu(),
+                                         "loss_scale": float(o.ost[K.OST_LOSS_SCALE].item())},
+                "optimizer_history": [{"criterion_name": "SpeechToUnitMultitaskTaskCriterion",
+                                       "optimizer_name": "FP16Optimizer",
+                                       "lr_scheduler_state": {"best": None}, "num_updates": n}],
+                "extra_state": {"num_updates": n, "train_iterator": dict(pos, shuffle=True)}}
 
     def load_state_dict(self, ckpt):
+        """Our own checkpoints restore the exact optimizer state.  A checkpoint written by fairseq
+        (its FP16Optimizer state has a different layout: per-parameter-group Adam state over
+        fairseq's flattened fp32 params) restores the weights, re-derives the fp32 master from them
+        (FP16Optimizer's behaviour with --reset-optimizer), starts fresh Adam moments and keeps
+        num_updates (lr schedule position) and the loss scale when the file records them."""
         self.sync()
         self.model.params.load_state_dict({k: v for k, v in ckpt["model"].items()
                                            if k != "decoder.output_projection.weight"})
         o, s = self.opt, ckpt.get("last_optimizer_state")
-        if s is None:
-            o.resync_master()
+        ours = isinstance(s, dict) and all(k in s for k in ("master", "exp_avg", "exp_avg_sq", "ost"))
+        if ours:
+            for name in ("master", "exp_avg", "exp_avg_sq", "ost"):
+                getattr(o, name).copy_(s[name])
             return
-        for name in ("master", "exp_avg", "exp_avg_sq", "ost"):
-            getattr(o, name).copy_(s[name])
+        o.resync_master()
+        o.exp_avg.zero_()
+        o.exp_avg_sq.zero_()
+        hist = ckpt.get("optimizer_history") or [{}]
+        n = (ckpt.get("extra_state") or {}).get("num_updates", hist[-1].get("num_updates", 0))
+        o.ost[K.OST_STEP] = float(n or 0)
+        if isinstance(s, dict) and s.get("loss_scale") is not None:
+            o.ost[K.OST_LOSS_SCALE] = float(s["loss_scale"])

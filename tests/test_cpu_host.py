@@ -267,3 +267,51 @@ def test_bench_gpus_flag_launches_ranks(monkeypatch):
     monkeypatch.delenv("MMS2UT_DIST_BACKEND")
     with pytest.raises(SystemExit, match="visible GPUs"):
         bench.launch_ranks(argparse.Namespace(gpus=2))
+
+
+def test_checkpoint_interchange_fairseq_layout(tmp_path):
+    """our checkpoint carries fairseq's top-level layout (model, last_optimizer_state
+    with loss_scale, optimizer_history, extra_state with the train iterator, args as an
+    argparse.Namespace) and round-trips exactly; a fairseq-written checkpoint (FP16Optimizer state
+    in fairseq's own layout) restores the weights, re-derives the fp32 master from them, starts
+    fresh Adam moments and keeps num_updates and the loss scale."""
+    import argparse
+    mm = pkg()
+    K = mm.kernels
+    cfg = mm.default_cfg(**R.no_dropout(R.tiny_config(conv_channels=256)))
+    model = mm.MMS2UTModel(cfg, device="cpu").init_params(seed=2)
+    tr = mm.trainer.Trainer(model, lr=1e-3)
+    tr.opt.ost[K.OST_STEP] = 5.0
+    tr.opt.ost[K.OST_LOSS_SCALE] = 32.0
+    tr.opt.exp_avg.fill_(0.25)
+    tr.position = {"epoch": 3, "iterations_in_epoch": 7}
+    st = tr.state_dict()
+    st["args"] = argparse.Namespace(arch="mm_s2ut_transformer", seed=1)
+    path = tmp_path / "checkpoint_last.pt"
+    torch.save(st, path)
+    with torch.serialization.safe_globals([argparse.Namespace]):
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert ck["optimizer_history"][-1]["num_updates"] == 5 and ck["extra_state"]["num_updates"] == 5
+    assert ck["extra_state"]["train_iterator"] == {"epoch": 3, "iterations_in_epoch": 7, "shuffle": True}
+    assert ck["last_optimizer_state"]["loss_scale"] == 32.0 and ck["args"].arch == "mm_s2ut_transformer"
+    model2 = mm.MMS2UTModel(cfg, device="cpu").init_params(seed=9)
+    tr2 = mm.trainer.Trainer(model2, lr=1e-3)
+    tr2.load_state_dict(ck)
+    assert torch.equal(model2.params.flat, model.params.flat) and torch.all(tr2.opt.exp_avg == 0.25)
+    assert tr2.completed_updates() == 5
+    # fairseq's own FP16Optimizer layout: no master/exp_avg/... keys of ours
+    fs_ck = {"model": dict(ck["model"]),
+             "last_optimizer_state": {"state": {0: {"step": 11, "exp_avg": torch.zeros(3)}},
+                                      "param_groups": [{"lr": 1e-4, "params": [0]}], "loss_scale": 16.0},
+             "optimizer_history": [{"criterion_name": "SpeechToUnitMultitaskTaskCriterion",
+                                    "optimizer_name": "FP16Optimizer", "num_updates": 11}],
+             "extra_state": {"train_iterator": {"epoch": 2, "iterations_in_epoch": 0}}}
+    fs_ck["model"]["encoder.layer_norm.weight"] = torch.full_like(fs_ck["model"]["encoder.layer_norm.weight"], 0.5)
+    model3 = mm.MMS2UTModel(cfg, device="cpu").init_params(seed=9)
+    tr3 = mm.trainer.Trainer(model3, lr=1e-3)
+    tr3.opt.exp_avg.fill_(1.0)
+    tr3.load_state_dict(fs_ck)
+    assert torch.all(model3.params.p["encoder.layer_norm.weight"] == 0.5)
+    assert torch.equal(tr3.opt.master, model3.params.flat.float())
+    assert torch.all(tr3.opt.exp_avg == 0) and torch.all(tr3.opt.exp_avg_sq == 0)
+    assert tr3.completed_updates() == 11 and float(tr3.opt.ost[K.OST_LOSS_SCALE]) == 16.0

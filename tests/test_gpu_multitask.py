@@ -161,3 +161,36 @@ def test_ctc_kernel_vs_torch():
     assert _rel(dg[..., :V], x.grad.transpose(0, 1)) < 2e-3
     assert dg[..., V:].abs().max() == 0 and dg[2].abs().max() == 0      # padding columns, impossible row
     assert dg[1, 30:].abs().max() == 0                                  # frames past the input length
+
+
+def test_ctc_kernel_large_vocab_deterministic():
+    """the CTC gradient no longer keeps per-vocabulary LDS tables (a subword target
+    dictionary of 10k+ entries used to fail), and loss / gradient are bit-reproducible (no float
+    atomics): V = 12000, two runs bit-identical, both equal to torch fp64."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    K = pkg("kernels")
+    g = torch.Generator().manual_seed(3)
+    B, T, V, S = 3, 60, 12000, 20
+    ld = 12000
+    logits = (2 * torch.randn(B * T, ld, generator=g)).half()
+    in_len = torch.tensor([60, 51, 44], dtype=torch.int32)
+    tl = torch.tensor([20, 13, 17], dtype=torch.int32)
+    tg = torch.randint(1, V, (B, S), generator=g)
+    tg[1, 4:8] = 777                                            # repeated label
+    lg, tgd, il, tld = logits.cuda(), tg.cuda(), in_len.cuda(), tl.cuda()
+    outs = []
+    for _ in range(2):
+        loss = torch.zeros(1, device="cuda")
+        work = K.ctc_loss_fwd(lg, B, T, V, tgd, il, tld, S, 0, True, loss)
+        d = K.ctc_loss_bwd(lg, B, T, V, tgd, il, tld, S, 0, work, torch.tensor([1.0], device="cuda"))
+        torch.cuda.synchronize()
+        outs.append((loss.cpu(), d.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    x = logits.double().view(B, T, V).transpose(0, 1).clone().requires_grad_(True)
+    flat = torch.cat([tg[b, :tl[b]] for b in range(B)])
+    ref = torch.nn.functional.ctc_loss(torch.log_softmax(x, -1), flat, in_len.long(), tl.long(), blank=0,
+                                       reduction="sum", zero_infinity=True)
+    ref.backward()
+    assert abs(outs[0][0].item() - ref.item()) / ref.item() < 1e-4
+    assert _rel(outs[0][1].float().view(B, T, ld), x.grad.transpose(0, 1)) < 2e-3

@@ -60,3 +60,31 @@ def test_fp16_adam_matches_fairseq_restatement(clip):
         assert err < 1e-5, (it, err)
         p16 = P.flat.cpu().float()
         assert torch.allclose(p16, master.half().float(), rtol=1e-3, atol=1e-7), it
+
+
+def test_fatal_state_is_sticky():
+    """an inconsistent grad norm across ranks (Trainer._check_grad_norms) in a step the
+    host does not read makes the device state FATAL for good: that step and every later one apply
+    no update, and the next host check raises FloatingPointError (on every rank: the state vector
+    is identical on all of them)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mm = pkg()
+    K = mm.kernels
+    dev = torch.device("cuda")
+    P = _Params(4096, dev)
+    opt = mm.optim.FP16Adam(P, lr=1e-3, warmup_updates=0, init_scale=1.0)
+    ss = torch.tensor([100.0], device=dev)
+    P.grad.fill_(0.01)
+    opt.step(ss)
+    assert opt.check_fatal()["step"] == 1
+    m0 = opt.master.clone()
+    buf = torch.tensor([1.0, 2.0], device=dev)      # two ranks' norms that disagree
+    opt.step(ss, check=lambda ost: K.grad_norm_check(buf, 2, 0, ost, 1))
+    opt.step(ss)                                    # a clean step later: still no update
+    torch.cuda.synchronize()
+    assert torch.equal(opt.master, m0)
+    st = opt.stats()
+    assert st["inconsistent"] and st["fatal"] and st["step"] == 1
+    with pytest.raises(FloatingPointError, match="inconsistent"):
+        opt.check_fatal()
