@@ -207,6 +207,136 @@ def _make_external_case(F, name, *, d, Di, N, B, Te, Ti, text_pad, img_pad, seed
     return res
 
 
+SHIPPED = dict(d=768, Di=768, B=2, Te=125, Ti=577, seed=300, probes=8)
+
+
+def shipped_inputs(seed=SHIPPED["seed"]):
+    """Inputs and parameters of the shipped-shape fusion golden case: d = Di =
+    768 (packed in_proj), Ti = 577 ViT tokens (+ the bias_kv key = 578), Te = 125, B = 2, text and
+    image padding.  Everything comes from a seeded numpy PCG64 stream and is rounded to fp16, so the
+    reference's float64 run and the HIP fp16 run see identical values; the fixture stores a SHA-256
+    of every array instead of the 3.5 M parameters (tests recompute and check it).  Weight
+    gradients are stored as sketches G @ R and L^T @ G with the Gaussian probes returned here."""
+    c = SHIPPED
+    d, Di, B, Te, Ti = c["d"], c["Di"], c["B"], c["Te"], c["Ti"]
+    rng = np.random.default_rng(seed)
+
+    def h(x):
+        return np.asarray(x, np.float16).astype(np.float64)
+
+    def xavier(o, i):
+        a = np.sqrt(6.0 / (i + o))
+        return h(rng.uniform(-a, a, (o, i)))
+
+    P = {
+        "image_pre_norm_module.weight": h(1.0 + 0.1 * rng.standard_normal(Di)),
+        "image_pre_norm_module.bias": h(0.1 * rng.standard_normal(Di)),
+        "gate_denses.0.weight": xavier(d, 2 * d),
+        "gate_denses.0.bias": h(0.1 * rng.standard_normal(d)),
+        "in_proj_weight": np.concatenate([xavier(d, d) / np.sqrt(2), xavier(d, Di) / np.sqrt(2),
+                                          xavier(d, Di) / np.sqrt(2)]).astype(np.float16).astype(np.float64),
+        "in_proj_bias": h(0.1 * rng.standard_normal(3 * d)),
+        "bias_k": h(0.05 * rng.standard_normal((1, 1, d))),
+        "bias_v": h(0.05 * rng.standard_normal((1, 1, d))),
+        "out_proj.weight": xavier(d, d),
+        "out_proj.bias": h(0.1 * rng.standard_normal(d)),
+    }
+    X = {"text": h(rng.standard_normal((Te, B, d))), "img": h(rng.standard_normal((Ti, B, Di))),
+         "gout": h(rng.standard_normal((Te, B, d)))}
+    text_len = np.array([Te, 100])
+    img_len = np.array([Ti, 450])
+    X["text_mask"] = np.arange(Te)[None, :] >= text_len[:, None]
+    X["img_mask"] = np.arange(Ti)[None, :] >= img_len[:, None]
+    shapes = {"in_proj_weight": (3 * d, d), "out_proj.weight": (d, d), "gate_denses.0.weight": (d, 2 * d),
+              "q_proj.weight": (d, d), "k_proj.weight": (d, Di), "v_proj.weight": (d, Di), "proj.weight": (d, d)}
+    probes = {n: (rng.standard_normal((sh[1], c["probes"])), rng.standard_normal((sh[0], c["probes"])))
+              for n, sh in shapes.items()}
+    return P, X, probes
+
+
+def shipped_model_params(P, att):
+    """The shipped case's parameters under the model's state-dict names (``encoder.*``) for one
+    attention type (selective attention takes q / k / v from the packed rows, proj = out_proj)."""
+    d = SHIPPED["d"]
+    out = {f"encoder.{k}": P[k] for k in ("image_pre_norm_module.weight", "image_pre_norm_module.bias",
+                                          "gate_denses.0.weight", "gate_denses.0.bias")}
+    if att == "multimodal_attention":
+        for k in ("in_proj_weight", "in_proj_bias", "bias_k", "bias_v", "out_proj.weight", "out_proj.bias"):
+            out[f"encoder.multimodal_attns.0.{k}"] = P[k]
+        return out
+    W, b = P["in_proj_weight"], P["in_proj_bias"]
+    for j, n in enumerate("qkv"):
+        out[f"encoder.selective_attns.0.{n}_proj.weight"] = W[j * d:(j + 1) * d]
+        out[f"encoder.selective_attns.0.{n}_proj.bias"] = b[j * d:(j + 1) * d]
+    out["encoder.selective_attns.0.proj.weight"] = P["out_proj.weight"]
+    out["encoder.selective_attns.0.proj.bias"] = P["out_proj.bias"]
+    return out
+
+
+def array_digest(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(np.asarray(a, np.float16)).tobytes()).hexdigest()
+
+
+def _make_shipped(M, F):
+    """Both attention types at the shipped shape, gate on, dropout 0 (the HIP RNG's masks cannot be
+    injected into nn.MultiheadAttention), float64 -> tests/golden/shipped_fusion.npz."""
+    c = SHIPPED
+    d, Di = c["d"], c["Di"]
+    P, X, probes = shipped_inputs()
+    out = {"seed": np.array(c["seed"]), **{f"digest.{k}": np.array(array_digest(v)) for k, v in {**P, **X}.items()
+                                           if k not in ("text_mask", "img_mask")}}
+    out["text_mask"], out["img_mask"] = X["text_mask"], X["img_mask"]
+    T = lambda a: torch.from_numpy(np.array(a))  # noqa: E731
+    for att in ("multimodal_attention", "selective_attention"):
+        hm = nn.Module()
+        hm.image_pre_norm_module = nn.LayerNorm([Di], 1e-5, True)
+        hm.image_dropout_module = MaskDropout(0.0, None)
+        hm.text_dropout_module = MaskDropout(0.0, None)
+        hm.gate_denses = nn.ModuleList([M.Linear(2 * d, d)])
+        hm.use_selective_gate, hm.is_merge_text_img, hm.multimodal_attention_type = True, False, att
+        if att == "multimodal_attention":
+            hm.multimodal_attns = nn.ModuleList([F.MultimodalAttention(embed_dim=d, kdim=Di, vdim=Di, num_heads=1,
+                                                                       dropout=0.0, add_bias_kv=True)])
+            names = {"multimodal_attns.0." + k: k for k in ("in_proj_weight", "in_proj_bias", "bias_k", "bias_v",
+                                                           "out_proj.weight", "out_proj.bias")}
+            src = dict(P)
+        else:
+            hm.selective_attns = nn.ModuleList([F.SelectiveAttention(qdim=d, kdim=Di, vdim=Di, attn_dim=d,
+                                                                     intermediate_dim=d, output_dim=d, num_heads=1,
+                                                                     attn_drop=0.0)])
+            W, b = P["in_proj_weight"], P["in_proj_bias"]
+            src = dict(P, **{"q_proj.weight": W[:d], "k_proj.weight": W[d:2 * d], "v_proj.weight": W[2 * d:],
+                             "q_proj.bias": b[:d], "k_proj.bias": b[d:2 * d], "v_proj.bias": b[2 * d:],
+                             "proj.weight": P["out_proj.weight"], "proj.bias": P["out_proj.bias"]})
+            names = {"selective_attns.0." + k: k for k in ("q_proj.weight", "k_proj.weight", "v_proj.weight",
+                                                          "q_proj.bias", "k_proj.bias", "v_proj.bias",
+                                                          "proj.weight", "proj.bias")}
+        names.update({k: k for k in ("image_pre_norm_module.weight", "image_pre_norm_module.bias",
+                                     "gate_denses.0.weight", "gate_denses.0.bias")})
+        hm = hm.double().train()
+        with torch.no_grad():
+            for n, prm in hm.named_parameters():
+                prm.copy_(T(src[names[n]]).view(prm.shape))
+        text = T(X["text"]).requires_grad_(True)
+        res, _ = M.MM_S2STransformerEncoder.fuse_img_feat(hm, text, 0, T(X["img"]), T(X["img_mask"]),
+                                                         T(X["text_mask"]))
+        (res * T(X["gout"])).sum().backward()
+        tag = "mma" if att == "multimodal_attention" else "sa"
+        out[f"{tag}.res"] = res.detach().numpy().astype(np.float32)
+        out[f"{tag}.grad_text"] = text.grad.numpy().astype(np.float32)
+        for n, prm in hm.named_parameters():
+            g = prm.grad.numpy().reshape(prm.shape)
+            key = names[n]
+            if g.ndim == 2:
+                R_, L_ = probes[key]
+                out[f"{tag}.gsk.{n}"] = (g @ R_).astype(np.float32)
+                out[f"{tag}.gskT.{n}"] = (L_.T @ g).astype(np.float32)
+            else:
+                out[f"{tag}.grad.{n}"] = g.astype(np.float32)
+    np.savez_compressed(os.path.join(OUT, "shipped_fusion.npz"), **out)
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference absent; nothing to do")
@@ -241,6 +371,8 @@ def main():
     for i, (name, d, Di, N, B, Te, Ti, tp, ip) in enumerate(ext):
         _make_external_case(F, name, d=d, Di=Di, N=N, B=B, Te=Te, Ti=Ti, text_pad=tp, img_pad=ip, seed=200 + i)
         print("wrote external", name)
+    _make_shipped(M, F)
+    print("wrote shipped_fusion")
 
 
 if __name__ == "__main__":

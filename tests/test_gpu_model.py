@@ -15,7 +15,7 @@ import torch
 
 from conftest import golden_files, pkg
 from oracle import ref_model as R
-from parity_util import check_outputs, grad_errors, report, run_model_pair
+from parity_util import check_outputs, check_relu_replay, grad_errors, report, run_model_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -45,6 +45,7 @@ def _run_pair(mm, cfg, lengths, tlens, img_mask=False, with_images=True, seed=0)
 
 def _check(r, grad_tol=GRAD_TOL):
     check_outputs(r)
+    check_relu_replay(r)
     bad = {k: e for k, e in grad_errors(r).items() if e > grad_tol}
     assert not bad, report(r)
 
@@ -133,6 +134,62 @@ def test_fusion_matches_reference_golden(mm, path):
                 assert model.params.g[name].float().norm() < 1e-2 * np.linalg.norm(z["grad.selective_attns.0.v_proj.bias"]) + 1e-3
                 continue
             assert rel(model.params.g[name], torch.from_numpy(z[k])) < 2e-2, name
+
+
+@pytest.mark.parametrize("att", ["multimodal_attention", "selective_attention"])
+def test_fusion_shipped_shape_golden(mm, att):
+    """the HIP fusion at the shipped shape — d = Di = 768 single head (the
+    768-wide attention path, Ti = 577 keys + the bias_kv column for multimodal attention), Te =
+    125, B = 2, image key padding — against the reference's own float64 run
+    (tests/golden/shipped_fusion.npz, oracle/gen_golden.py _make_shipped; fuse.py:65-167,
+    mm_s2s_transformer.py:594-622).  Inputs / parameters are regenerated from the fixture's seed
+    and checked against its SHA-256 digests; weight gradients are compared through the stored
+    sketches G @ R and L^T @ G.  Tolerances as the toy-shape golden cases."""
+    from oracle import gen_golden as G
+    import os
+    from conftest import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "shipped_fusion.npz"))
+    P, X, probes = G.shipped_inputs(int(z["seed"]))
+    for k, v in {**P, **X}.items():
+        if f"digest.{k}" in z.files:
+            assert G.array_digest(v) == str(z[f"digest.{k}"]), k
+    c = G.SHIPPED
+    d, Di, B, Te, Ti = c["d"], c["Di"], c["B"], c["Te"], c["Ti"]
+    tag = "mma" if att == "multimodal_attention" else "sa"
+    cfg = mm.default_cfg(encoder_embed_dim=d, encoder_layers=0, decoder_layers=0, image_feat_dim=Di,
+                         encoder_attention_heads=1, multimodal_attention_type=att, use_selective_gate=True,
+                         SA_image_dropout=0.0, SA_text_dropout=0.0, SA_attention_dropout=0.0, conv_channels=16,
+                         decoder_embed_dim=d, decoder_attention_heads=1, vocab_size=8)
+    model = mm.MMS2UTModel(cfg, device="cuda")
+    model.params.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in G.shipped_model_params(P, att).items()},
+                                 strict=False)
+    text = torch.from_numpy(X["text"]).transpose(0, 1).reshape(B * Te, d).cuda().half().contiguous()
+    img = torch.from_numpy(X["img"]).transpose(0, 1).cuda().half().contiguous()
+    km = torch.zeros(B, (Ti + 1 + 7) // 8 * 8, dtype=torch.uint8)
+    km[:, :Ti] = torch.from_numpy(X["img_mask"]).to(torch.uint8)
+    res, ctx = model.fusion_fwd(text, img, km.cuda(), B, Te)
+    assert rel(res, torch.from_numpy(z[f"{tag}.res"]).transpose(0, 1).reshape(B * Te, d)) < 5e-3
+    gout = torch.from_numpy(X["gout"]).transpose(0, 1).reshape(B * Te, d).cuda().half().contiguous()
+    dtext = model.fusion_bwd(ctx, gout)
+    torch.cuda.synchronize()
+    assert rel(dtext, torch.from_numpy(z[f"{tag}.grad_text"]).transpose(0, 1).reshape(B * Te, d)) < 1e-2
+    checked = 0
+    for k in z.files:
+        if k.startswith(f"{tag}.grad."):
+            name = "encoder." + k[len(tag) + 6:]
+            if name.endswith("selective_attns.0.k_proj.bias"):   # mathematically zero (shift-invariant softmax)
+                assert model.params.g[name].float().norm() < 1e-2 * np.linalg.norm(z["sa.grad.selective_attns.0.v_proj.bias"]) + 1e-3
+                continue
+            assert rel(model.params.g[name].view(z[k].shape), torch.from_numpy(z[k])) < 2e-2, name
+            checked += 1
+        elif k.startswith(f"{tag}.gsk."):
+            n = k[len(tag) + 5:]
+            g = model.params.g["encoder." + n].float().cpu().double().numpy()
+            R_, L_ = probes[n.split(".", 2)[-1] if "attns" in n else n]
+            assert rel(torch.from_numpy(g @ R_), torch.from_numpy(z[k]).double()) < 2e-2, k
+            assert rel(torch.from_numpy(L_.T @ g), torch.from_numpy(z[f"{tag}.gskT.{n}"]).double()) < 2e-2, k
+            checked += 1
+    assert checked >= 7
 
 
 def test_fusion_dropout_replay_vs_oracle(mm):

@@ -18,7 +18,7 @@ import torch
 
 from conftest import pkg
 from oracle import ref_model as R
-from parity_util import check_outputs, grad_errors, layer_dgrad_errors, report, run_model_pair
+from parity_util import check_outputs, check_relu_replay, grad_errors, layer_dgrad_errors, report, run_model_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -46,6 +46,7 @@ def test_full_base_vit_dropout_replay(mm):
     print(report(r))
     assert r.Te == 250 and r.n_masks == 1 + 12 * 4 + 2 + 1 + 6 * 6
     check_outputs(r)
+    check_relu_replay(r)
     _assert_grads(r)
     for k, e in layer_dgrad_errors(r).items():
         assert e < GRAD_TOL, (k, e)
@@ -59,6 +60,7 @@ def test_full_detr_modality_dropout(mm, modality):
     r = run_model_pair(mm, cfg, lengths, tlens, img_tokens=100, img_mask=True, seed=22, modality=modality)
     print(modality, report(r))
     check_outputs(r)
+    check_relu_replay(r)
     _assert_grads(r)
     enc_keys = [k for k in r.grads if k.startswith("encoder.transformer_layers") or k.startswith("encoder.subsample")]
     if modality == "audio":

@@ -4,7 +4,9 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden_files
+import os
+
+from conftest import GOLDEN, golden_files
 from oracle import ref_model as R
 
 
@@ -68,3 +70,43 @@ def test_external_transformer_oracle_matches_reference(path):
             g = P[name].grad
             g = np.zeros_like(z[k]) if g is None else g.numpy()
             np.testing.assert_allclose(g, z[k], rtol=1e-8, atol=1e-10, err_msg=name)
+
+
+def _shipped():
+    from oracle import gen_golden as G
+    z = np.load(os.path.join(GOLDEN, "shipped_fusion.npz"))
+    P, X, probes = G.shipped_inputs(int(z["seed"]))
+    for k, v in {**P, **X}.items():     # the regenerated arrays are the ones the reference ran on
+        if f"digest.{k}" in z.files:
+            assert G.array_digest(v) == str(z[f"digest.{k}"]), k
+    return G, z, P, X, probes
+
+
+@pytest.mark.parametrize("att", ["multimodal_attention", "selective_attention"])
+def test_shipped_shape_oracle_matches_reference(att):
+    """the oracle's fusion restatement at the shipped shape (d = Di = 768,
+    Ti = 577 (+ bias_kv), Te = 125, B = 2, text and image padding, gate on) against the reference's
+    own float64 run (tests/golden/shipped_fusion.npz); weight gradients through their stored
+    sketches G @ R, L^T @ G."""
+    G, z, P, X, probes = _shipped()
+    tag = "mma" if att == "multimodal_attention" else "sa"
+    cfg = R.base_config(multimodal_attention_type=att, use_selective_gate=True, SA_image_dropout=0.0,
+                        SA_text_dropout=0.0, SA_attention_dropout=0.0)
+    Pm = {k: torch.from_numpy(np.array(v)).clone().requires_grad_(True) for k, v in G.shipped_model_params(P, att).items()}
+    text = torch.from_numpy(X["text"]).clone().requires_grad_(True)
+    res = R.fuse_img_feat(Pm, text, torch.from_numpy(X["img"]), torch.from_numpy(X["img_mask"]),
+                          torch.from_numpy(X["text_mask"]), cfg, {}, dtype=torch.float64)
+    np.testing.assert_allclose(res.detach().numpy(), z[f"{tag}.res"], rtol=1e-5, atol=1e-6)
+    (res * torch.from_numpy(X["gout"])).sum().backward()
+    np.testing.assert_allclose(text.grad.numpy(), z[f"{tag}.grad_text"], rtol=1e-5, atol=1e-6)
+    for k in z.files:
+        if k.startswith(f"{tag}.grad."):
+            g = Pm["encoder." + k[len(tag) + 6:]].grad.numpy().reshape(z[k].shape)
+            np.testing.assert_allclose(g, z[k], rtol=1e-5, atol=1e-6, err_msg=k)
+        elif k.startswith(f"{tag}.gsk."):
+            n = k[len(tag) + 5:]
+            g = Pm["encoder." + n].grad.numpy()
+            key = n.split(".", 2)[-1] if "attns" in n else n
+            R_, L_ = probes[key]
+            np.testing.assert_allclose(g @ R_, z[k], rtol=1e-5, atol=1e-5, err_msg=k)
+            np.testing.assert_allclose(L_.T @ g, z[f"{tag}.gskT.{n}"], rtol=1e-5, atol=1e-5, err_msg=k)
