@@ -89,7 +89,9 @@ def make_batches(cfg, rank, nb, max_tokens, device, frontend, n_utts=3000, img_t
         # GEMM-kernel share of the algorithmic FLOPs: everything but the multi-head attention
         # products, which the fused attention kernel executes (the fusion attention stays on GEMMs)
         gemm_flops = flops - (mha if model_mod.FLASH else 0)
-        out.append((wb, batch, sample, 3 * flops, 3 * gemm_flops))
+        # host copies of the first batch's waveforms (collated order) for the CPU baseline's fbank
+        host_waves = [waves[i] for i in wb["order"]] if bi == 0 else None
+        out.append((wb, batch, sample, 3 * flops, 3 * gemm_flops, host_waves))
     return out
 
 
@@ -126,29 +128,42 @@ def cycle_batches(steps, nbatches):
     return max(d for d in range(1, max(1, min(steps, nbatches)) + 1) if steps % d == 0)
 
 
-def cpu_baseline(cfg, model, sample, budget_s=20.0):
+def cpu_baseline(cfg, model, sample, waves, budget_s=20.0, target_frames=3000):
     """The oracle (fp32 PyTorch-CPU restatement) timed on the host cores on a bounded sample of the
-    same workload: a few utterances of one batch, full training step (fwd + bwd + Adam)."""
+    same workload, like for like with the GPU step: the first utterances of
+    the bench's first batch (the GPU's own waveforms, image features and targets, up to
+    ``target_frames`` source frames), per step the Kaldi fbank + utterance CMVN of their waveforms
+    (oracle/ref_fbank.py), collation, the model forward with every dropout site on (Bernoulli
+    masks drawn on the CPU), backward and the FP16Optimizer/Adam update."""
+    from oracle import ref_fbank as RF
     from oracle import ref_model as R
-    ocfg = R.no_dropout(dict(cfg))
+    ocfg = dict(cfg)
     sd = {k: v.detach().float().cpu() for k, v in model.params.p.items()}
     P = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
     ni = sample["net_input"]
-    n = 2
-    sub = {"net_input": {"src_tokens": torch.randn(n, int(ni["src_lengths"][0]), 80),
-                         "src_lengths": ni["src_lengths"][:n].clone(),
-                         "prev_output_tokens": ni["prev_output_tokens"][:n],
-                         "imgs_list": [ni["imgs_list"][0][:n].float()] if ni["imgs_list"] else [],
-                         "img_masks_list": [None] if ni["imgs_list"] else []},
-           "target": sample["target"][:n]}
-    frames = int(sub["net_input"]["src_lengths"].sum())
+    lens = ni["src_lengths"].tolist()
+    n = 1
+    while n < len(lens) and sum(lens[:n + 1]) <= target_frames:
+        n += 1
+    frames = int(sum(lens[:n]))
+    tt = int((sample["target"][:n] != 1).sum(1).max())
+    drop = R.CPUDropout(seed=1)
     states = {k: (torch.zeros_like(v), torch.zeros_like(v)) for k, v in P.items()}
     masters = {k: v.detach().clone() for k, v in P.items()}
 
     def step(i):
+        feats = [RF.utterance_cmvn(RF.fbank(w)) for w in waves[:n]]
+        src = torch.zeros(n, max(f.shape[0] for f in feats), 80)
+        for b, f in enumerate(feats):
+            src[b, :f.shape[0]] = torch.from_numpy(f)
+        sub = {"net_input": {"src_tokens": src, "src_lengths": ni["src_lengths"][:n].clone(),
+                             "prev_output_tokens": ni["prev_output_tokens"][:n, :tt],
+                             "imgs_list": [ni["imgs_list"][0][:n].float()] if ni["imgs_list"] else [],
+                             "img_masks_list": [None] if ni["imgs_list"] else []},
+               "target": sample["target"][:n, :tt]}
         for v in P.values():
             v.grad = None
-        loss, _, _ = R.model_forward(P, sub, ocfg)
+        loss, _, _ = R.model_forward(P, sub, ocfg, masks=drop)
         loss.backward()
         names = list(P)
         R.fp16_optimizer_step([masters[k] for k in names], [P[k].grad.half() for k in names],
@@ -165,8 +180,10 @@ def cpu_baseline(cfg, model, sample, budget_s=20.0):
     dt = time.time() - t0
     return {"value": frames * k / dt, "unit": "audio-frames/s", "cores": torch.get_num_threads(),
             "cpu": cpu_model(), "kind": "port",
-            "sample": f"oracle fp32 training step (fwd+bwd+FP16Optimizer/Adam), {n} utterances / "
-                      f"{frames} frames of the base config, {k} steps in {dt:.1f}s"}
+            "sample": f"oracle fp32 training step on the first B={n} utterances ({frames} source frames, "
+                      f"{tt} target positions) of the bench's first batch: Kaldi fbank + utterance CMVN of their "
+                      f"waveforms, forward with dropout on at every site (CPU-drawn masks), backward, "
+                      f"FP16Optimizer/Adam; {k} steps in {dt:.1f}s on {torch.get_num_threads()} threads"}
 
 
 def decode_cpu_baseline(model, sample, beam, budget_s=20.0):
@@ -471,7 +488,7 @@ def main():
     traffic, traffic_src = gemm_pmc_traffic()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, model, batches[0][2], args.cpu_budget)
+        cpu = cpu_baseline(cfg, model, batches[0][2], batches[0][5], args.cpu_budget)
     if rank == 0:
         achieved = (flops_all / (gemm_all / 1e3) / 1e12) if gemm_all > 0 else None
         class_lines = {k: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[2] / args.steps,
