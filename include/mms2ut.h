@@ -272,9 +272,11 @@ int mms2ut_scale_dropout_bwd(const mms2ut_half* dx, mms2ut_half* dh, int64_t n, 
 int mms2ut_token_embed_fwd(const int64_t* tok, const mms2ut_half* E, const mms2ut_half* pos_table,
                            mms2ut_half* x, int B, int T, int D, int pad_idx, float scale, float p,
                            uint64_t seed, uint64_t offset, hipStream_t stream);
-/* dE[tok] += scale*mask*dx (fp32 accumulation buffer dE32 [V][D]; pad rows skipped)          */
+/* dE[tok] += scale*mask*dx (fp32 accumulation buffer dE32 [V][D], D <= 1024; pad rows skipped).
+ * Deterministic: one block per vocabulary row sums its positions in ascending order (no float
+ * atomics), so the tied-embedding gradient is bit-reproducible.                              */
 int mms2ut_token_embed_bwd(const int64_t* tok, const mms2ut_half* dx, float* dE32, int B, int T,
-                           int D, int pad_idx, float scale, float p, uint64_t seed,
+                           int D, int V, int pad_idx, float scale, float p, uint64_t seed,
                            uint64_t offset, hipStream_t stream);
 /* out(fp16) = a(fp16) + b32(fp32) elementwise                                                */
 int mms2ut_add_f32_to_f16(const mms2ut_half* a, const float* b, mms2ut_half* out, int64_t n,

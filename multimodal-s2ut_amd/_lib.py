@@ -118,7 +118,7 @@ SIGNATURES = {
     "mms2ut_encoder_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, f32, f32, u64, u64, vp]),
     "mms2ut_scale_dropout_bwd": (i32, [vp, vp, i64, f32, f32, u64, u64, vp]),
     "mms2ut_token_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, f32, f32, u64, u64, vp]),
-    "mms2ut_token_embed_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, f32, u64, u64, vp]),
+    "mms2ut_token_embed_bwd": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, f32, f32, u64, u64, vp]),
     "mms2ut_add_f32_to_f16": (i32, [vp, vp, vp, i64, vp]),
     "mms2ut_add_f16": (i32, [vp, vp, vp, i64, vp]),
     "mms2ut_glu_fwd": (i32, [vp, vp, i64, i32, vp]),

@@ -652,7 +652,7 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
   PH_STAMP(0);
   load_chunk(z, 0);
   load_kv(z);
-  if (tid < QC) sD[0][tid] = 0.f;
+  static_assert(QC * CH * sizeof(float) <= sizeof(sDS), "D partials must fit the dS^T buffer");
   int gc = 0;  // running chunk counter: parity selects the sL / sD buffer
   for (; z < Z; z += gridDim.x) {
     const int b = z / P.H, h = z % P.H, znext = z + gridDim.x;
@@ -697,13 +697,23 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
           float dot = 0.f;
 #pragma unroll
           for (int e = 0; e < 8; ++e) dot += (float)o8[e] * (float)d8[e];
-          if (qbase + r < Tq) atomicAdd(&Dr[r], dot);
+          // row r's CH partial dots go to sDS (free until phase 2) at [r][c] = i, summed below in
+          // column order: deterministic (no LDS float atomics)
+          reinterpret_cast<float*>(sDS)[i] = (qbase + r < Tq) ? dot : 0.f;
         }
       }
-      if (tid < QC) { L[tid] = rl * 1.4426950408889634f; sD[buf ^ 1][tid] = 0.f; }   // LSE in log2 units
+      if (tid < QC) L[tid] = rl * 1.4426950408889634f;   // LSE in log2 units
       if (!LAST) load_chunk(z, qbase + QC);
       else if (znext < Z) load_chunk(znext, 0);
       __syncthreads();
+      if (tid < QC) {
+        const float* part = reinterpret_cast<const float*>(sDS) + tid * CH;
+        float dsum = 0.f;
+#pragma unroll
+        for (int c = 0; c < CH; ++c) dsum += part[c];
+        Dr[tid] = dsum;
+      }
+      __syncthreads();   // D complete; phase 2 overwrites sDS
       PH_STAMP(3 + 5 * gc);
       // ---- phase 2: wave w owns keys 16w + 128j: dV, dK accumulate, dS^T -> LDS.  Query steps
       // outermost: the step's Q / dO row fragments and the transposed dO / Q operands of the dV / dK

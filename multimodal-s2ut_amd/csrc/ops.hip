@@ -679,22 +679,51 @@ __global__ void token_embed_fwd_kernel(const int64_t* __restrict__ tok, const h1
   }
 }
 
-__global__ void token_embed_bwd_kernel(const int64_t* __restrict__ tok, const h16* __restrict__ dx,
-                                       float* __restrict__ dE, int B, int T, int D, int pad, float scale,
-                                       float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
+// Embedding-gradient scatter dE[v] += sum_{p: tok[p] = v} scale * dropout(dx[p]), deterministic:
+// one block per vocabulary row walks the token positions in order, 256 at a time (a wave ballot
+// per chunk marks the matches), and each thread accumulates its own columns over the matches in
+// ascending position order — no float atomics, so the gradient is bit-reproducible run to run.
+constexpr int TEB_NT = 256, TEB_COLS = 4;   // D <= 1024
+__global__ void __launch_bounds__(TEB_NT) token_embed_bwd_kernel(
+    const int64_t* __restrict__ tok, const h16* __restrict__ dx, float* __restrict__ dE, long N, int D, int pad,
+    float scale, float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
   if (thresh) seed = mms_step_seed(seed);
-  const int lane = threadIdx.x & 63;
-  const long bt = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (bt >= (long)B * T) return;
-  const int64_t tk = tok[bt];
-  if (tk == pad) return;  // nn.Embedding(padding_idx): no grad to the pad row
+  const int v = blockIdx.x;
+  if (v == pad) return;  // nn.Embedding(padding_idx): no grad to the pad row
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ uint64_t sm[TEB_NT / 64];
   const float ds = thresh ? 1.f / (1.f - p) : 1.f;
-  for (int d = lane; d < D; d += 64) {
-    float v = (float)dx[bt * D + d] * scale;
-    if (thresh) v = mms_keep(seed, offset + bt * D + d, thresh) ? v * ds : 0.f;
-    atomicAdd(dE + tk * D + d, v);
+  float acc[TEB_COLS] = {0.f, 0.f, 0.f, 0.f};
+  for (long c0 = 0; c0 < N; c0 += TEB_NT) {
+    const long q = c0 + tid;
+    const uint64_t bits = __ballot(q < N && tok[q] == v);
+    if (lane == 0) sm[w] = bits;
+    __syncthreads();
+#pragma unroll
+    for (int ww = 0; ww < TEB_NT / 64; ++ww) {
+      uint64_t b = sm[ww];
+      while (b) {
+        const int l = __ffsll((unsigned long long)b) - 1;
+        b &= b - 1;
+        const long row = c0 + ww * 64 + l;
+#pragma unroll
+        for (int k = 0; k < TEB_COLS; ++k) {
+          const int d = tid + k * TEB_NT;
+          if (d < D) {
+            float x = (float)dx[row * D + d] * scale;
+            if (thresh) x = mms_keep(seed, offset + row * D + d, thresh) ? x * ds : 0.f;
+            acc[k] += x;
+          }
+        }
+      }
+    }
+    __syncthreads();
   }
-  (void)B;
+#pragma unroll
+  for (int k = 0; k < TEB_COLS; ++k) {
+    const int d = tid + k * TEB_NT;
+    if (d < D) dE[(long)v * D + d] += acc[k];
+  }
 }
 
 __global__ void add_f32_to_f16_kernel(const h16* __restrict__ a, const float* __restrict__ b,
@@ -1137,11 +1166,13 @@ extern "C" int mms2ut_token_embed_fwd(const int64_t* tok, const h16* E, const h1
 }
 
 extern "C" int mms2ut_token_embed_bwd(const int64_t* tok, const h16* dx, float* dE32, int B, int T,
-                                      int D, int pad_idx, float scale, float p, uint64_t seed,
+                                      int D, int V, int pad_idx, float scale, float p, uint64_t seed,
                                       uint64_t offset, hipStream_t s) {
+  MMS_REQUIRE(D > 0 && D <= TEB_NT * TEB_COLS && V > 0, "token_embed_bwd: D=%d (max %d) V=%d", D,
+              TEB_NT * TEB_COLS, V);
   const long n = (long)B * T;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(token_embed_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, s, tok, dx, dE32, B, T, D,
+  hipLaunchKernelGGL(token_embed_bwd_kernel, dim3(V), dim3(TEB_NT), 0, s, tok, dx, dE32, n, D,
                      pad_idx, scale, p, mms_drop_thresh(p), seed, offset);
   return mms::check_launch("token_embed_bwd");
 }

@@ -239,7 +239,7 @@ def register(fairseq):
                 for name, t in task.multitask_tasks.items():
                     in_dim = cfg["encoder_embed_dim"] if t.args.input_from == "encoder" else cfg["decoder_embed_dim"]
                     dec = S2STransformerMultitaskModelBase.build_multitask_decoder(t.args, t.target_dictionary, in_dim)
-                    setattr(model, f"{name}_decoder", dec)
+                    setattr(model, f"{name}_decoder", dec.to(dev))
                     wrap = FairseqEncoderModel if t.args.decoder_type == "ctc" else FairseqMultiModel
                     model.multitask_decoders[name] = wrap(getattr(model, f"{name}_decoder"))
             return model
@@ -329,8 +329,9 @@ def register(fairseq):
                 ni = dict(sample["net_input"], return_all_hiddens=True)
                 _, extra = model(**ni)
                 cfg = model.impl.cfg
-                loss, nll = runtime.label_smoothed_ce(extra["_logits_padded"], extra["_batch"].target,
-                                                      cfg["vocab_size"], self.eps, cfg["padding_idx"])
+                tgt = sample["target"].to(extra["_logits_padded"].device).contiguous()
+                loss, nll = runtime.label_smoothed_ce(extra["_logits_padded"], tgt, cfg["vocab_size"], self.eps,
+                                                      cfg["padding_idx"])
                 ss = sample["target"].size(0) if self.sentence_avg else sample["ntokens"]
                 return loss, ss, {"loss": loss.detach(), "nll_loss": nll.detach(),
                                   "ntokens": sample["ntokens"], "nsentences": sample["target"].size(0),

@@ -702,7 +702,7 @@ def token_embed(tok, E, pos_table, B, T, D, pad, scale, p, drop):
 
 def token_embed_bwd(tok, dx, dE32, B, T, D, pad, scale, p, drop):
     seed, off = drop if p > 0 else (0, 0)
-    call("mms2ut_token_embed_bwd", tok.data_ptr(), dx.data_ptr(), dE32.data_ptr(), B, T, D, pad,
+    call("mms2ut_token_embed_bwd", tok.data_ptr(), dx.data_ptr(), dE32.data_ptr(), B, T, D, dE32.shape[0], pad,
          float(scale), float(p), seed, off, _s())
 
 

@@ -256,9 +256,9 @@ def report(r, top=12):
         lines.append(f"  argmax compared at {r.argmax_compared} / {r.argmax_positions} non-pad positions")
     if getattr(r, "relu_stats", None):
         dis, tot = sum(s[1] for s in r.relu_stats), sum(s[2] for s in r.relu_stats)
-        worst = max((s[3] / max(s[4], 1e-30) for s in r.relu_stats), default=0.0)
+        flip = max((s[3] / max(s[4], 1e-30) for s in r.relu_stats), default=0.0)
         lines.append(f"  ReLU replay: {dis} sign flips / {tot} units ({dis / max(tot, 1):.2e}); "
-                     f"largest flipped |pre-act| / mean |pre-act| = {worst:.2e}")
+                     f"largest flipped |pre-act| / mean |pre-act| = {flip:.2e}")
     lines += [f"  grad {k}: {e:.3e}" for k, e in worst]
     if r.taps:
         lines += [f"  dgrad {k}: {e:.3e}" for k, e in sorted(layer_dgrad_errors(r).items())]

@@ -101,3 +101,26 @@ def test_full_batch_training_property(mm):
     first = applied.index(True)
     after = [l for l, a in zip(losses[first + 1:], applied[first + 1:])]
     assert len(after) >= 2 and after[-1] < losses[first], (losses, applied)
+
+
+def test_training_step_bit_reproducible(mm):
+    """The whole training step is deterministic (no float atomics on the gradient path: the
+    attention backward's D = rowsum(dO*O) and the tied-embedding scatter reduce in a fixed
+    order): the same batch with the same dropout seed gives bit-identical gradients twice — the
+    property the data-parallel bucket-size invariance (scripts/_dp2_rehearsal.sh) rests on."""
+    cfg = mm.default_cfg()
+    model = mm.MMS2UTModel(cfg, device="cuda").init_params(seed=4)
+    corpus = mm.data.SyntheticSpeechMulti30K(n_utts=300, seed=9)
+    bs = corpus.batches(20000)
+    batch = mm.runtime.prepare_batch(corpus.sample(bs[len(bs) // 2]), cfg, "cuda")
+    grads = []
+    for _ in range(2):
+        model.drop.reset(77)
+        model.np_rng = type("D", (), {"random": staticmethod(lambda: 0.99)})()
+        model.params.grad.zero_()
+        logits = mm.runtime.model_logits(model, batch)
+        loss, _ = mm.runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"], 0.2, 1)
+        loss.backward(torch.tensor(8.0, device="cuda"))
+        torch.cuda.synchronize()
+        grads.append(model.params.grad.clone())
+    assert torch.equal(grads[0], grads[1])
