@@ -445,6 +445,80 @@ int mms2ut_specaugment_f16(mms2ut_half* x, const int32_t* frame_off, int B, int 
                            const int32_t* masks, int n_freq, int n_time, int use_const,
                            float mask_value, hipStream_t stream);
 
+/* ---------------------------------------------------------------- transformer layers
+ * One whole pre-LN transformer layer per call — SURVEY §8b "encoder / decoder layer fwd/bwd":
+ *   MMS_LAYER_ENC: fairseq TransformerEncoderLayer (encoder_normalize_before; A5, reached from
+ *     S2TTransformerEncoder._forward at mm_s2s_transformer.py:464):
+ *     x += drop(out_proj(MHA(LN1(x), key_len))); x += drop(fc2(drop(relu(fc1(LN3(x))))))
+ *   MMS_LAYER_DEC: fairseq TransformerDecoderLayer (decoder_normalize_before; A10, reached at
+ *     mm_s2s_transformer.py:693-696): causal self-attention block (LN1), cross-attention block
+ *     (LN2, q_proj, K|V of the encoder output precomputed for all layers, out_proj), FFN (LN3).
+ * The kernels are the ones the per-launch entries above run (GEMM epilogues, flash attention,
+ * LayerNorm), enqueued in one call: forward on `s`; backward's dgrad chain on `main` and its
+ * weight / bias / LayerNorm-parameter gradients on `side` (forked per job; side == main or NULL
+ * runs them in order on main).  Dropout: rate and counter offset per site, one seed.
+ * Buffers (the library never allocates): the forward writes what the backward needs and the
+ * layer output into `saved` (mms2ut_layer_arena: byte offsets per MMS_SLOT_*); the backward writes
+ * dx (and dropout(dx) when emit_p > 0) and every temporary into `scratch` (mms2ut_layer_scratch),
+ * which the side stream reads — keep it (and `saved`) alive until the side stream is joined.
+ * Split-K partials go to the per-stream workspaces sized by mms2ut_layer_ws.               */
+enum { MMS_LAYER_ENC = 0, MMS_LAYER_DEC = 1 };
+enum {
+  MMS_SLOT_M1 = 0, MMS_SLOT_R1, MMS_SLOT_H1, MMS_SLOT_QKV, MMS_SLOT_LSE_SA, MMS_SLOT_O, MMS_SLOT_XA,
+  MMS_SLOT_M2, MMS_SLOT_R2, MMS_SLOT_H2, MMS_SLOT_Q, MMS_SLOT_LSE_CA, MMS_SLOT_CO, MMS_SLOT_XB,
+  MMS_SLOT_M3, MMS_SLOT_R3, MMS_SLOT_H3, MMS_SLOT_F1, MMS_SLOT_OUT, MMS_LAYER_NSLOT
+};
+
+typedef struct mms2ut_layer {
+  int kind;                       /* MMS_LAYER_ENC / MMS_LAYER_DEC                               */
+  int B, T, Tk, d, H, F;          /* T: the layer's length; Tk: cross-attention keys (decoder)   */
+  float eps;
+  const int32_t* self_len;        /* [B] self-attention key lengths                              */
+  const int32_t* cross_len;       /* [B] decoder: encoder output lengths                         */
+  /* parameters ([out, in] row-major fp16) */
+  const mms2ut_half *ln1_g, *ln1_b, *w_qkv, *b_qkv, *w_o, *b_o;     /* self-attention block    */
+  const mms2ut_half *ln2_g, *ln2_b, *w_cq, *b_cq, *w_co, *b_co;     /* cross-attention block   */
+  const mms2ut_half* kv;          /* decoder: K | V of the encoder output [B*Tk] rows, ld_kv     */
+  int64_t ld_kv;
+  const mms2ut_half *ln3_g, *ln3_b, *w_fc1, *b_fc1, *w_fc2, *b_fc2; /* FFN block               */
+  /* W^T images [in, out] of the dgrad weights, or NULL (transposed reads of W) */
+  const mms2ut_half *wt_qkv, *wt_o, *wt_cq, *wt_co, *wt_fc1, *wt_fc2;
+  /* gradients (views of the flat gradient buffer); g_ln*: [gamma | beta] */
+  mms2ut_half *g_ln1, *g_w_qkv, *g_b_qkv, *g_w_o, *g_b_o;
+  mms2ut_half *g_ln2, *g_w_cq, *g_b_cq, *g_w_co, *g_b_co;
+  mms2ut_half *g_ln3, *g_w_fc1, *g_b_fc1, *g_w_fc2, *g_b_fc2;
+  /* dropout: residual / attention-probability / activation rates, counter offsets per site */
+  float p_drop, p_attn, p_act;
+  uint64_t seed;
+  uint64_t off_sa_attn, off_sa_res, off_ca_attn, off_ca_res, off_act, off_ffn_res;
+  const mms2ut_half* x;           /* layer input [B*T, d]                                        */
+  void* saved;                    /* forward arena; holds the output (MMS_SLOT_OUT)              */
+} mms2ut_layer;
+
+typedef struct mms2ut_layer_grad {
+  const mms2ut_half* dy;          /* gradient of the layer output [B*T, d]                       */
+  const mms2ut_half* dy_drop;     /* dropout(dy) with the FFN residual mask, or NULL             */
+  float emit_p;                   /* > 0: also write dropout(dx) (the layer below's residual mask) */
+  uint64_t emit_seed, emit_offset;
+  mms2ut_half* dkv;               /* decoder: gradient of this layer's K | V columns, ld_dkv     */
+  int64_t ld_dkv;
+  void* scratch;
+  float* main_ws;
+  int64_t main_ws_floats;
+  float* side_ws;
+  int64_t side_ws_floats;
+} mms2ut_layer_grad;
+
+/* arena size (and the byte offset of every MMS_SLOT_*, -1 for slots the kind does not use)     */
+int mms2ut_layer_arena(const mms2ut_layer* layer, int64_t* offsets, int64_t* bytes);
+/* backward scratch size; dx_offsets[0] = dx, [1] = dropout(dx) (-1 unless emit_p > 0)          */
+int mms2ut_layer_scratch(const mms2ut_layer* layer, float emit_p, int64_t* dx_offsets, int64_t* bytes);
+/* floats of the main-stream (split-K fixup) and side-stream (weight-gradient slabs) workspaces   */
+int mms2ut_layer_ws(const mms2ut_layer* layer, int64_t* main_floats, int64_t* side_floats);
+int mms2ut_layer_fwd(const mms2ut_layer* layer, float* main_ws, int64_t main_ws_floats, hipStream_t stream);
+int mms2ut_layer_bwd(const mms2ut_layer* layer, const mms2ut_layer_grad* grad, hipStream_t main,
+                     hipStream_t side);
+
 #ifdef __cplusplus
 }
 #endif

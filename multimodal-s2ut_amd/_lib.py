@@ -72,6 +72,35 @@ class AttnArgs(C.Structure):
 
 ATTN_ARGS = _packer(AttnArgs)
 
+LAYER_ENC, LAYER_DEC = 0, 1
+(SLOT_M1, SLOT_R1, SLOT_H1, SLOT_QKV, SLOT_LSE_SA, SLOT_O, SLOT_XA, SLOT_M2, SLOT_R2, SLOT_H2, SLOT_Q, SLOT_LSE_CA,
+ SLOT_CO, SLOT_XB, SLOT_M3, SLOT_R3, SLOT_H3, SLOT_F1, SLOT_OUT, LAYER_NSLOT) = range(20)
+
+
+class LayerArgs(C.Structure):
+    """mms2ut_layer (include/mms2ut.h): one pre-LN transformer layer."""
+    _fields_ = [("kind", i32), ("B", i32), ("T", i32), ("Tk", i32), ("d", i32), ("H", i32), ("F", i32),
+                ("eps", f32), ("self_len", vp), ("cross_len", vp)] + \
+        [(n, vp) for n in ("ln1_g", "ln1_b", "w_qkv", "b_qkv", "w_o", "b_o", "ln2_g", "ln2_b", "w_cq", "b_cq",
+                           "w_co", "b_co", "kv")] + [("ld_kv", i64)] + \
+        [(n, vp) for n in ("ln3_g", "ln3_b", "w_fc1", "b_fc1", "w_fc2", "b_fc2",
+                           "wt_qkv", "wt_o", "wt_cq", "wt_co", "wt_fc1", "wt_fc2",
+                           "g_ln1", "g_w_qkv", "g_b_qkv", "g_w_o", "g_b_o", "g_ln2", "g_w_cq", "g_b_cq",
+                           "g_w_co", "g_b_co", "g_ln3", "g_w_fc1", "g_b_fc1", "g_w_fc2", "g_b_fc2")] + \
+        [("p_drop", f32), ("p_attn", f32), ("p_act", f32), ("seed", u64)] + \
+        [(n, u64) for n in ("off_sa_attn", "off_sa_res", "off_ca_attn", "off_ca_res", "off_act", "off_ffn_res")] + \
+        [("x", vp), ("saved", vp)]
+
+
+class LayerGradArgs(C.Structure):
+    """mms2ut_layer_grad (include/mms2ut.h)."""
+    _fields_ = [("dy", vp), ("dy_drop", vp), ("emit_p", f32), ("emit_seed", u64), ("emit_offset", u64),
+                ("dkv", vp), ("ld_dkv", i64), ("scratch", vp), ("main_ws", vp), ("main_ws_floats", i64),
+                ("side_ws", vp), ("side_ws_floats", i64)]
+
+
+LAYER_GRAD_ARGS = _packer(LayerGradArgs)
+
 
 # name -> (restype, argtypes); every symbol include/mms2ut.h declares
 SIGNATURES = {
@@ -141,6 +170,11 @@ SIGNATURES = {
     "mms2ut_fbank_f32": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
     "mms2ut_fbank_cmvn_collate": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
     "mms2ut_specaugment_f16": (i32, [vp, vp, i32, i32, i32, vp, i32, i32, i32, f32, vp]),
+    "mms2ut_layer_arena": (i32, [vp, vp, vp]),
+    "mms2ut_layer_scratch": (i32, [vp, f32, vp, vp]),
+    "mms2ut_layer_ws": (i32, [vp, vp, vp]),
+    "mms2ut_layer_fwd": (i32, [vp, vp, i64, vp]),
+    "mms2ut_layer_bwd": (i32, [vp, vp, vp, vp]),
     "mms2ut_log_softmax_step": (i32, [vp, i64, i64, i32, i32, i32, i32, vp, vp]),
     "mms2ut_kv_cache_gather": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "mms2ut_decode_self_attn": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, vp, i64, i64, vp, i64, f32, vp]),

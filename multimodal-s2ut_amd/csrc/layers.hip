@@ -1,0 +1,432 @@
+// Transformer layers as single C-ABI calls: one fairseq pre-LN TransformerEncoderLayer /
+// TransformerDecoderLayer (encoder_normalize_before / decoder_normalize_before) forward, and its
+// hand-written backward with the weight gradients on a second (side) stream.
+//
+// The host used to issue these launches one by one from Python (~15 us of interpreter + ctypes
+// per launch on top of the HIP runtime's own ~4 us, ~750 launches per training step); here the
+// whole per-layer sequence is enqueued from C++ in one call.  The kernels, their arguments, the
+// dropout counters and the stream order are exactly those of the per-launch path, so results are
+// bit-identical to it (tests/test_gpu_layers.py checks that against the oracle-pinned model).
+//
+// Memory: the library still never allocates.  The forward writes every tensor the backward needs
+// (and the layer output) into a caller-owned arena whose layout mms2ut_layer_arena() returns;
+// the backward writes its temporaries (and dx) into a caller-owned scratch block
+// (mms2ut_layer_scratch()) that must stay alive until the side stream has been joined, because
+// the weight-gradient GEMMs read from it; split-K slabs live in caller-owned per-stream
+// workspaces sized by mms2ut_layer_ws().
+#include <math.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "../../include/mms2ut.h"
+
+namespace {
+
+constexpr int64_t kAlign = 256;   // bytes: every arena / scratch tensor starts 256-B aligned
+
+int64_t al(int64_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
+
+// ---------------------------------------------------------------- arena / scratch layouts
+struct Dims {
+  bool dec;
+  int64_t R, Rk, d, F, BHT, BHTk;
+};
+
+Dims dims_of(const mms2ut_layer* L) {
+  Dims D;
+  D.dec = L->kind == MMS_LAYER_DEC;
+  D.R = (int64_t)L->B * L->T;
+  D.Rk = (int64_t)L->B * L->Tk;
+  D.d = L->d;
+  D.F = L->F;
+  D.BHT = (int64_t)L->B * L->H * L->T;
+  D.BHTk = D.BHT;   // cross attention: one LSE / D row per query
+  return D;
+}
+
+// forward arena slots (bytes per slot), in layout order
+void arena_sizes(const Dims& D, int64_t* sz) {
+  const int64_t h = 2, f = 4;
+  for (int i = 0; i < MMS_LAYER_NSLOT; ++i) sz[i] = 0;
+  sz[MMS_SLOT_M1] = sz[MMS_SLOT_R1] = D.R * f;
+  sz[MMS_SLOT_H1] = D.R * D.d * h;
+  sz[MMS_SLOT_QKV] = D.R * 3 * D.d * h;
+  sz[MMS_SLOT_LSE_SA] = D.BHT * f;
+  sz[MMS_SLOT_O] = D.R * D.d * h;
+  sz[MMS_SLOT_XA] = D.R * D.d * h;
+  if (D.dec) {
+    sz[MMS_SLOT_M2] = sz[MMS_SLOT_R2] = D.R * f;
+    sz[MMS_SLOT_H2] = D.R * D.d * h;
+    sz[MMS_SLOT_Q] = D.R * D.d * h;
+    sz[MMS_SLOT_LSE_CA] = D.BHTk * f;
+    sz[MMS_SLOT_CO] = D.R * D.d * h;
+    sz[MMS_SLOT_XB] = D.R * D.d * h;
+  }
+  sz[MMS_SLOT_M3] = sz[MMS_SLOT_R3] = D.R * f;
+  sz[MMS_SLOT_H3] = D.R * D.d * h;
+  sz[MMS_SLOT_F1] = D.R * D.F * h;
+  sz[MMS_SLOT_OUT] = D.R * D.d * h;
+}
+
+int64_t layout(const int64_t* sz, int n, int64_t* off) {
+  int64_t o = 0;
+  for (int i = 0; i < n; ++i) {
+    off[i] = sz[i] ? o : -1;
+    o += al(sz[i]);
+  }
+  return o;
+}
+
+// backward scratch slots
+enum {
+  S_DX = 0, S_DXD, S_DYD, S_DF1, S_DH3, S_DX3, S_DY3B, S_DO2, S_DQ, S_DD_CA, S_DH2, S_DX2, S_DY2B,
+  S_DO, S_DQKV, S_DD_SA, S_DH1, S_P3, S_P2, S_P1, S_BPART, S_N
+};
+
+int ln_parts(int64_t R, int D) { return mms2ut_layernorm_bwd_nparts(R, D); }
+
+void scratch_sizes(const Dims& D, float emit_p, int64_t* sz) {
+  const int64_t h = 2, f = 4, Rd = D.R * D.d * h;
+  for (int i = 0; i < S_N; ++i) sz[i] = 0;
+  sz[S_DX] = Rd;
+  sz[S_DXD] = emit_p > 0.f ? Rd : 0;
+  sz[S_DYD] = Rd;
+  sz[S_DF1] = D.R * D.F * h;
+  sz[S_DH3] = Rd;
+  sz[S_DY3B] = Rd;   // dropout(dx of the FFN LN) = the residual-branch gradient of the block below
+  if (D.dec) {
+    sz[S_DX3] = Rd;
+    sz[S_DO2] = Rd;
+    sz[S_DQ] = Rd;
+    sz[S_DD_CA] = D.BHTk * f;
+    sz[S_DH2] = Rd;
+    sz[S_DY2B] = Rd;
+  }
+  sz[S_DX2] = Rd;
+  sz[S_DO] = Rd;
+  sz[S_DQKV] = D.R * 3 * D.d * h;
+  sz[S_DD_SA] = D.BHT * f;
+  sz[S_DH1] = Rd;
+  const int64_t lp = (int64_t)ln_parts(D.R, (int)D.d) * 2 * D.d * f;
+  sz[S_P3] = lp;
+  sz[S_P2] = D.dec ? lp : 0;
+  sz[S_P1] = lp;
+  // colsum partials of the bias-gradient fallback (wgrads whose shapes the fused row sums skip)
+  sz[S_BPART] = (int64_t)mms2ut_colsum_nparts(D.R) * std::max<int64_t>(3 * D.d, D.F) * f;
+}
+
+// ---------------------------------------------------------------- launch helpers
+struct Ctx {
+  hipStream_t main, side;
+  float* main_ws;
+  int64_t main_ws_floats;
+  float* side_ws;
+  int64_t side_ws_floats;
+  float* bpart;   // scratch for the bias-gradient fallback partials
+};
+
+int fixup_splits(int64_t M, int64_t N, int64_t K) {
+  // kernels.py _fixup_splits: short-M fused-epilogue GEMMs split K until ~512 workgroups run
+  if (N % 4 || K < 512) return 1;
+  const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  if (tiles >= 128) return 1;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(512 / tiles, K / 256), 16));
+}
+
+int wgrad_splits(int64_t tiles, int64_t kred) {
+  // kernels.py _splitk_for: the largest split whose tiles*s blocks fit one round of 512 slots
+  int s = (int)std::max<int64_t>(1, std::min<int64_t>(16, 512 / std::max<int64_t>(tiles, 1)));
+  while (s > 1 && kred / s < 256) --s;
+  return s;
+}
+
+mms2ut_gemm_args gemm_args() {
+  mms2ut_gemm_args a = {};
+  a.batch = 1;
+  a.bdiv = 1;
+  a.splitk = 1;
+  a.alpha = 1.f;
+  return a;
+}
+
+// C[M, N] = epi(A[M, K] @ B[N, K]^T + bias): the forward / dgrad shape (both operands
+// K-contiguous unless b_kc = 0), with the short-M split-K fixup of kernels.gemm
+int gemm_nt(const Ctx& c, const mms2ut_half* A, int64_t lda, const mms2ut_half* B, int64_t ldb, int b_kc,
+            mms2ut_half* C, int64_t ldc, int64_t M, int64_t N, int64_t K, int epi, const mms2ut_half* bias,
+            const mms2ut_half* aux, int64_t ldaux, float p, uint64_t seed, uint64_t off, int64_t ld_rng) {
+  mms2ut_gemm_args a = gemm_args();
+  a.A = A; a.B = B; a.C = C;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.a_kcontig = 1; a.b_kcontig = b_kc;
+  a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.epi = epi; a.bias = bias; a.aux = aux; a.ldaux = ldaux;
+  a.dropout_p = p; a.seed = seed; a.offset = off; a.ld_rng = ld_rng;
+  const int s = fixup_splits(M, N, K);
+  if (s > 1) {
+    MMS_REQUIRE(c.main_ws && c.main_ws_floats >= (int64_t)s * M * N, "layer: main workspace too small for a split-K fixup");
+    a.splitk = s;
+    a.splitk_ws = c.main_ws;
+    a.splitk_ws_floats = c.main_ws_floats;
+  }
+  return mms2ut_gemm_f16(&a, c.main);
+}
+
+// y = x @ W^T + b (nn.Linear) on the main stream
+int linear(const Ctx& c, const mms2ut_half* x, const mms2ut_half* W, const mms2ut_half* b, mms2ut_half* y,
+           int64_t M, int64_t N, int64_t K, int epi = MMS_EPI_F16, const mms2ut_half* aux = nullptr,
+           float p = 0.f, uint64_t seed = 0, uint64_t off = 0) {
+  return gemm_nt(c, x, K, W, K, 1, y, N, M, N, K, epi, b, aux, aux ? N : 0, p, seed, off, N);
+}
+
+// dx[M, K] = dy[M, N] @ W[N, K]: through the W^T image when there is one (both operands
+// K-contiguous), else transposed reads of W (kernels.linear_dgrad)
+int dgrad(const Ctx& c, const mms2ut_half* dy, int64_t lddy, const mms2ut_half* W, const mms2ut_half* WT,
+          mms2ut_half* dx, int64_t M, int64_t N, int64_t K, int epi = MMS_EPI_F16, const mms2ut_half* aux = nullptr,
+          float p = 0.f) {
+  if (WT) return gemm_nt(c, dy, lddy, WT, N, 1, dx, K, M, K, N, epi, nullptr, aux, aux ? K : 0, p, 0, 0, K);
+  return gemm_nt(c, dy, lddy, W, K, 0, dx, K, M, K, N, epi, nullptr, aux, aux ? K : 0, p, 0, 0, K);
+}
+
+int fork(const Ctx& c) { return c.side == c.main ? 0 : mms2ut_stream_wait(c.side, c.main); }
+
+// dW[N, K] = dy[M, N]^T @ x[M, K] and db[N] = colsum(dy), on the side stream (kernels.linear_wgrad):
+// fp32 split-K slabs with the bias partials as A-row sums, one reduction launch
+int wgrad(const Ctx& c, const mms2ut_half* dy, int64_t lddy, const mms2ut_half* x, int64_t ldx, mms2ut_half* dW,
+          mms2ut_half* db, int64_t M, int64_t N, int64_t K) {
+  int rc = fork(c);
+  if (rc) return rc;
+  const int64_t tiles = ((N + 127) / 128) * ((K + 127) / 128);
+  const int s = wgrad_splits(tiles, M);
+  const bool fused_db = db && K % 64 == 0 && N % 4 == 0;
+  const int64_t need = (int64_t)s * N * K + (db ? (int64_t)s * N : 0);
+  MMS_REQUIRE(c.side_ws && c.side_ws_floats >= need, "layer: side workspace too small (%ld < %ld floats)",
+              (long)c.side_ws_floats, (long)need);
+  float* slabs = c.side_ws;
+  float* rs = c.side_ws + (int64_t)s * N * K;
+  mms2ut_gemm_args a = gemm_args();
+  a.A = dy; a.B = x; a.C = slabs;
+  a.M = (int)N; a.N = (int)K; a.K = (int)M;
+  a.a_kcontig = 0; a.b_kcontig = 0;
+  a.lda = lddy; a.ldb = ldx; a.ldc = K;
+  a.epi = MMS_EPI_F32; a.splitk = s; a.sCsplit = N * K;
+  if (fused_db) { a.rowsum = rs; a.ld_rowsum = N; }
+  if ((rc = mms2ut_gemm_f16(&a, c.side))) return rc;
+  if (fused_db) return mms2ut_splitk_reduce_bias(slabs, s, N * K, (int)N, (int)K, dW, K, rs, db, c.side);
+  if ((rc = mms2ut_splitk_reduce(slabs, s, N * K, (int)N, (int)K, dW, K, 1, 1.f, c.side))) return rc;
+  if (!db) return 0;
+  // kernels.bias_grad: column partials of dy, then their sums
+  const int np = mms2ut_colsum_nparts(M);
+  if ((rc = mms2ut_colsum_f16(dy, M, (int)N, lddy, c.bpart, np, c.side))) return rc;
+  return mms2ut_colsum_parts(c.bpart, np, (int)N, db, 0, c.side);
+}
+
+// LayerNorm backward (+ residual gradient dres, + dropout(dx) for the sublayer below when p > 0);
+// the gamma | beta partial sums are reduced on the side stream
+int ln_bwd(const Ctx& c, const mms2ut_half* dy, const mms2ut_half* x, const mms2ut_half* g, const float* mean,
+           const float* rstd, const mms2ut_half* dres, mms2ut_half* dx, mms2ut_half* dxd, float p, uint64_t seed,
+           uint64_t off, float* part, mms2ut_half* dgb, int64_t R, int D) {
+  int rc = mms2ut_layernorm_bwd(dy, x, g, mean, rstd, dres, dx, part, R, D, p > 0.f ? dxd : nullptr, p, seed, off,
+                                c.main);
+  if (rc || (rc = fork(c))) return rc;
+  return mms2ut_colsum_parts(part, ln_parts(R, D), 2 * D, dgb, 0, c.side);
+}
+
+mms2ut_attn_args attn(const mms2ut_half* q, int64_t ldq, const mms2ut_half* k, const mms2ut_half* v, int64_t ldkv,
+                      mms2ut_half* o, int64_t ldo, int B, int H, int Tq, int Tk, int hd, const int32_t* klen, int causal,
+                      float p, uint64_t seed, uint64_t off, float* lse) {
+  mms2ut_attn_args a = {};
+  a.q = q; a.k = k; a.v = v; a.o = o;
+  a.ldq = ldq; a.ldk = ldkv; a.ldv = ldkv; a.ldo = ldo;
+  a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.hd = hd;
+  a.key_len = klen; a.causal = causal;
+  a.scale = (float)pow((double)hd, -0.5);   // float(hd ** -0.5) as the per-launch path packs it
+  a.p = p; a.seed = p > 0.f ? seed : 0; a.offset = p > 0.f ? off : 0;
+  a.lse = lse;
+  return a;
+}
+
+template <typename T>
+T* at(void* base, const int64_t* off, int slot) {
+  return off[slot] < 0 ? nullptr : reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off[slot]);
+}
+
+}  // namespace
+
+extern "C" int mms2ut_layer_arena(const mms2ut_layer* L, int64_t* offsets, int64_t* bytes) {
+  MMS_REQUIRE(L && bytes, "layer_arena: null");
+  int64_t sz[MMS_LAYER_NSLOT], off[MMS_LAYER_NSLOT];
+  arena_sizes(dims_of(L), sz);
+  *bytes = layout(sz, MMS_LAYER_NSLOT, off);
+  if (offsets) std::copy(off, off + MMS_LAYER_NSLOT, offsets);
+  return 0;
+}
+
+extern "C" int mms2ut_layer_scratch(const mms2ut_layer* L, float emit_p, int64_t* dx_offsets, int64_t* bytes) {
+  MMS_REQUIRE(L && bytes, "layer_scratch: null");
+  int64_t sz[S_N], off[S_N];
+  scratch_sizes(dims_of(L), emit_p, sz);
+  *bytes = layout(sz, S_N, off);
+  if (dx_offsets) { dx_offsets[0] = off[S_DX]; dx_offsets[1] = off[S_DXD]; }
+  return 0;
+}
+
+extern "C" int mms2ut_layer_ws(const mms2ut_layer* L, int64_t* main_floats, int64_t* side_floats) {
+  MMS_REQUIRE(L && main_floats && side_floats, "layer_ws: null");
+  const Dims D = dims_of(L);
+  int64_t mw = 0, sw = 0;
+  auto fw = [&](int64_t M, int64_t N, int64_t K) {
+    const int s = fixup_splits(M, N, K);
+    if (s > 1) mw = std::max(mw, (int64_t)s * M * N);
+  };
+  auto ww = [&](int64_t M, int64_t N, int64_t K) {
+    const int s = wgrad_splits(((N + 127) / 128) * ((K + 127) / 128), M);
+    sw = std::max(sw, (int64_t)s * N * K + (int64_t)s * N);
+  };
+  const int64_t R = D.R, d = D.d, F = D.F;
+  // forward / dgrad GEMMs (M, N, K)
+  fw(R, 3 * d, d); fw(R, d, d); fw(R, F, d); fw(R, d, F);
+  fw(R, d, 3 * d); fw(R, F, d); fw(R, d, F);
+  // weight gradients (rows M, out N, in K)
+  ww(R, 3 * d, d); ww(R, d, d); ww(R, F, d); ww(R, d, F);
+  if (D.dec) { fw(R, d, d); ww(R, d, d); }
+  *main_floats = mw;
+  *side_floats = sw;
+  return 0;
+}
+
+extern "C" int mms2ut_layer_fwd(const mms2ut_layer* L, float* main_ws, int64_t main_ws_floats, hipStream_t s) {
+  MMS_REQUIRE(L && L->x && L->saved, "layer_fwd: null layer / input / arena");
+  MMS_REQUIRE(L->kind == MMS_LAYER_ENC || L->kind == MMS_LAYER_DEC, "layer_fwd: kind %d", L->kind);
+  MMS_REQUIRE(L->H > 0 && L->d % L->H == 0 && L->d % 8 == 0 && L->F % 8 == 0, "layer_fwd: d=%d H=%d F=%d", L->d, L->H, L->F);
+  MMS_REQUIRE(L->kind != MMS_LAYER_DEC || (L->kv && L->ld_kv % 8 == 0), "layer_fwd: decoder needs kv (ld %% 8)");
+  const Dims D = dims_of(L);
+  int64_t sz[MMS_LAYER_NSLOT], off[MMS_LAYER_NSLOT];
+  arena_sizes(D, sz);
+  layout(sz, MMS_LAYER_NSLOT, off);
+  void* A = L->saved;
+  const Ctx c{s, s, main_ws, main_ws_floats, nullptr, 0, nullptr};
+  const int64_t R = D.R, d = D.d, F = D.F;
+  const int hd = L->d / L->H;
+  int rc;
+  // self-attention block: x -> LN -> q|k|v -> attention -> out_proj (+dropout +residual)
+  mms2ut_half* h1 = at<mms2ut_half>(A, off, MMS_SLOT_H1);
+  mms2ut_half* qkv = at<mms2ut_half>(A, off, MMS_SLOT_QKV);
+  mms2ut_half* O = at<mms2ut_half>(A, off, MMS_SLOT_O);
+  mms2ut_half* xa = at<mms2ut_half>(A, off, MMS_SLOT_XA);
+  if ((rc = mms2ut_layernorm_fwd(L->x, L->ln1_g, L->ln1_b, h1, at<float>(A, off, MMS_SLOT_M1),
+                                 at<float>(A, off, MMS_SLOT_R1), R, (int)d, L->eps, s))) return rc;
+  if ((rc = linear(c, h1, L->w_qkv, L->b_qkv, qkv, R, 3 * d, d))) return rc;
+  {
+    mms2ut_attn_args a = attn(qkv, 3 * d, qkv + d, qkv + 2 * d, 3 * d, O, d, L->B, L->H, L->T, L->T, hd,
+                              L->self_len, D.dec ? 1 : 0, L->p_attn, L->seed, L->off_sa_attn,
+                              at<float>(A, off, MMS_SLOT_LSE_SA));
+    if ((rc = mms2ut_mha_varlen_fwd(&a, s))) return rc;
+  }
+  if ((rc = linear(c, O, L->w_o, L->b_o, xa, R, d, d, MMS_EPI_DROP_RESID, L->x, L->p_drop, L->seed, L->off_sa_res)))
+    return rc;
+  const mms2ut_half* xf = xa;   // the FFN block's input
+  if (D.dec) {
+    // cross-attention block: LN -> q_proj -> attention over the precomputed encoder K | V -> out_proj
+    mms2ut_half* h2 = at<mms2ut_half>(A, off, MMS_SLOT_H2);
+    mms2ut_half* q = at<mms2ut_half>(A, off, MMS_SLOT_Q);
+    mms2ut_half* cO = at<mms2ut_half>(A, off, MMS_SLOT_CO);
+    mms2ut_half* xb = at<mms2ut_half>(A, off, MMS_SLOT_XB);
+    if ((rc = mms2ut_layernorm_fwd(xa, L->ln2_g, L->ln2_b, h2, at<float>(A, off, MMS_SLOT_M2),
+                                   at<float>(A, off, MMS_SLOT_R2), R, (int)d, L->eps, s))) return rc;
+    if ((rc = linear(c, h2, L->w_cq, L->b_cq, q, R, d, d))) return rc;
+    mms2ut_attn_args a = attn(q, d, L->kv, L->kv + d, L->ld_kv, cO, d, L->B, L->H, L->T, L->Tk, hd, L->cross_len, 0,
+                              L->p_attn, L->seed, L->off_ca_attn, at<float>(A, off, MMS_SLOT_LSE_CA));
+    if ((rc = mms2ut_mha_varlen_fwd(&a, s))) return rc;
+    if ((rc = linear(c, cO, L->w_co, L->b_co, xb, R, d, d, MMS_EPI_DROP_RESID, xa, L->p_drop, L->seed,
+                     L->off_ca_res))) return rc;
+    xf = xb;
+  }
+  // FFN block: LN -> fc1 (+relu +dropout) -> fc2 (+dropout +residual)
+  mms2ut_half* h3 = at<mms2ut_half>(A, off, MMS_SLOT_H3);
+  mms2ut_half* f1 = at<mms2ut_half>(A, off, MMS_SLOT_F1);
+  if ((rc = mms2ut_layernorm_fwd(xf, L->ln3_g, L->ln3_b, h3, at<float>(A, off, MMS_SLOT_M3),
+                                 at<float>(A, off, MMS_SLOT_R3), R, (int)d, L->eps, s))) return rc;
+  if ((rc = linear(c, h3, L->w_fc1, L->b_fc1, f1, R, F, d, MMS_EPI_RELU_DROP, nullptr, L->p_act, L->seed, L->off_act)))
+    return rc;
+  return linear(c, f1, L->w_fc2, L->b_fc2, at<mms2ut_half>(A, off, MMS_SLOT_OUT), R, d, F, MMS_EPI_DROP_RESID, xf,
+                L->p_drop, L->seed, L->off_ffn_res);
+}
+
+extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* G, hipStream_t main,
+                                hipStream_t side) {
+  MMS_REQUIRE(L && G && G->dy && G->scratch && L->saved, "layer_bwd: null layer / gradient / scratch / arena");
+  MMS_REQUIRE(L->kind != MMS_LAYER_DEC || G->dkv, "layer_bwd: decoder needs dkv");
+  if (!side) side = main;
+  const Dims D = dims_of(L);
+  int64_t sz[MMS_LAYER_NSLOT], off[MMS_LAYER_NSLOT], ssz[S_N], so[S_N];
+  arena_sizes(D, sz);
+  layout(sz, MMS_LAYER_NSLOT, off);
+  scratch_sizes(D, G->emit_p, ssz);
+  layout(ssz, S_N, so);
+  void* A = L->saved;
+  void* S = G->scratch;
+  const Ctx c{main, side, G->main_ws, G->main_ws_floats, G->side_ws, G->side_ws_floats, at<float>(S, so, S_BPART)};
+  const int64_t R = D.R, d = D.d, F = D.F;
+  const int hd = L->d / L->H, Dm = (int)d;
+  const float pd = L->p_drop;
+  int rc;
+  auto H_ = [&](int slot) { return at<mms2ut_half>(A, off, slot); };
+  auto F_ = [&](int slot) { return at<float>(A, off, slot); };
+  auto SH = [&](int slot) { return at<mms2ut_half>(S, so, slot); };
+  auto SF = [&](int slot) { return at<float>(S, so, slot); };
+  const mms2ut_half* xf = D.dec ? H_(MMS_SLOT_XB) : H_(MMS_SLOT_XA);
+  // ---- FFN block.  dyd = dropout(dy) with the fc2 residual mask (from the layer above, or here)
+  const mms2ut_half* dyd = G->dy_drop;
+  if (!dyd) {
+    if (pd > 0.f) {
+      if ((rc = mms2ut_dropout_fwd(G->dy, SH(S_DYD), R * d, pd, L->seed, L->off_ffn_res, main))) return rc;
+      dyd = SH(S_DYD);
+    } else {
+      dyd = G->dy;
+    }
+  }
+  if ((rc = dgrad(c, dyd, d, L->w_fc2, L->wt_fc2, SH(S_DF1), R, d, F, MMS_EPI_RELU_DROP_BWD, H_(MMS_SLOT_F1),
+                  L->p_act))) return rc;
+  if ((rc = wgrad(c, dyd, d, H_(MMS_SLOT_F1), F, L->g_w_fc2, L->g_b_fc2, R, d, F))) return rc;
+  if ((rc = dgrad(c, SH(S_DF1), F, L->w_fc1, L->wt_fc1, SH(S_DH3), R, F, d))) return rc;
+  if ((rc = wgrad(c, SH(S_DF1), F, H_(MMS_SLOT_H3), d, L->g_w_fc1, L->g_b_fc1, R, F, d))) return rc;
+  // LN3 backward: dx of the FFN input (+ the residual dy) and its dropout with the mask of the
+  // block below's residual branch (cross-attention for the decoder, self-attention for the encoder)
+  mms2ut_half* dxf = D.dec ? SH(S_DX3) : SH(S_DX2);
+  const uint64_t below_off = D.dec ? L->off_ca_res : L->off_sa_res;
+  if ((rc = ln_bwd(c, SH(S_DH3), xf, L->ln3_g, F_(MMS_SLOT_M3), F_(MMS_SLOT_R3), G->dy, dxf, SH(S_DY3B), pd, L->seed,
+                   below_off, SF(S_P3), L->g_ln3, R, Dm))) return rc;
+  const mms2ut_half* dbr = pd > 0.f ? SH(S_DY3B) : dxf;   // the block below's residual-branch gradient
+  mms2ut_half* dxa = SH(S_DX2);                            // gradient of the self-attention block output
+  if (D.dec) {
+    // ---- cross-attention block
+    if ((rc = dgrad(c, dbr, d, L->w_co, L->wt_co, SH(S_DO2), R, d, d))) return rc;
+    if ((rc = wgrad(c, dbr, d, H_(MMS_SLOT_CO), d, L->g_w_co, L->g_b_co, R, d, d))) return rc;
+    mms2ut_attn_args a = attn(H_(MMS_SLOT_Q), d, L->kv, L->kv + d, L->ld_kv, H_(MMS_SLOT_CO), d, L->B, L->H, L->T, L->Tk,
+                              hd, L->cross_len, 0, L->p_attn, L->seed, L->off_ca_attn, F_(MMS_SLOT_LSE_CA));
+    if ((rc = mms2ut_mha_varlen_bwd(&a, SH(S_DO2), d, 0, SF(S_DD_CA), SH(S_DQ), d, 0, G->dkv, G->ld_dkv, 0,
+                                    G->dkv + d, G->ld_dkv, 0, main))) return rc;
+    if ((rc = dgrad(c, SH(S_DQ), d, L->w_cq, L->wt_cq, SH(S_DH2), R, d, d))) return rc;
+    if ((rc = wgrad(c, SH(S_DQ), d, H_(MMS_SLOT_H2), d, L->g_w_cq, L->g_b_cq, R, d, d))) return rc;
+    if ((rc = ln_bwd(c, SH(S_DH2), H_(MMS_SLOT_XA), L->ln2_g, F_(MMS_SLOT_M2), F_(MMS_SLOT_R2), dxf, dxa, SH(S_DY2B),
+                     pd, L->seed, L->off_sa_res, SF(S_P2), L->g_ln2, R, Dm))) return rc;
+    dbr = pd > 0.f ? SH(S_DY2B) : dxa;
+  }
+  // ---- self-attention block
+  if ((rc = dgrad(c, dbr, d, L->w_o, L->wt_o, SH(S_DO), R, d, d))) return rc;
+  if ((rc = wgrad(c, dbr, d, H_(MMS_SLOT_O), d, L->g_w_o, L->g_b_o, R, d, d))) return rc;
+  {
+    mms2ut_half* qkv = H_(MMS_SLOT_QKV);
+    mms2ut_half* dqkv = SH(S_DQKV);
+    mms2ut_attn_args a = attn(qkv, 3 * d, qkv + d, qkv + 2 * d, 3 * d, H_(MMS_SLOT_O), d, L->B, L->H, L->T, L->T, hd,
+                              L->self_len, D.dec ? 1 : 0, L->p_attn, L->seed, L->off_sa_attn, F_(MMS_SLOT_LSE_SA));
+    if ((rc = mms2ut_mha_varlen_bwd(&a, SH(S_DO), d, 0, SF(S_DD_SA), dqkv, 3 * d, 0, dqkv + d, 3 * d, 0, dqkv + 2 * d,
+                                    3 * d, 0, main))) return rc;
+    if ((rc = dgrad(c, dqkv, 3 * d, L->w_qkv, L->wt_qkv, SH(S_DH1), R, 3 * d, d))) return rc;
+    if ((rc = wgrad(c, dqkv, 3 * d, H_(MMS_SLOT_H1), d, L->g_w_qkv, L->g_b_qkv, R, 3 * d, d))) return rc;
+  }
+  // LN1 backward: the layer input's gradient (+ dropout for the layer below when asked)
+  return ln_bwd(c, SH(S_DH1), L->x, L->ln1_g, F_(MMS_SLOT_M1), F_(MMS_SLOT_R1), dxa, SH(S_DX), SH(S_DXD), G->emit_p,
+                G->emit_seed, G->emit_offset, SF(S_P1), L->g_ln1, R, Dm);
+}

@@ -298,16 +298,149 @@ class TransposedWeights:
         self.event.record(side)
         self.waited = False
 
-    def get(self, W):
+    def get(self, W, wait=True):
         if self.event is None or W.dim() != 2:
             return None
         off = self.lookup.get(((W.data_ptr() - self.flat.data_ptr()) // 2, W.shape[0], W.shape[1]))
         if off is None or W.stride(1) != 1 or W.stride(0) != W.shape[1]:
             return None
-        if not self.waited:
+        if wait:
+            self.wait_ready()
+        return self.flatT[off:off + W.numel()].view(W.shape[1], W.shape[0])
+
+    def wait_ready(self):
+        """The current stream waits for this step's refresh (once per refresh)."""
+        if not self.waited and self.event is not None:
             torch.cuda.current_stream(self.flat.device).wait_event(self.event)
             self.waited = True
-        return self.flatT[off:off + W.numel()].view(W.shape[1], W.shape[0])
+
+
+_STREAM_WS = {}
+
+
+def stream_workspace(numel, device):
+    """fp32 scratch private to the current stream (grow-only; a regrown buffer is released to the
+    caching allocator on the stream that allocated and used it, so later reuse is stream-ordered)."""
+    if numel <= 0:
+        return None
+    key = _s()
+    buf = _STREAM_WS.get(key)
+    if buf is None or buf.numel() < numel:
+        buf = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        _STREAM_WS[key] = buf
+    return buf
+
+
+class LayerCall:
+    """One pre-LN transformer layer enqueued by a single library call (include/mms2ut.h
+    mms2ut_layer_fwd / mms2ut_layer_bwd: the whole per-layer launch sequence from C++ instead of
+    ~25 launches issued one by one from Python).  Parameter, gradient and W^T pointers are bound
+    once (the flat buffers never move); each forward sets shapes, lengths, dropout offsets and the
+    arena, and snapshots the argument block for its backward."""
+
+    _sizes = {}
+
+    def __init__(self, kind, d, H, F, params, grads, dgrad_weights, eps=1e-5):
+        a = _lib.LayerArgs()
+        a.kind, a.d, a.H, a.F, a.eps = kind, d, H, F, eps
+        for f, t in params.items():
+            setattr(a, f, t.data_ptr())
+        for f, t in grads.items():
+            setattr(a, f, t.data_ptr())
+        self.a, self.kind, self.d = a, kind, d
+        self.dgrad_weights = dgrad_weights     # {"wt_qkv": W [out, in], ...}
+        self.wt_of = None
+
+    def _bind_wt(self):
+        wt = TransposedWeights.active
+        if wt is self.wt_of:
+            return
+        for f, W in self.dgrad_weights.items():
+            img = wt.get(W, wait=False) if wt is not None else None
+            setattr(self.a, f, 0 if img is None else img.data_ptr())
+        self.wt_of = wt
+
+    def sizes(self):
+        a = self.a
+        key = (a.kind, a.B, a.T, a.Tk, a.d, a.H, a.F)
+        s = LayerCall._sizes.get(key)
+        if s is None:
+            offs = (ctypes.c_int64 * _lib.LAYER_NSLOT)()
+            nb, mw, sw = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            call("mms2ut_layer_arena", ctypes.byref(a), offs, ctypes.byref(nb))
+            call("mms2ut_layer_ws", ctypes.byref(a), ctypes.byref(mw), ctypes.byref(sw))
+            s = (nb.value, list(offs), mw.value, sw.value, {})
+            LayerCall._sizes[key] = s
+        return s
+
+    def fwd(self, x, B, T, self_len, seed, p, offs, Tk=0, cross_len=None, kv=None):
+        """p = (p_drop, p_attn, p_act); offs = the six site offsets (mms2ut_layer order).
+        Returns (arena uint8, byte offsets, argument snapshot)."""
+        a = self.a
+        a.B, a.T, a.Tk = B, T, Tk
+        a.self_len = self_len.data_ptr()
+        a.cross_len = cross_len.data_ptr() if cross_len is not None else 0
+        a.kv, a.ld_kv = (kv.data_ptr(), kv.stride(0)) if kv is not None else (0, 0)
+        a.p_drop, a.p_attn, a.p_act = p
+        a.seed = seed
+        a.off_sa_attn, a.off_sa_res, a.off_ca_attn, a.off_ca_res, a.off_act, a.off_ffn_res = offs
+        a.x = x.data_ptr()
+        self._bind_wt()
+        nb, offsets, mw, _, _ = self.sizes()
+        arena = torch.empty(nb, dtype=torch.uint8, device=x.device)
+        a.saved = arena.data_ptr()
+        ws = stream_workspace(mw, x.device)
+        call("mms2ut_layer_fwd", ctypes.byref(a), None if ws is None else ws.data_ptr(), mw, _s())
+        return arena, offsets, bytes(a)
+
+    @staticmethod
+    def view(arena, offsets, slot, shape, dtype=F16):
+        n = 1
+        for s in shape:
+            n *= s
+        o = offsets[slot]
+        return arena[o:o + n * torch.tensor([], dtype=dtype).element_size()].view(dtype).view(shape)
+
+    def bwd(self, snap, arena, dy, R, dy_drop=None, emit=None, dkv=None):
+        """Backward of the forward whose argument snapshot is ``snap``.  emit = (p, (seed, offset)):
+        also return dropout(dx) for the layer below.  Returns (dx, dropout(dx) or dx)."""
+        emit_p, (emit_seed, emit_off) = (emit[0], emit[1]) if emit is not None and emit[0] > 0 else (0.0, (0, 0))
+        nb, offsets, mw, sw, scr = self.sizes()
+        sk = emit_p > 0
+        s = scr.get(sk)
+        if s is None:
+            dxo, sb = (ctypes.c_int64 * 2)(), ctypes.c_int64()
+            call("mms2ut_layer_scratch", ctypes.byref(self.a), float(emit_p), dxo, ctypes.byref(sb))
+            s = scr[sk] = (sb.value, list(dxo))
+        sbytes, dxo = s
+        dev = dy.device
+        scratch = torch.empty(sbytes, dtype=torch.uint8, device=dev)
+        if TransposedWeights.active is not None:
+            TransposedWeights.active.wait_ready()
+        main_ws = stream_workspace(mw, dev)
+        side = 0
+        if _Side.enabled:
+            side_stream(dev)
+            side = _Side.ptr
+            with _SIDE_REGION:
+                side_ws = _workspace("layer_side", sw, dev)
+        else:
+            side_ws = _workspace("layer_side", sw, dev) if sw > 0 else None
+        g = _lib.LAYER_GRAD_ARGS.pack(
+            dy.data_ptr(), 0 if dy_drop is None else dy_drop.data_ptr(), float(emit_p), int(emit_seed),
+            int(emit_off), 0 if dkv is None else dkv.data_ptr(), 0 if dkv is None else dkv.stride(0),
+            scratch.data_ptr(), 0 if main_ws is None else main_ws.data_ptr(), mw,
+            0 if side_ws is None else side_ws.data_ptr(), sw)
+        call("mms2ut_layer_bwd", snap, g, _s(), side)
+        if side:
+            # the side stream reads the arena (saved activations) and the scratch: keep both until
+            # side_join; nothing else may reuse them before the weight gradients ran
+            _Side.keep.extend((arena, scratch))
+            _Side.used = True
+        d = self.d
+        dx = scratch[dxo[0]:dxo[0] + 2 * R * d].view(F16).view(R, d)
+        dxd = scratch[dxo[1]:dxo[1] + 2 * R * d].view(F16).view(R, d) if sk else dx
+        return dx, dxd
 
 
 def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None, mask=None):

@@ -481,6 +481,7 @@ class MMS2UTModel:
         self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
         self.wt = None  # K.TransposedWeights of the dgrad weights (built at the first training forward)
         self._wpad = {}  # subsampler conv weights zero-padded to whole 64-wide k-tiles (subsample_fwd)
+        self._layer_calls = {}  # layer prefix -> K.LayerCall (one-call transformer layers)
 
     def dgrad_weights(self):
         """Every weight matrix the hand-written backward multiplies a gradient by (dx = dy @ W),
@@ -681,8 +682,105 @@ class MMS2UTModel:
                 dcol = K.linear_dgrad(dy, W.view(W.shape[0], -1))
                 dx = K.col2im(dcol, B, L["Tin"], L["Tout"], L["C"], L["k"])
 
-    # -------------------------------------------------------------- encoder layer
+    # -------------------------------------------------------------- transformer layers (one call each)
+    def _layer_call(self, prefix, kind, d, H, F):
+        """The K.LayerCall of layer ``prefix`` (bound to its parameter / gradient / W^T slots)."""
+        lc = self._layer_calls.get(prefix)
+        if lc is not None:
+            return lc
+        P, G, span = self.P, self.G, self.params.span
+        q0, v0 = prefix + ".self_attn.q_proj", prefix + ".self_attn.v_proj"
+        params = {"ln1_g": P(prefix + ".self_attn_layer_norm.weight"), "ln1_b": P(prefix + ".self_attn_layer_norm.bias"),
+                  "w_qkv": span(q0 + ".weight", v0 + ".weight"), "b_qkv": span(q0 + ".bias", v0 + ".bias"),
+                  "w_o": P(prefix + ".self_attn.out_proj.weight"), "b_o": P(prefix + ".self_attn.out_proj.bias"),
+                  "ln3_g": P(prefix + ".final_layer_norm.weight"), "ln3_b": P(prefix + ".final_layer_norm.bias"),
+                  "w_fc1": P(prefix + ".fc1.weight"), "b_fc1": P(prefix + ".fc1.bias"),
+                  "w_fc2": P(prefix + ".fc2.weight"), "b_fc2": P(prefix + ".fc2.bias")}
+        lns = lambda n: span(n + ".weight", n + ".bias", grad=True)  # noqa: E731
+        grads = {"g_ln1": lns(prefix + ".self_attn_layer_norm"), "g_w_qkv": span(q0 + ".weight", v0 + ".weight", grad=True),
+                 "g_b_qkv": span(q0 + ".bias", v0 + ".bias", grad=True),
+                 "g_w_o": G(prefix + ".self_attn.out_proj.weight"), "g_b_o": G(prefix + ".self_attn.out_proj.bias"),
+                 "g_ln3": lns(prefix + ".final_layer_norm"), "g_w_fc1": G(prefix + ".fc1.weight"),
+                 "g_b_fc1": G(prefix + ".fc1.bias"), "g_w_fc2": G(prefix + ".fc2.weight"), "g_b_fc2": G(prefix + ".fc2.bias")}
+        wts = {"wt_qkv": span(q0 + ".weight", v0 + ".weight").view(3 * d, d), "wt_o": P(prefix + ".self_attn.out_proj.weight"),
+               "wt_fc1": P(prefix + ".fc1.weight"), "wt_fc2": P(prefix + ".fc2.weight")}
+        if kind == K._lib.LAYER_DEC:
+            e = prefix + ".encoder_attn"
+            params.update(ln2_g=P(prefix + ".encoder_attn_layer_norm.weight"), ln2_b=P(prefix + ".encoder_attn_layer_norm.bias"),
+                          w_cq=P(e + ".q_proj.weight"), b_cq=P(e + ".q_proj.bias"),
+                          w_co=P(e + ".out_proj.weight"), b_co=P(e + ".out_proj.bias"))
+            grads.update(g_ln2=lns(prefix + ".encoder_attn_layer_norm"), g_w_cq=G(e + ".q_proj.weight"),
+                         g_b_cq=G(e + ".q_proj.bias"), g_w_co=G(e + ".out_proj.weight"), g_b_co=G(e + ".out_proj.bias"))
+            wts.update(wt_cq=P(e + ".q_proj.weight"), wt_co=P(e + ".out_proj.weight"))
+        lc = K.LayerCall(kind, d, H, F, params, grads, wts)
+        self._layer_calls[prefix] = lc
+        return lc
+
     def enc_layer_fwd(self, l, x, B, T, lens32):
+        """fairseq TransformerEncoderLayer (pre-LN) forward as one library call (mms2ut_layer_fwd).
+        Dropout sites draw their counters in the per-launch order (attention, out_proj residual,
+        activation, fc2 residual), so masks are those of enc_layer_fwd_ref."""
+        cfg = self.cfg
+        d, H, F_ = cfg["encoder_embed_dim"], cfg["encoder_attention_heads"], cfg["encoder_ffn_embed_dim"]
+        R = B * T
+        pd, pa, pact = self._p("dropout"), self._p("attention_dropout"), self._p("activation_dropout")
+        c = {"x": x, "B": B, "T": T, "lens32": lens32, "pd": pd, "pa": pa, "pact": pact}
+        c["drop_attn"] = self._drop(pa, B * H * T * T)
+        c["drop1"] = self._drop(pd, R * d)
+        c["drop_act"] = self._drop(pact, R * F_)
+        c["drop2"] = self._drop(pd, R * d)
+        o = lambda dr: dr[1] if dr else 0  # noqa: E731
+        lc = self._layer_call(f"encoder.transformer_layers.{l}", K._lib.LAYER_ENC, d, H, F_)
+        arena, offs, snap = lc.fwd(x, B, T, lens32, self.drop.seed, (pd, pa, pact),
+                                   (o(c["drop_attn"]), o(c["drop1"]), 0, 0, o(c["drop_act"]), o(c["drop2"])))
+        c.update(lc=lc, arena=arena, snap=snap)
+        c["f1"] = K.LayerCall.view(arena, offs, K._lib.SLOT_F1, (R, F_))
+        return K.LayerCall.view(arena, offs, K._lib.SLOT_OUT, (R, d)), c
+
+    def enc_layer_bwd(self, l, c, dx3, dy2=None, emit=None):
+        """Backward of enc_layer_fwd (mms2ut_layer_bwd): dx3 = gradient of the layer output, dy2 =
+        dropout(dx3) with the fc2-residual mask when the layer above produced it, emit = (p, drop)
+        of the layer below's fc2 residual.  Returns (dx, masked dx or None)."""
+        dx, dxd = c["lc"].bwd(c["snap"], c["arena"], dx3, c["B"] * c["T"], dy_drop=dy2, emit=emit)
+        return dx, (dxd if emit is not None else None)
+
+    def dec_layer_fwd(self, l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None, spec=None):
+        """fairseq TransformerDecoderLayer (pre-LN) forward as one library call; the cross-attention
+        K | V are this layer's columns of the batched projection kv_all."""
+        spec = spec or self.dspec
+        if tgt_len32 is None:
+            raise NotImplementedError("decoder layers need right-padded targets (fairseq collate_tokens, left_pad=False)")
+        p = f"{spec.prefix}.layers.{l}"
+        d, H, F_ = spec.d, spec.H, spec.F
+        R = B * Tt
+        pd, pa, pact = self._sp(spec.pd), self._sp(spec.pa), self._sp(spec.pact)
+        c = {"x": x, "B": B, "Tt": Tt, "Te": Te, "pd": pd, "pa": pa, "pact": pact}
+        c["drop_sa"] = self._drop(pa, B * H * Tt * Tt)
+        c["drop1"] = self._drop(pd, R * d)
+        c["drop_ca"] = self._drop(pa, B * H * Tt * Te)
+        c["drop2"] = self._drop(pd, R * d)
+        c["drop_act"] = self._drop(pact, R * F_)
+        c["drop3"] = self._drop(pd, R * d)
+        o = lambda dr: dr[1] if dr else 0  # noqa: E731
+        lc = self._layer_call(p, K._lib.LAYER_DEC, d, H, F_)
+        kv = kv_all[:, 2 * d * l:2 * d * (l + 1)]
+        arena, offs, snap = lc.fwd(x, B, Tt, tgt_len32, self.drop.seed, (pd, pa, pact),
+                                   (o(c["drop_sa"]), o(c["drop1"]), o(c["drop_ca"]), o(c["drop2"]), o(c["drop_act"]),
+                                    o(c["drop3"])), Tk=Te, cross_len=enc_len32, kv=kv)
+        c.update(lc=lc, arena=arena, snap=snap)
+        c["f1"] = K.LayerCall.view(arena, offs, K._lib.SLOT_F1, (R, F_))
+        return K.LayerCall.view(arena, offs, K._lib.SLOT_OUT, (R, d)), c
+
+    def dec_layer_bwd(self, l, c, dx4, dkv_all, dy3=None, emit=None, spec=None):
+        """Backward of dec_layer_fwd; writes this layer's K | V gradient into its dkv_all columns."""
+        spec = spec or self.dspec
+        d = spec.d
+        dkv = dkv_all[:, 2 * d * l:2 * d * (l + 1)]
+        dx, dxd = c["lc"].bwd(c["snap"], c["arena"], dx4, c["B"] * c["Tt"], dy_drop=dy3, emit=emit, dkv=dkv)
+        return dx, (dxd if emit is not None else None)
+
+    # -------------------------------------------------------------- encoder layer (per-launch reference)
+    def enc_layer_fwd_ref(self, l, x, B, T, lens32):
         cfg = self.cfg
         p = f"encoder.transformer_layers.{l}"
         d, H = cfg["encoder_embed_dim"], cfg["encoder_attention_heads"]
@@ -723,7 +821,7 @@ class MMS2UTModel:
         c.update(B=B, T=T, lens32=lens32, pd=pd, pa=pa, pact=pact)
         return x3, c
 
-    def enc_layer_bwd(self, l, c, dx3, dy2=None, emit=None):
+    def enc_layer_bwd_ref(self, l, c, dx3, dy2=None, emit=None):
         """dx3: gradient of the layer output; dy2: dropout(dx3) with this layer's fc2-branch mask
         when the LayerNorm backward above already produced it.  emit=(p, drop) makes this
         layer's first LayerNorm backward also produce the masked gradient for the layer below.
@@ -1111,7 +1209,7 @@ class MMS2UTModel:
     def _sp(self, p):
         return p if self.training else 0.0
 
-    def dec_layer_fwd(self, l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None, spec=None):
+    def dec_layer_fwd_ref(self, l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None, spec=None):
         spec = spec or self.dspec
         p = f"{spec.prefix}.layers.{l}"
         d, H = spec.d, spec.H
@@ -1167,7 +1265,7 @@ class MMS2UTModel:
                       p=pd, drop=c["drop3"])
         return x4, c
 
-    def dec_layer_bwd(self, l, c, dx4, dkv_all, dy3=None, emit=None, spec=None):
+    def dec_layer_bwd_ref(self, l, c, dx4, dkv_all, dy3=None, emit=None, spec=None):
         """Returns (dx, masked dx for the layer below or None); writes this layer's cross-attention
         K/V gradient into its columns of dkv_all [B*Te, L_d*2d] (the K/V projection's dgrad and
         wgrad run once for all layers, decoder_backward).  dy3/emit as enc_layer_bwd's dy2/emit."""

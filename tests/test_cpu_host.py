@@ -315,3 +315,19 @@ def test_checkpoint_interchange_fairseq_layout(tmp_path):
     assert torch.equal(tr3.opt.master, model3.params.flat.float())
     assert torch.all(tr3.opt.exp_avg == 0) and torch.all(tr3.opt.exp_avg_sq == 0)
     assert tr3.completed_updates() == 11 and float(tr3.opt.ost[K.OST_LOSS_SCALE]) == 16.0
+
+
+def test_layer_arena_layout_queries():
+    """The arena / scratch / workspace size queries are consistent with the slots the model reads."""
+    K = pkg("kernels")
+    lc = K.LayerCall(K._lib.LAYER_DEC, 768, 8, 3072, {}, {}, {})
+    lc.a.B, lc.a.T, lc.a.Tk = 4, 151, 125
+    nb, offs, mw, sw, _ = lc.sizes()
+    rows = 4 * 151
+    assert offs[K._lib.SLOT_OUT] + 2 * rows * 768 <= nb and offs[K._lib.SLOT_F1] >= 0 and offs[K._lib.SLOT_XB] >= 0
+    assert all(o % 256 == 0 for o in offs if o >= 0)
+    assert mw > 0 and sw > 0          # short M: fixups on the main stream, split-K slabs on the side
+    enc = K.LayerCall(K._lib.LAYER_ENC, 768, 8, 3072, {}, {}, {})
+    enc.a.B, enc.a.T = 80, 125
+    _, eo, emw, esw, _ = enc.sizes()
+    assert eo[K._lib.SLOT_XB] == -1 and eo[K._lib.SLOT_Q] == -1 and emw == 0 and esw > 0

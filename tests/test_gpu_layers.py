@@ -1,0 +1,82 @@
+"""GPU: the one-call transformer layers (include/mms2ut.h mms2ut_layer_fwd / mms2ut_layer_bwd,
+csrc/layers.hip) are bit-identical to the per-launch path they replace (model.enc_layer_*_ref /
+dec_layer_*_ref, the kernel-by-kernel sequence the oracle parity tests pinned): logits, every
+parameter gradient and the encoder-output gradient, dropout on at every site, on the base dims
+and on a short batch whose GEMMs take the split-K fixup path.  Also checks the layers with the
+weight-gradient side stream folded into the main stream (the bench's roofline pass)."""
+import pytest
+import torch
+
+from conftest import pkg
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mm():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return pkg()
+
+
+class _Draws:
+    def random(self):
+        return 0.99
+
+
+def _step(mm, model, batch, cfg, ref):
+    M = type(model)
+    if ref:
+        model.enc_layer_fwd = M.enc_layer_fwd_ref.__get__(model)
+        model.enc_layer_bwd = M.enc_layer_bwd_ref.__get__(model)
+        model.dec_layer_fwd = M.dec_layer_fwd_ref.__get__(model)
+        model.dec_layer_bwd = M.dec_layer_bwd_ref.__get__(model)
+    else:
+        for n in ("enc_layer_fwd", "enc_layer_bwd", "dec_layer_fwd", "dec_layer_bwd"):
+            model.__dict__.pop(n, None)
+    model.drop.reset(4321)
+    model.np_rng = _Draws()
+    model.params.grad.zero_()
+    stash = {}
+    eb = model.encoder_backward
+
+    def enc_bwd(ctx, denc, dstates=None):
+        stash["denc"] = denc.clone()
+        return eb(ctx, denc, dstates)
+    model.encoder_backward = enc_bwd
+    try:
+        logits = mm.runtime.model_logits(model, batch)
+        out = logits.clone()
+        loss, _ = mm.runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"], 0.2, 1)
+        loss.backward(torch.tensor(16.0, device="cuda"))
+        torch.cuda.synchronize()
+    finally:
+        model.__dict__.pop("encoder_backward", None)
+    return out, model.params.grad.clone(), stash["denc"]
+
+
+@pytest.mark.parametrize("case", ["base", "short_fixup", "side_folded"])
+def test_layer_calls_bit_identical_to_per_launch(mm, case):
+    K = mm.kernels
+    if case == "short_fixup":
+        cfg = mm.default_cfg(encoder_layers=2, decoder_layers=2)
+        lengths, tlens = [90, 70], [25, 20]            # M = B*T of a few hundred rows: fixup splits
+    else:
+        cfg = mm.default_cfg(encoder_layers=2, decoder_layers=2)
+        lengths, tlens = [700, 640, 560, 500], [211, 193, 169, 151]
+    model = mm.MMS2UTModel(cfg, device="cuda").init_params(seed=8)
+    sample = mm.data.make_sample(lengths, tlens, img_tokens=577, img_dim=768, seed=5)
+    batch = mm.runtime.prepare_batch(sample, cfg, "cuda")
+    side = K._Side.enabled
+    if case == "side_folded":
+        K._Side.enabled = False
+    try:
+        lg_n, g_n, de_n = _step(mm, model, batch, cfg, ref=False)
+        lg_r, g_r, de_r = _step(mm, model, batch, cfg, ref=True)
+    finally:
+        K._Side.enabled = side
+    assert torch.equal(lg_n, lg_r)
+    assert torch.equal(de_n, de_r)
+    bad = [n for n, (o, _, k) in model.params.offsets.items() if not torch.equal(g_n[o:o + k], g_r[o:o + k])]
+    assert not bad, bad[:10]
+    assert float(g_n.float().norm()) > 0
