@@ -222,10 +222,6 @@ def decode_main(args):
     device = torch.device("cuda", 0)
     torch.cuda.set_device(device)
     cfg = mm.default_cfg()
-    if os.environ.get("MMS2UT_BENCH_NO_DROPOUT"):   # A/B only: what the dropout masks cost
-        for k in ("dropout", "attention_dropout", "activation_dropout", "SA_image_dropout",
-                  "SA_text_dropout", "SA_attention_dropout"):
-            cfg[k] = 0.0
     model = mm.MMS2UTModel(cfg, device=device).init_params(seed=1)
     bsz, frames, beam = args.decode_bsz, args.decode_frames, 10
     sample = data.make_sample([frames] * bsz, [10] * bsz, img_tokens=577, img_dim=768, seed=0)

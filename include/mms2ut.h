@@ -81,21 +81,6 @@ typedef struct mms2ut_gemm_args {
    * unsplit grid covers a tenth of the CUs.                                                       */
   float* splitk_ws;
   int64_t splitk_ws_floats;
-  /* in-launch split-K reduction (epi = MMS_EPI_F32, batch 1, N % 4 == 0): each split still writes
-   * its alpha-scaled fp32 slab to C, then the last split to finish a tile (per-tile arrival counter
-   * red_cnt[tiles_m*tiles_n], zero on entry and left zero on exit) sums the tile's slabs in split
-   * order -> fp16 red_out (ld_red_out), and with rowsum the bias partials -> fp16 red_bias.  The
-   * same bytes mms2ut_splitk_reduce(_bias) produces, without its launch.                         */
-  mms2ut_half* red_out;
-  int64_t ld_red_out;
-  mms2ut_half* red_bias;
-  int32_t* red_cnt;
-  /* 1-bit activity mask of a ReLU+dropout output, bit (n % 8) of byte mask[m*ld_mask + n/8] =
-   * (the stored fp16 C[m][n] > 0): MMS_EPI_RELU_DROP also writes it when mask != null (N % 8 == 0);
-   * MMS_EPI_RELU_DROP_BWD with aux == null reads it instead of the fp16 activation (1/16 of the
-   * bytes for the fc2 dgrad, bit-identical output).                                            */
-  uint8_t* mask;
-  int64_t ld_mask;
 } mms2ut_gemm_args;
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
@@ -158,9 +143,6 @@ int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler);
  * Trainer.train_step; here the per-update seed lives on the device).                           */
 int mms2ut_bind_step_seed(const uint64_t* delta);
 int mms2ut_step_seed_advance(uint64_t* delta, uint64_t inc, hipStream_t stream);
-/* new stream whose kernels may only run on the CUs whose bit is set in mask[nwords]
- * (hipExtStreamCreateWithCUMask); used for the weight-gradient side stream.                    */
-int mms2ut_stream_create_cumask(const uint32_t* mask, int nwords, hipStream_t* out);
 
 /* ---------------------------------------------------------------- LayerNorm (eps, affine)
  * Replaces fairseq LayerNorm (self_attn_layer_norm / final_layer_norm / encoder_attn_layer_norm /

@@ -36,8 +36,6 @@ class GemmArgs(C.Structure):
         ("ld_rng", i64),
         ("rowsum", vp), ("ld_rowsum", i64),
         ("splitk_ws", vp), ("splitk_ws_floats", i64),
-        ("red_out", vp), ("ld_red_out", i64), ("red_bias", vp), ("red_cnt", vp),
-        ("mask", vp), ("ld_mask", i64),
     ]
 
 
@@ -123,7 +121,6 @@ SIGNATURES = {
     "mms2ut_accum_f16_f32": (i32, [vp, vp, i64, vp]),
     "mms2ut_splitk_reduce": (i32, [vp, i32, i64, i32, i32, vp, i64, i32, f32, vp]),
     "mms2ut_splitk_reduce_bias": (i32, [vp, i32, i64, i32, i32, vp, i64, vp, vp, vp]),
-    "mms2ut_stream_create_cumask": (i32, [vp, i32, vp]),
     "mms2ut_transpose_batch": (i32, [vp, vp, vp, i32, i32, vp]),
     "mms2ut_layernorm_fwd": (i32, [vp, vp, vp, vp, vp, vp, i64, i32, f32, vp]),
     "mms2ut_layernorm_bwd": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i64, i32, vp, f32, u64, u64, vp]),

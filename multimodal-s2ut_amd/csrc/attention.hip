@@ -943,21 +943,12 @@ extern "C" int mms2ut_mha_varlen_fwd(const mms2ut_attn_args* a, hipStream_t s) {
   AttnP P = make_params(a);
   // each wave owns 16 query rows: 8 waves (128 rows) for Tq <= 128, else 16 waves (256 rows), so
   // that for every length up to 256 each (b, h) streams its K/V exactly once
-  int nw = a->Tq > 16 * ATTN_NW ? 2 * ATTN_NW : ATTN_NW;
-  {
-    // MMS2UT_ATTN_FWD_NW=4: 64 query rows per block (A/B runs)
-    const char* ne = getenv("MMS2UT_ATTN_FWD_NW");
-    if (ne && ne[0] == '4') nw = ATTN_NW / 2;
-  }
+  const int nw = a->Tq > 16 * ATTN_NW ? 2 * ATTN_NW : ATTN_NW;
   dim3 grid((a->Tq + 16 * nw - 1) / (16 * nw), a->B * a->H);
   return pick_hd(a->hd, [&](auto HDc) {
     constexpr int HD = decltype(HDc)::value;
-    const char* se = getenv("MMS2UT_ATTN_FWD_SHORT");
-    const bool short_k = a->Tk <= 2 * KB && !(se && se[0] == '0') && P.ldk < (1L << 24) && P.ldv < (1L << 24);
-    if (nw == ATTN_NW / 2) {
-      if (short_k) hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW / 2, true>), grid, dim3(32 * ATTN_NW), 0, s, P);
-      else hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW / 2>), grid, dim3(32 * ATTN_NW), 0, s, P);
-    } else if (nw == ATTN_NW) {
+    const bool short_k = a->Tk <= 2 * KB && P.ldk < (1L << 24) && P.ldv < (1L << 24);
+    if (nw == ATTN_NW) {
       if (short_k) hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW, true>), grid, dim3(64 * ATTN_NW), 0, s, P);
       else hipLaunchKernelGGL((attn_fwd_kernel<HD, ATTN_NW>), grid, dim3(64 * ATTN_NW), 0, s, P);
     } else {
@@ -982,13 +973,11 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
   P.dk = dk; P.lddk = lddk; P.sdkb = sdkb ? sdkb : (long)a->Tk * lddk;
   P.dv = dv; P.lddv = lddv; P.sdvb = sdvb ? sdvb : (long)a->Tk * lddv;
   {
-    const char* ke = getenv("MMS2UT_ATTN_KV16");
-    P.kv16 = !(ke && ke[0] == '0') && P.lddk % 8 == 0 && P.lddv % 8 == 0 && P.sdkb % 8 == 0 && P.sdvb % 8 == 0 &&
+    P.kv16 = P.lddk % 8 == 0 && P.lddv % 8 == 0 && P.sdkb % 8 == 0 && P.sdvb % 8 == 0 &&
              (a->hd % 16) == 0 && ((uintptr_t)P.dk & 15) == 0 && ((uintptr_t)P.dv & 15) == 0;
   }
   const int Z = a->B * a->H;
-  const char* fe = getenv("MMS2UT_ATTN_FUSED");
-  const bool fused_ok = !(fe && fe[0] == '0') && a->Tk <= 256 && a->hd <= 96 &&
+  const bool fused_ok = a->Tk <= 256 && a->hd <= 96 &&
                         P.ldo % 8 == 0 && P.sob % 8 == 0 && ((uintptr_t)P.o & 15) == 0 &&
                         P.lddo % 8 == 0 && P.sdob % 8 == 0 && ((uintptr_t)P.dout & 15) == 0;
   if (fused_ok) {
@@ -997,11 +986,7 @@ extern "C" int mms2ut_mha_varlen_bwd(const mms2ut_attn_args* a, const mms2ut_hal
       if constexpr (HD <= 96) {
         // persistent grid: one block per CU (the kernel's LDS allows no second), each looping
         // over heads so that the next head's loads overlap the current head's MFMA phases
-        // MMS2UT_ATTN_PERSIST=0: one block per head; =N>1: at most N blocks (tests use a small N
-        // so that every block walks several heads / chunks through the prefetch path)
-        const char* pe = getenv("MMS2UT_ATTN_PERSIST");
-        const int cap = pe ? atoi(pe) : 0;
-        const int grid = (pe && pe[0] == '0') ? Z : std::min(Z, cap > 1 ? cap : num_cus());
+        const int grid = std::min(Z, num_cus());
         if (a->Tk <= 128)
           hipLaunchKernelGGL((attn_bwd_fused_kernel<HD, 1>), dim3(grid), dim3(512), 0, s, P, Z);
         else

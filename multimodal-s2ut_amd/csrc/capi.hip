@@ -151,15 +151,3 @@ extern "C" int mms2ut_step_seed_advance(uint64_t* delta, uint64_t inc, hipStream
   return mms::check_launch("step_seed_advance");
 }
 
-// ------------------------------------------------------------------------------------------
-// A stream restricted to a subset of CUs (bit i of mask = logical CU i), for the weight-gradient
-// side stream: the dgrad chain on the main stream then keeps the remaining CUs to itself.
-// ------------------------------------------------------------------------------------------
-extern "C" int mms2ut_stream_create_cumask(const uint32_t* mask, int nwords, hipStream_t* out) {
-  MMS_REQUIRE(mask && nwords > 0 && out, "stream_create_cumask: bad arguments");
-  if (hipExtStreamCreateWithCUMask(out, (uint32_t)nwords, mask) != hipSuccess) {
-    mms::set_error("stream_create_cumask: hipExtStreamCreateWithCUMask failed");
-    return 1;
-  }
-  return 0;
-}

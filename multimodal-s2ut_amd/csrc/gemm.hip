@@ -47,9 +47,7 @@ struct GemmP {
   int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity
   float* rowsum; long ld_rowsum;  // RS kernels: split-K partial A-row sums (bias gradient)
   int group_m;  // tile-rows per L2 group (tile_coords)
-  h16* red_out; long ld_red_out; h16* red_bias; int* red_cnt;  // in-launch split-K reduction
   unsigned long long* stamps;  // profiling: per block {first, last} s_memrealtime tick, or null
-  uint8_t* mask; long ldmask;  // RELU_DROP: written when set; RELU_DROP_BWD: read when aux is null
 };
 
 // Live kernel timing (bench roofline): with P.stamps set, thread 0 of every block stores the
@@ -69,7 +67,6 @@ MMS_DEV void stamp_end(unsigned long long* stamps, unsigned long long t0) {
   }
 }
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 MMS_DEV int swz_mn(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
@@ -154,14 +151,6 @@ MMS_DEV h16x8 read_frag(const char* lds, int sub, int kk, int lane) {
   }
 }
 
-// 1-bit ReLU/dropout mask layout (ldmask = N/8 byte columns): 64-row blocks, and inside a block the
-// 8 rows m, m+8, ..., m+56 of one 8-column group in one 8-byte word, so that a lane of the staged
-// epilogue (8 columns x rows m0 + 8*pass) writes / reads its whole mask as one u64:
-//   byte(m, n) = ((m / 64) * ldmask + n / 8) * 64 + (m % 8) * 8 + (m % 64) / 8,  bit = n % 8
-MMS_DEV long mask_byte(long m, int n, long ldmask) {
-  return (((m >> 6) * ldmask + (n >> 3)) << 6) + ((m & 7) << 3) + ((m & 63) >> 3);
-}
-
 MMS_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 // torch F.gelu (approximate='none'): 0.5 z (1 + erf(z / sqrt 2)) and its derivative
 MMS_DEV float gelu_(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
@@ -237,16 +226,10 @@ MMS_DEV void epilogue_store(const GemmP& P, void* Cz, const h16* auxz, int m, in
       for (int r = 0; r < 4; ++r) if (n + r < N) g_row[n + r] = (h16)g[r];
     }
   } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
-    if (auxz) {
-      float h[4];
-      ld4(auxz + (long)m * P.ldaux, n, h);
+    float h[4];
+    ld4(auxz + (long)m * P.ldaux, n, h);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
-    } else {   // 1-bit mask: bits n%8 .. n%8+3 of byte n/8
-      const unsigned bits = (unsigned)P.mask[mask_byte(m, n, P.ldmask)] >> (n & 7);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = ((bits >> r) & 1u) ? x[r] * dscale : 0.f;
-    }
+    for (int r = 0; r < 4; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
   } else if (EPI == MMS_EPI_F16_ACC) {
     float c[4];
     ld4(C, n, c);
@@ -289,16 +272,7 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
   const int N = P.N;
   if (EPI == MMS_EPI_F32) {
     float* C = reinterpret_cast<float*>(Cz) + (long)m * P.ldc;
-    if (P.red_cnt && n + 7 < N) {
-      // slab of an in-launch split-K reduction: write-through (sc1) stores, so the reducing block on
-      // any XCD sees them after its acquire without a release (L2 write-back) in every split block
-      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(Cz, (short)0, 0x7fffffff, 0x00020000);
-      const int off = (int)(((long)m * P.ldc + n) * 4);
-      const f32x4 lo = {v[0] * P.alpha, v[1] * P.alpha, v[2] * P.alpha, v[3] * P.alpha};
-      const f32x4 hi = {v[4] * P.alpha, v[5] * P.alpha, v[6] * P.alpha, v[7] * P.alpha};
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), rc, off, 0, 16);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), rc, off + 16, 0, 16);
-    } else if (n + 7 < N) {
+    if (n + 7 < N) {
       *reinterpret_cast<f32x4*>(C + n) = f32x4{v[0] * P.alpha, v[1] * P.alpha, v[2] * P.alpha, v[3] * P.alpha};
       *reinterpret_cast<f32x4*>(C + n + 4) = f32x4{v[4] * P.alpha, v[5] * P.alpha, v[6] * P.alpha, v[7] * P.alpha};
     } else {
@@ -309,12 +283,6 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
   if (!(P.vec16 && n + 7 < N)) {
     epilogue_store<EPI>(P, Cz, auxz, m, n, f32x4{v[0], v[1], v[2], v[3]});
     epilogue_store<EPI>(P, Cz, auxz, m, n + 4, f32x4{v[4], v[5], v[6], v[7]});
-    if (EPI == MMS_EPI_RELU_DROP && P.mask) {   // from the values this thread just stored
-      const h16* C = reinterpret_cast<const h16*>(Cz) + (long)m * P.ldc;
-      unsigned b = 0;
-      for (int r = 0; r < 8; ++r) if (n + r < N && (float)C[n + r] > 0.f) b |= 1u << r;
-      P.mask[mask_byte(m, n, P.ldmask)] = (uint8_t)b;
-    }
     return;
   }
   float x[8];
@@ -365,16 +333,10 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
     for (int r = 0; r < 8; ++r) gv[r] = (h16)g[r];
     *reinterpret_cast<h16x8*>(P.out2 + (long)m * P.ldo2 + n) = gv;
   } else if (EPI == MMS_EPI_RELU_DROP_BWD) {
-    if (auxz) {
-      float h[8];
-      ld8(auxz + (long)m * P.ldaux + n, h);
+    float h[8];
+    ld8(auxz + (long)m * P.ldaux + n, h);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
-    } else {
-      const unsigned bits = P.mask[mask_byte(m, n, P.ldmask)];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) o[r] = ((bits >> r) & 1u) ? x[r] * dscale : 0.f;
-    }
+    for (int r = 0; r < 8; ++r) o[r] = h[r] > 0.f ? x[r] * dscale : 0.f;
   } else if (EPI == MMS_EPI_F16_ACC) {
     float c[8];
     ld8(C + n, c);
@@ -401,12 +363,6 @@ MMS_DEV void epilogue_store8(const GemmP& P, void* Cz, const h16* auxz, int m, i
 #pragma unroll
   for (int r = 0; r < 8; ++r) ov8[r] = (h16)o[r];
   *reinterpret_cast<h16x8*>(C + n) = ov8;
-  if (EPI == MMS_EPI_RELU_DROP && P.mask) {
-    unsigned b = 0;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) b |= ((float)ov8[r] > 0.f ? 1u : 0u) << r;
-    P.mask[mask_byte(m, n, P.ldmask)] = (uint8_t)b;
-  }
 }
 
 // Epilogue through LDS: each wave parks its 64x64 fp32 accumulator tile in 16 KiB of the (now idle)
@@ -486,14 +442,6 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
   h16* C = reinterpret_cast<h16*>(Cz);
   h16x8 ax[8], ax2[8];
   const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
-  // this lane's mask word: rows m0 + 8*pass (pass = byte), columns n..n+7 (bit); m0 % 64 < 8
-  unsigned long long* mword = nullptr;
-  unsigned long long mbits = 0;
-  // (only lanes with a valid first row: the buffer is padded to whole 64-row blocks of M)
-  if ((EPI == MMS_EPI_RELU_DROP || (EPI == MMS_EPI_RELU_DROP_BWD && !auxz)) && P.mask && m0 < P.M) {
-    mword = reinterpret_cast<unsigned long long*>(P.mask + mask_byte(m0, n, P.ldmask));
-    if (EPI == MMS_EPI_RELU_DROP_BWD) mbits = *mword;
-  }
 #pragma unroll
   for (int pass = 0; pass < 8; ++pass) {
     const int m = m0 + 8 * pass;
@@ -502,11 +450,6 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
     if (LOADS && m < P.M) {
       if (EPI == MMS_EPI_F16_ACC) {
         ax[pass] = *reinterpret_cast<const h16x8*>(C + (long)m * P.ldc + n);
-      } else if (EPI == MMS_EPI_RELU_DROP_BWD && !auxz) {
-        // 1-bit activity mask in place of the fp16 activation: expand to 1 / 0 (only > 0 is tested)
-        const unsigned bits = (unsigned)(mbits >> (8 * pass)) & 0xffu;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ax[pass][e] = (h16)(float)((bits >> e) & 1u);
       } else {
         ax[pass] = *reinterpret_cast<const h16x8*>(auxz + (long)m * P.ldaux + n);
         if (EPI == MMS_EPI_GATE) ax2[pass] = *reinterpret_cast<const h16x8*>(auxz + (long)m * P.ldaux + P.N + n);
@@ -582,16 +525,9 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[4][4
         else o = x[e];
         o8[e] = (h16)o;
       }
-      if (EPI == MMS_EPI_RELU_DROP && mword) {
-        unsigned b = 0;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) b |= ((float)o8[e] > 0.f ? 1u : 0u) << e;
-        mbits |= (unsigned long long)b << (8 * pass);
-      }
     }
     *reinterpret_cast<h16x8*>(C + (long)m * P.ldc + n) = o8;
   }
-  if (EPI == MMS_EPI_RELU_DROP && mword) *mword = mbits;   // rows past M: zero bits (never read)
 }
 
 template <bool A_KC, bool B_KC, int EPI>
@@ -705,54 +641,6 @@ MMS_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// In-launch split-K reduction (MI355X guide §5 'Projection GEMM at M = 256' item 2, write-through
-// form): every split stores its slab tile (and bias partials) with sc1 write-through stores, drains
-// them (vmcnt(0) in every wave) and takes a relaxed agent-scope ticket on the tile's counter; the
-// split drawing the last ticket acquires and sums the tile's slabs in split order (bit-identical
-// to splitk_reduce_kernel) into the fp16 output, plus the bias partials of the first tile column.
-// It leaves the counter at zero for the next launch.  (The release-fence form costs an L2
-// write-back per split block: measured 20.6 vs 18.2 ms per training step.)
-template <bool RS>
-MMS_DEV void splitk_inlaunch_reduce(const GemmP& P, char* smem, int tile, int bm, int bn, bool rs_tile) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's slab (and rowsum) stores are done
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);             // the staging ring is idle: reuse it for the flag
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(P.red_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = old == P.splitk - 1;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  const float* slab0 = reinterpret_cast<const float*>(P.C);
-  const int c = bn + 4 * (threadIdx.x & 31);
-  if (c < P.N) {
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const int m = bm + (threadIdx.x >> 5) + 8 * i;
-      if (m >= P.M) break;
-      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-      for (int k = 0; k < P.splitk; ++k)
-        sum += *reinterpret_cast<const f32x4*>(slab0 + k * P.sCsplit + (long)m * P.ldc + c);
-      *reinterpret_cast<h16x4*>(P.red_out + (long)m * P.ld_red_out + c) =
-          h16x4{(h16)sum[0], (h16)sum[1], (h16)sum[2], (h16)sum[3]};
-    }
-  }
-  if (RS && rs_tile && P.red_bias && threadIdx.x < BM) {
-    const int m = bm + threadIdx.x;
-    if (m < P.M) {
-      float sum = 0.f;
-      for (int k = 0; k < P.splitk; ++k) sum += P.rowsum[(long)k * P.ld_rowsum + m];
-      P.red_bias[m] = (h16)sum;
-    }
-  }
-  if (threadIdx.x == 0) P.red_cnt[tile] = 0;
-}
-
 template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
 __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
   const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
@@ -847,14 +735,7 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
     for (int i = 0; i < 4; ++i) {
       const int m = bm + wm * 64 + i * 16 + lane;
       if (m < P.M) {
-        const float val = rs[i][0] * P.alpha;
-        if (P.red_cnt) {   // read by the in-launch reducer: write-through, as the slab
-          const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(P.rowsum, (short)0, 0x7fffffff, 0x00020000);
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rr,
-                                                (int)(((long)zs * P.ld_rowsum + m) * 4), 0, 16);
-        } else {
-          P.rowsum[(long)zs * P.ld_rowsum + m] = val;
-        }
+        P.rowsum[(long)zs * P.ld_rowsum + m] = rs[i][0] * P.alpha;
       }
     }
   }
@@ -868,12 +749,6 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   // last k-step waited for vmcnt(0))
   __syncthreads();
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
-  if constexpr (EPI == MMS_EPI_F32) {
-    if (P.red_cnt) {
-      __syncthreads();   // every wave is past its staged-epilogue reads of the ring
-      splitk_inlaunch_reduce<RS>(P, smem, tm * tiles_n + tn, bm, bn, tn == 0);
-    }
-  }
   stamp_end(P.stamps, t_start);
 }
 
@@ -888,26 +763,6 @@ constexpr int BK32 = 32, T32_BYTES = 128 * 32 * 2, ST32 = 4;
 MMS_DEV int swz32(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1); }
 
 template <bool KC>
-MMS_DEV void dma_tile32(__amdgpu_buffer_rsrc_t rs, char* lds, long ld, int row0, int k0rel, int wid, int lane) {
-  // 8 wave-instructions per 8 KiB image: wave `wid` issues 2
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int ins = wid * 2 + i;
-    int voff;
-    if (KC) {
-      const int row = ins * 16 + (lane >> 2), slot = lane & 3;
-      const int c = slot ^ swz32(row);
-      voff = (int)(((long)(row0 + row) * ld + k0rel + c * 8) * 2);
-    } else {
-      const int kr = ins * 4 + (lane >> 4), slot = lane & 15;
-      const int c = slot ^ swz_mn(kr);
-      voff = (int)(((long)(k0rel + kr) * ld + row0 + c * 8) * 2);
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
-  }
-}
-
-template <bool KC>
 MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
   if (KC) {
     const int r = sub + (lane & 15);
@@ -916,81 +771,6 @@ MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
     return __builtin_bit_cast(h16x8, v);
   }
   return read_frag<false>(lds, sub, 0, lane);
-}
-
-template <bool A_KC, bool B_KC, int EPI>
-__global__ void __launch_bounds__(NT, 2) gemm_dma32_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
-  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
-  if (P.thresh) P.seed = mms_step_seed(P.seed);
-  __shared__ __attribute__((aligned(16))) char smem[ST32 * 2 * T32_BYTES];
-  int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
-  const int zb = z / P.splitk, zs = z % P.splitk;
-  const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
-  const int kbeg = zs * P.kchunk;
-  const int kend = min(P.K, kbeg + P.kchunk);
-  const int bm = tm * BM, bn = tn * BN;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-  const h16* Ab = P.A + z1 * P.sA1 + z2 * P.sA2 + (A_KC ? 0 : (long)kbeg * P.lda);
-  const h16* Bb = P.B + z1 * P.sB1 + z2 * P.sB2 + (B_KC ? 0 : (long)kbeg * P.ldb);
-  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2
-                          : ((long)(kend - kbeg - 1) * P.lda + ((P.M + 7) & ~7)) * 2;
-  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2
-                          : ((long)(kend - kbeg - 1) * P.ldb + ((P.N + 7) & ~7)) * 2;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)a_ext, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)b_ext, 0x00020000);
-#define SA32(s) (smem + (2 * (s)) * T32_BYTES)
-#define SB32(s) (smem + (2 * (s) + 1) * T32_BYTES)
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (kend - kbeg + BK32 - 1) / BK32;
-  auto k_rel = [&](int t, bool kc) { return kc ? kbeg + t * BK32 : t * BK32; };
-#pragma unroll
-  for (int t = 0; t < ST32 - 1; ++t) {
-    if (t < nk) {
-      dma_tile32<A_KC>(ra, SA32(t), P.lda, bm, k_rel(t, A_KC), wid, lane);
-      dma_tile32<B_KC>(rb, SB32(t), P.ldb, bn, k_rel(t, B_KC), wid, lane);
-    }
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    // k-tile kt landed once only the younger (issued later) ones are outstanding: 4 per k-tile
-    const int younger = min(ST32 - 2, nk - 1 - kt);
-    if (younger >= 2) wait_vm<8>(); else if (younger == 1) wait_vm<4>(); else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    const int nxt = kt + ST32 - 1;
-    if (nxt < nk) {
-      const int sb = nxt % ST32;
-      dma_tile32<A_KC>(ra, SA32(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
-      dma_tile32<B_KC>(rb, SB32(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
-    }
-    const int cur = kt % ST32;
-    h16x8 fa[4], fb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = read_frag32<A_KC>(SA32(cur), wm * 64 + i * 16, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = read_frag32<B_KC>(SB32(cur), wn * 64 + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-  }
-#undef SA32
-#undef SB32
-  char* Cz;
-  if (EPI == MMS_EPI_F32)
-    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
-  else
-    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
-  const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
-  __syncthreads();
-  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
-  stamp_end(P.stamps, t_start);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1024,88 +804,6 @@ MMS_DEV void dma_slot2(__amdgpu_buffer_rsrc_t rs, char* img, long ld, int row0, 
     }
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + half * T32_BYTES + hi * 1024), 16, voff, 0, 0, 0);
   }
-}
-
-template <bool A_KC, bool B_KC, int EPI>
-__global__ void __launch_bounds__(NT2, 2) gemm256_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
-  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
-  if (P.thresh) P.seed = mms_step_seed(P.seed);
-  __shared__ __attribute__((aligned(16))) char smem[RING2 * SLOT2];
-  int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
-  const int zb = z / P.splitk, zs = z % P.splitk;
-  const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
-  const int kbeg = zs * P.kchunk;
-  const int kend = min(P.K, kbeg + P.kchunk);
-  const int bm = tm * BM2, bn = tn * BN2;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const h16* Ab = P.A + z1 * P.sA1 + z2 * P.sA2 + (A_KC ? 0 : (long)kbeg * P.lda);
-  const h16* Bb = P.B + z1 * P.sB1 + z2 * P.sB2 + (B_KC ? 0 : (long)kbeg * P.ldb);
-  const long a_ext = A_KC ? ((long)(P.M - 1) * P.lda + P.K) * 2
-                          : ((long)(kend - kbeg - 1) * P.lda + ((P.M + 7) & ~7)) * 2;
-  const long b_ext = B_KC ? ((long)(P.N - 1) * P.ldb + P.K) * 2
-                          : ((long)(kend - kbeg - 1) * P.ldb + ((P.N + 7) & ~7)) * 2;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, (int)a_ext, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, (int)b_ext, 0x00020000);
-#define SLA(s) (smem + (s) * SLOT2)
-#define SLB(s) (smem + (s) * SLOT2 + 2 * T32_BYTES)
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = (kend - kbeg + BK32 - 1) / BK32;
-  auto k_rel = [&](int t, bool kc) { return kc ? kbeg + t * BK32 : t * BK32; };
-#pragma unroll
-  for (int t = 0; t < RING2 - 1; ++t) {
-    if (t < nk) {
-      dma_slot2<A_KC>(ra, SLA(t), P.lda, bm, k_rel(t, A_KC), wid, lane);
-      dma_slot2<B_KC>(rb, SLB(t), P.ldb, bn, k_rel(t, B_KC), wid, lane);
-    }
-  }
-  // this wave's A rows live in half wr of the A image, its B columns in half wc>>1 at (wc&1)*64
-  const int a_half = wr * T32_BYTES, b_half = (wc >> 1) * T32_BYTES, b_sub = (wc & 1) * 64;
-  for (int ks = 0; ks < nk; ++ks) {
-    // slot ks landed once only the younger slots' DMAs (4 instructions each) are outstanding
-    const int younger = min(RING2 - 2, nk - 1 - ks);
-    if (younger >= 2) wait_vm<8>(); else if (younger == 1) wait_vm<4>(); else wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int nxt = ks + RING2 - 1;
-    if (nxt < nk) {
-      const int sn = nxt % RING2;
-      dma_slot2<A_KC>(ra, SLA(sn), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
-      dma_slot2<B_KC>(rb, SLB(sn), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
-    }
-    const int cur = ks % RING2;
-    h16x8 fa[8], fb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = read_frag32<B_KC>(SLB(cur) + b_half, b_sub + j * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = read_frag32<A_KC>(SLA(cur) + a_half, i * 16, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-  }
-#undef SLA
-#undef SLB
-  char* Cz;
-  if (EPI == MMS_EPI_F32)
-    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2 + zs * P.sCsplit) * 4;
-  else
-    Cz = reinterpret_cast<char*>(P.C) + (z1 * P.sC1 + z2 * P.sC2) * 2;
-  const h16* auxz = P.aux ? P.aux + z1 * P.sX1 + z2 * P.sX2 : nullptr;
-  __syncthreads();
-  staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), bm + wr * 128, bn + wc * 64,
-                       0, 0, wid, lane, Cz, auxz);
-  __syncthreads();
-  staged_epilogue<EPI>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[4]), bm + wr * 128 + 64, bn + wc * 64,
-                       0, 0, wid, lane, Cz, auxz);
-  stamp_end(P.stamps, t_start);
 }
 
 // Software-pipelined form of the same tile: each 32-deep slot runs in two MFMA phases (rows
@@ -1232,73 +930,36 @@ __global__ void __launch_bounds__(NT2, 2) gemm256p_kernel(GemmP P, int tiles_m, 
   stamp_end(P.stamps, t_start);
 }
 
+#define MMS_EPI_CASES CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32) \
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
+
+// 256x256 tile, software-pipelined, 4-slot ring (the plain form and a 5-slot ring measured slower)
 template <bool A_KC, bool B_KC>
 int launch_256(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   const int total = tm * tn * nz;
   dim3 grid(total), block(NT2);
-  const char* v = getenv("MMS2UT_GEMM256");
-  const int var = v ? v[0] - '0' : 4;
-  if (var == 4 || var == 5) {
-    switch (epi) {
-#define CASE(E) case E: if (var == 4) hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, E, 4>), grid, block, 0, s, P, tm, tn, total); \
-                        else hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, E, 5>), grid, block, 0, s, P, tm, tn, total); break;
-      CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
-#undef CASE
-      default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
-    }
-    return mms::check_launch("gemm256p");
-  }
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, E>), grid, block, 0, s, P, tm, tn, total); break;
-    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
+#define CASE(E) case E: hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, E, 4>), grid, block, 0, s, P, tm, tn, total); break;
+    MMS_EPI_CASES
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
-  return mms::check_launch("gemm256");
+  return mms::check_launch("gemm256p");
 }
 
-template <bool A_KC, bool B_KC>
-int launch_dma32(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
-  const int total = tm * tn * nz;
-  dim3 grid(total), block(NT);
-  switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma32_kernel<A_KC, B_KC, E>), grid, block, 0, s, P, tm, tn, total); break;
-    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
-#undef CASE
-    default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
-  }
-  return mms::check_launch("gemm_dma32");
-}
-
+// 128x128 tile, LDS-DMA, 2 stages: 64 KiB of LDS, 2 blocks per CU (3 stages at 1 block per CU and
+// a BK = 32 four-deep ring both measured slower on the step's shapes, round-2 scripts/gemm_bench.py, git history)
 template <bool A_KC, bool B_KC>
 int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
-  const char* bk = getenv("MMS2UT_GEMM_BK");
-  if (bk && bk[0] == '3') return launch_dma32<A_KC, B_KC>(epi, P, tm, tn, nz, s);
   const int total = tm * tn * nz;
   dim3 grid(total), block(NT);
-  // 2 stages (64 KiB LDS, 2 blocks/CU) measured fastest on this step's shapes; 3 = 1 block/CU
-  const char* st = getenv("MMS2UT_DMA_STAGES");
-  if (!(st && st[0] == '3')) {
-    switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 2>), grid, block, 0, s, P, tm, tn, total); break;
-      CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-      CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
-#undef CASE
-      default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
-    }
-    return mms::check_launch("gemm_dma2");
-  }
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 3>), grid, block, 0, s, P, tm, tn, total); break;
-    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dma_kernel<A_KC, B_KC, E, 2>), grid, block, 0, s, P, tm, tn, total); break;
+    MMS_EPI_CASES
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
-  return mms::check_launch("gemm_dma");
+  return mms::check_launch("gemm_dma2");
 }
 
 template <bool A_KC, bool B_KC>
@@ -1308,8 +969,7 @@ int launch_epi(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   const size_t lds = 0;
   switch (epi) {
 #define CASE(E) case E: hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, E>), grid, block, lds, s, P, tm, tn, total); break;
-    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_F32)
-    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
+    MMS_EPI_CASES
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
@@ -1449,16 +1109,8 @@ extern "C" int mms2ut_profile_end(float* total_ms, int* launches, double* flops)
 
 static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream);
 
-// tile-rows per L2 group of the tile order (tile_coords); MMS2UT_GEMM_GROUP overrides (A/B runs)
-static int gemm_group_m() {
-  static int g = 0;
-  if (g == 0) {
-    const char* e = getenv("MMS2UT_GEMM_GROUP");
-    g = e ? atoi(e) : 8;
-    if (g < 1) g = 8;
-  }
-  return g;
-}
+// tile-rows per L2 group of the tile order (tile_coords)
+constexpr int kGroupM = 8;
 
 extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (!g_prof.on || g_prof.n >= g_prof.cap) return gemm_dispatch(a, stream);
@@ -1484,7 +1136,6 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
     const double c_bytes = (double)a->M * a->N * (a->epi == MMS_EPI_F32 ? 4.0 * (a->splitk > 0 ? a->splitk : 1) : 2.0);
     double extra = 0.0;
     if (a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_RELU_DROP_BWD || a->epi == MMS_EPI_F16_ACC) extra = 2.0 * a->M * a->N;
-    if (a->mask) extra = (double)a->M * a->N / 8.0;   // 1-bit mask written (RELU_DROP) or read instead of aux
     if (a->epi == MMS_EPI_GATE) extra = 6.0 * a->M * a->N;  // o, t read; g written
     g_prof.bytes += nb * (2.0 * ((double)a->M * a->K + (double)a->N * a->K) + c_bytes + extra);
   }
@@ -1544,12 +1195,9 @@ extern "C" int mms2ut_profile_bytes(double* bytes) {
   return 0;
 }
 
-// 256x256-tile kernel or the 128x128 one.  MMS2UT_GEMM_TILE=256 / =128 forces a choice (A/B runs).
+// 256x256-tile kernel or the 128x128 one
 static bool use_256(const mms2ut_gemm_args* a, int nz) {
-  const char* t = getenv("MMS2UT_GEMM_TILE");
-  if (t && t[0] == '2') return true;
-  if (t && t[0] == '1') return false;
-  // measured (scripts/gemm_ab.py): the 256 tile wins only with a long K and enough tiles to keep
+  // measured (round-2 A/B, scripts/gemm_ab.py in git history): the 256 tile wins only with a long K and enough tiles to keep
   // one block per CU busy (subsampler conv2, large squares); the step's K = 768 projections and
   // every N = 768 shape run faster on 128x128 tiles at two blocks per CU
   return nz == 1 && a->K >= 2048 && a->N >= 1536 && a->M >= 4096;
@@ -1582,7 +1230,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     mms2ut_gemm_args b = *a;
     b.C = a->splitk_ws; b.ldc = a->N; b.sC1 = b.sC2 = 0; b.sCsplit = (int64_t)a->M * a->N;
     b.epi = MMS_EPI_F32; b.bias = nullptr; b.aux = nullptr; b.out2 = nullptr; b.dropout_p = 0.f;
-    b.splitk_ws = nullptr; b.mask = nullptr;
+    b.splitk_ws = nullptr;
     const int rc = gemm_dispatch(&b, stream);
     if (rc) return rc;
     GemmP F{};
@@ -1591,10 +1239,9 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     F.aux = a->aux; F.ldaux = a->ldaux; F.out2 = a->out2; F.ldo2 = a->ldo2;
     F.p = a->dropout_p; F.thresh = mms_drop_thresh(a->dropout_p); F.seed = a->seed; F.offset = a->offset;
     F.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
-    F.mask = a->mask; F.ldmask = a->ld_mask;
     MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux,
                 "gemm: epilogue needs aux");
-    MMS_REQUIRE(a->epi != MMS_EPI_RELU_DROP_BWD || a->aux || a->mask, "gemm: RELU_DROP_BWD needs aux or mask");
+    MMS_REQUIRE(a->epi != MMS_EPI_RELU_DROP_BWD || a->aux, "gemm: RELU_DROP_BWD needs aux");
     MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");
     MMS_REQUIRE(a->ldc % 4 == 0 && (!a->aux || (a->ldaux % 4 == 0 && ((uintptr_t)a->aux & 7) == 0)) &&
                 (!a->bias || ((uintptr_t)a->bias & 7) == 0), "gemm: fixup operand alignment");
@@ -1617,22 +1264,10 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.out2 = a->out2; P.ldo2 = a->ldo2;
   P.p = a->dropout_p; P.thresh = mms_drop_thresh(a->dropout_p); P.seed = a->seed; P.offset = a->offset;
   P.ld_rng = a->ld_rng > 0 ? a->ld_rng : a->N;
-  P.group_m = gemm_group_m();
-  if (a->mask) {
-    MMS_REQUIRE((a->epi == MMS_EPI_RELU_DROP || a->epi == MMS_EPI_RELU_DROP_BWD) && a->batch == 1 && a->N % 8 == 0 &&
-                    a->ld_mask == a->N / 8 && ((uintptr_t)a->mask & 7) == 0,
-                "gemm: the 1-bit mask needs epi RELU_DROP(_BWD), batch 1, N %% 8 == 0, ld_mask = N/8, 8-B alignment");
-    P.mask = a->mask; P.ldmask = a->ld_mask;
-  }
-  if (a->red_cnt) {
-    MMS_REQUIRE(a->epi == MMS_EPI_F32 && a->batch == 1 && a->N % 4 == 0 && a->ldc % 4 == 0 && a->red_out &&
-                    a->ld_red_out % 4 == 0 && ((uintptr_t)a->red_out & 7) == 0 && ((uintptr_t)a->C & 15) == 0,
-                "gemm: in-launch split-K reduction needs epi F32, batch 1, N %% 4 == 0, aligned buffers");
-    P.red_out = a->red_out; P.ld_red_out = a->ld_red_out; P.red_bias = a->red_bias; P.red_cnt = a->red_cnt;
-  }
+  P.group_m = kGroupM;
   MMS_REQUIRE(!(a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP_BWD) || a->aux,
               "gemm: epilogue needs aux");
-  MMS_REQUIRE(a->epi != MMS_EPI_RELU_DROP_BWD || a->aux || a->mask, "gemm: RELU_DROP_BWD needs aux or mask");
+  MMS_REQUIRE(a->epi != MMS_EPI_RELU_DROP_BWD || a->aux, "gemm: RELU_DROP_BWD needs aux");
   MMS_REQUIRE(!(a->epi == MMS_EPI_GATE || a->epi == MMS_EPI_GELU_DROP) || a->out2, "gemm: epilogue needs out2");
   {
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
@@ -1649,10 +1284,6 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   hipStream_t s = stream;
   // LDS-DMA pipeline when every K-contiguous operand has whole 64-wide k-tiles and the operand
   // extents fit a buffer descriptor; otherwise the register-staged kernel (predicated tails)
-  // default: LDS-DMA pipeline (2 stages); MMS2UT_GEMM_PATH=reg forces the register-staged
-  // kernel for A/B measurements (scripts/gemm_bench.py)
-  const char* path_env = getenv("MMS2UT_GEMM_PATH");
-  const bool force_reg = path_env && path_env[0] == 'r';
   MMS_REQUIRE(!a->aux || (a->ldaux % 4 == 0 && ((uintptr_t)a->aux & 7) == 0), "gemm: aux must be 8-B aligned with ldaux %% 4 == 0");
   MMS_REQUIRE(!a->bias || ((uintptr_t)a->bias & 7) == 0, "gemm: bias must be 8-B aligned");
   const bool k_ok = (!a_kc || a->K % BK == 0) && (!b_kc || a->K % BK == 0);
@@ -1669,18 +1300,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     hipLaunchKernelGGL((gemm_dma_kernel<false, false, MMS_EPI_F32, 2, true>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
     return mms::check_launch("gemm_dma_rs");
   }
-  if (a->red_cnt) {
-    // the reduction lives in the 2-stage LDS-DMA kernel only: no other kernel may take this GEMM
-    MMS_REQUIRE(dma_ok, "gemm: in-launch split-K reduction needs the LDS-DMA path (K %% 64, extents)");
-    P.stamps = stamp_take((long)tm * tn * nz);
-    dim3 grid(tm * tn * nz), block(NT);
-    if (a_kc && b_kc) hipLaunchKernelGGL((gemm_dma_kernel<true, true, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
-    else if (a_kc) hipLaunchKernelGGL((gemm_dma_kernel<true, false, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
-    else if (b_kc) hipLaunchKernelGGL((gemm_dma_kernel<false, true, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
-    else hipLaunchKernelGGL((gemm_dma_kernel<false, false, MMS_EPI_F32, 2>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
-    return mms::check_launch("gemm_dma_red");
-  }
-  if (!force_reg && dma_ok) {
+  if (dma_ok) {
     if (use_256(a, nz)) {
       const int tm2 = (a->M + BM2 - 1) / BM2, tn2 = (a->N + BN2 - 1) / BN2;
       P.stamps = stamp_take((long)tm2 * tn2 * nz);

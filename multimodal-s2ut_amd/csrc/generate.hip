@@ -277,10 +277,9 @@ __global__ void __launch_bounds__(256) splitk_epilogue_ln_kernel(const float* __
 
 // BeamSearch.step's candidate selection for one step: per sentence b, the top k of
 // lprobs[b, j, v] + scores[b*beam + j] over (j, v) (only j = 0 at step 0, when every beam holds
-// the same prefix), in descending score order, ties to the lower flat index j*V + v.  One
-// 1024-thread block per sentence: each thread keeps a sorted top-k of its strided share in
-// registers (64-bit keys: order-preserving score bits | inverted index, an unrolled insertion
-// network), then k block-wide max rounds pop the heads.  Replaces torch.topk over [bsz, beam*V].
+// the same prefix), in descending score order, ties to the lower flat index j*V + v.  Keys are
+// 64-bit (order-preserving score bits | inverted index), so a max is a unique candidate.  Replaces
+// torch.topk over [bsz, beam*V].
 MMS_DEV uint64_t beam_key(float v, uint32_t idx) {
   uint32_t u = __float_as_uint(v);
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -297,61 +296,12 @@ MMS_DEV uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
-template <int KK>
-__global__ void __launch_bounds__(1024) beam_topk_kernel(const float* __restrict__ lprobs, const float* __restrict__ prev,
-                                                        long ld_prev, int beam, int V, int jmax, int k,
-                                                        float* __restrict__ out_score, int64_t* __restrict__ out_tok,
-                                                        int64_t* __restrict__ out_beam) {
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint64_t top[KK];
-#pragma unroll
-  for (int i = 0; i < KK; ++i) top[i] = 0;
-  const int n = jmax * V;
-  for (int i = tid; i < n; i += 1024) {
-    const int j = i / V, v = i - j * V;
-    float sc = lprobs[((long)b * beam + j) * V + v];
-    if (prev) sc += prev[((long)b * beam + j) * ld_prev];
-    uint64_t x = beam_key(sc, (uint32_t)i);
-    if (x > top[KK - 1]) {
-#pragma unroll
-      for (int t = 0; t < KK; ++t) {
-        const uint64_t hi = x > top[t] ? x : top[t], lo = x > top[t] ? top[t] : x;
-        top[t] = hi;
-        x = lo;
-      }
-    }
-  }
-  __shared__ uint64_t s_best[16];
-  for (int r = 0; r < k; ++r) {
-    const uint64_t m = wave_max_u64(top[0]);
-    if (lane == 0) s_best[w] = m;
-    __syncthreads();
-    uint64_t best = s_best[0];
-#pragma unroll
-    for (int q = 1; q < 16; ++q) best = s_best[q] > best ? s_best[q] : best;
-    __syncthreads();
-    if (top[0] == best && best != 0) {     // exactly one owner: flat indices are unique
-#pragma unroll
-      for (int t = 0; t < KK - 1; ++t) top[t] = top[t + 1];
-      top[KK - 1] = 0;
-    }
-    if (tid == 0) {
-      const uint32_t idx = 0xFFFFFFFFu - (uint32_t)best;
-      uint32_t u = (uint32_t)(best >> 32);
-      u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
-      out_score[(long)b * k + r] = __uint_as_float(u);
-      out_tok[(long)b * k + r] = idx % V;
-      out_beam[(long)b * k + r] = idx / V;
-    }
-  }
-}
-
-// Two-pass form of the same selection, spreading a sentence over BT_PARTS waves (the one-block
-// kernel keeps a sentence on one CU): pass 1 — each wave takes a contiguous share of the sentence's
+// Two passes, spreading a sentence over BT_PARTS waves (a one-block-per-sentence form keeps a
+// sentence on one CU and measured slower): pass 1 — each wave takes a contiguous share of the sentence's
 // candidates, keeps a per-lane register top-k and pops its own top k by k wave-max rounds into
 // part[b][p][k] (key 0 = empty); pass 2 — one wave per sentence merges the BT_PARTS*k keys the same
-// way and decodes them.  The keys are unique (flat index in the low word), so the result equals the
-// one-pass selection exactly.
+// way and decodes them.  The keys are unique (flat index in the low word), so the result equals a
+// global sort exactly.
 constexpr int BT_PARTS = 32;
 
 template <int KK>
@@ -524,16 +474,6 @@ extern "C" int mms2ut_beam_topk(const float* lprobs, const float* prev_scores, i
   if (bsz == 0) return 0;
   const float* prev = first_step ? nullptr : prev_scores;
   const int kk = k <= 8 ? 8 : k <= 16 ? 16 : k <= 24 ? 24 : 32;
-  const char* e = getenv("MMS2UT_BEAM_TOPK_1PASS");
-  if (e && e[0] == '1') {
-    switch (kk) {
-#define CASE(KK) case KK: hipLaunchKernelGGL(beam_topk_kernel<KK>, dim3(bsz), dim3(1024), 0, s, lprobs, prev, \
-                                             (long)ld_prev, beam, V, jmax, k, out_score, out_tok, out_beam); break;
-      CASE(8) CASE(16) CASE(24) CASE(32)
-#undef CASE
-    }
-    return mms::check_launch("beam_topk");
-  }
   MMS_REQUIRE(work != nullptr, "beam_topk: work buffer (bsz * 32 * k uint64) required");
   const dim3 g1((bsz * BT_PARTS + 3) / 4);
   switch (kk) {

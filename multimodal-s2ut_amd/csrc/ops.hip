@@ -903,8 +903,7 @@ int pick_cpl(int chunks_per_row, F&& f) {
 // the half-wave LayerNorm forward: D a multiple of 256 (<= 1024), 16-B aligned rows and operands
 static bool ln_fwd16_ok(const h16* x, const h16* g, const h16* b, const h16* y, int D) {
   auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  const char* e = getenv("MMS2UT_LN_FWD16");
-  return !(e && e[0] == '0') && D % 256 == 0 && D <= 1024 && al(x) && al(g) && al(b) && al(y);
+  return D % 256 == 0 && D <= 1024 && al(x) && al(g) && al(b) && al(y);
 }
 
 static int ln_fwd16_launch(const h16* x, const h16* g, const h16* b, h16* y, float* mean, float* rstd,
@@ -956,43 +955,31 @@ extern "C" int mms2ut_layernorm_fwd_ex(const h16* x, const h16* gamma, const h16
   });
 }
 
-// row pairs per wave of ln_bwd16 (D % 256 == 0): MMS2UT_LN_NP in {1, 2, 4}, default 1 — 8 rows per
-// block, twice the blocks of the 16-row layout: 18.95 vs 19.26 ms per training step over three
-// interleaved A/B pairs (scripts/ln_np_ab2.sh; the in-step LN backward shares the CUs with the
-// side-stream weight gradients, where the shorter blocks interleave better)
-static int ln16_np() {
-  const char* e = getenv("MMS2UT_LN_NP");
-  const int v = e ? atoi(e) : 1;
-  return (v == 2 || v == 4) ? v : 1;
-}
+// row pairs per wave of ln_bwd16 (D % 256 == 0): one — 8 rows per block, twice the blocks of the
+// 16-row layout: 18.95 vs 19.26 ms per training step over three interleaved A/B pairs (round 2,
+// round-2 scripts/ln_np_ab2.sh, git history; the in-step LN backward shares the CUs with the side-stream weight
+// gradients, where the shorter blocks interleave better)
+constexpr int kLnNP = 1;
 
-static bool ln16_path(int D) {
-  const char* e16 = getenv("MMS2UT_LN16");
-  return D % 256 == 0 && D <= 1024 && !(e16 && e16[0] == '0');
-}
+static bool ln16_path(int D) { return D % 256 == 0 && D <= 1024; }
 
 extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
   return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
 }
 
-// groups of 8*NP rows per ln_bwd16 block: enough blocks to fill the chip (MMS2UT_LN_BLOCKS, default
-// 1024), each folding its groups' dgamma / dbeta into one partial row — the partials (rows / 8 x 6 KB
+// groups of 8*NP rows per ln_bwd16 block: enough blocks to fill the chip (1024), each folding its
+// groups' dgamma / dbeta into one partial row — the partials (rows / 8 x 6 KB
 // at D = 768, ~35 MB for the image LayerNorm) are what colsum_parts reads back on the side stream
 static int ln16_iters(int64_t rows) {
-  static long target = 0;
-  if (target == 0) {
-    const char* e = getenv("MMS2UT_LN_BLOCKS");
-    target = e ? atol(e) : 1024;
-    if (target < 1) target = 1024;
-  }
-  const long groups = (rows + 8 * ln16_np() - 1) / (8 * ln16_np());
+  constexpr long target = 1024;
+  const long groups = (rows + 8 * kLnNP - 1) / (8 * kLnNP);
   const long it = (groups + target - 1) / target;
   return (int)(it > 1 ? it : 1);
 }
 
 extern "C" int mms2ut_layernorm_bwd_nparts(int64_t rows, int D) {
   if (!ln16_path(D)) return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
-  const long rpb = 8L * ln16_np() * ln16_iters(rows);
+  const long rpb = 8L * kLnNP * ln16_iters(rows);
   return (int)((rows + rpb - 1) / rpb);
 }
 
@@ -1007,13 +994,11 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
   if (rows == 0) return 0;
   const int nb = mms2ut_layernorm_bwd_nparts(rows, D);
   if (ln16_path(D)) {
-    const int np = ln16_np();
 #define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
                                           gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
                                           offset, 0L, 0L, 0.f, 0u, (uint64_t)0, (uint64_t)0, ln16_iters(rows)); break;
-    switch ((D / 256) * 8 + np) {
-      CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1) CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
-      CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
+    switch ((D / 256) * 8 + kLnNP) {
+      CASE(1, kLnNP) CASE(2, kLnNP) CASE(3, kLnNP) CASE(4, kLnNP)
     }
 #undef CASE
     return mms::check_launch("layernorm_bwd16");
@@ -1041,17 +1026,14 @@ extern "C" int mms2ut_layernorm_bwd_ex(const h16* dy, const h16* x, const h16* g
   MMS_REQUIRE(D % 256 == 0 && D <= 1024, "layernorm_bwd_ex: D must be a multiple of 256 and <= 1024");
   MMS_REQUIRE(dy_grp >= 0 && (dy_grp == 0 || dy_grp_out >= dy_grp), "layernorm_bwd_ex: need dy_grp_out >= dy_grp");
   if (rows == 0) return 0;
-  MMS_REQUIRE(ln16_path(D), "layernorm_bwd_ex: the 16-B path is disabled (MMS2UT_LN16=0)");
   const int nb = mms2ut_layernorm_bwd_nparts(rows, D);
   const uint32_t thresh = mms_drop_thresh(p), thin = mms_drop_thresh(dy_p);
-  const int np = ln16_np();
 #define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
                                           gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
                                           offset, (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset, \
                                           ln16_iters(rows)); break;
-  switch ((D / 256) * 8 + np) {
-    CASE(1, 1) CASE(2, 1) CASE(3, 1) CASE(4, 1) CASE(1, 2) CASE(2, 2) CASE(3, 2) CASE(4, 2)
-    CASE(1, 4) CASE(2, 4) CASE(3, 4) CASE(4, 4)
+  switch ((D / 256) * 8 + kLnNP) {
+    CASE(1, kLnNP) CASE(2, kLnNP) CASE(3, kLnNP) CASE(4, kLnNP)
   }
 #undef CASE
   return mms::check_launch("layernorm_bwd_ex");

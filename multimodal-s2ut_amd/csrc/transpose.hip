@@ -1,5 +1,5 @@
 // Batched fp16 matrix transpose: the weight images W^T that let every dgrad GEMM read both
-// operands K-contiguous (ds_read_b128 fragments instead of transposed reads; scripts/gemm_ab.py:
+// operands K-contiguous (ds_read_b128 fragments instead of transposed reads; round-2 A/B, scripts/gemm_ab.py in git history:
 // 13-20 % faster on the step's dgrad shapes).  One launch refreshes every registered matrix after
 // each optimizer update; it runs on the side stream beside the next forward.
 //

@@ -5,7 +5,6 @@ Tensors are fp16 (``torch.float16``) unless stated; shapes are checked before th
 """
 import ctypes
 import math
-import os
 
 import torch
 
@@ -64,85 +63,26 @@ class Dropout:
 def gemm(A, B, C, M, N, K, *, a_kc=True, b_kc=True, lda, ldb, ldc, batch=1, bdiv=1,
          sA=(0, 0), sB=(0, 0), sC=(0, 0), epi=EPI_F16, alpha=1.0, bias=None, aux=None, ldaux=0,
          sX=(0, 0), out2=None, ldo2=0, p=0.0, seed=0, offset=0, ld_rng=0, splitk=1, sCsplit=0,
-         rowsum=None, ld_rowsum=0, red_out=None, red_bias=None, red_cnt=None, mask=None):
+         rowsum=None, ld_rowsum=0, fixup=True):
     """One mms2ut_gemm_f16 launch.  The argument block is packed in one struct call (_lib.GEMM_ARGS,
-    the C layout of mms2ut_gemm_args): this runs a few hundred times per training step."""
+    the C layout of mms2ut_gemm_args).  Short-M fused-epilogue GEMMs take the split-K fixup
+    (fixup=False: the unsplit kernel, for tests)."""
     ws_p = ws_n = 0
-    tail = 0
-    if splitk == 1 and epi != EPI_F32 and batch == 1 and rowsum is None and _SPLITK_FIX:
+    if fixup and splitk == 1 and epi != EPI_F32 and batch == 1 and rowsum is None:
         s = _fixup_splits(M, N, K)
         if s > 1:
             ws = _workspace("splitk_fix", s * M * N, C.device)
             splitk, ws_p, ws_n = s, ws.data_ptr(), ws.numel()
-        elif _TAIL_SPLIT:
-            tail = _tail_split_rows(M, N, K)
-    red_p = ld_red = red_b = red_c = 0
-    if red_cnt is not None:
-        red_p, ld_red = red_out.data_ptr(), red_out.stride(0)
-        red_b, red_c = (0 if red_bias is None else red_bias.data_ptr()), red_cnt.data_ptr()
-    mask_p = ld_mask = 0
-    if mask is not None:   # 1-bit ReLU/dropout activity mask (relu_mask_alloc), written or read
-        assert mask.dtype == torch.uint8 and mask.shape[0] >= (M + 63) // 64 * 64 and mask.stride(1) == 1
-        mask_p, ld_mask = mask.data_ptr(), mask.stride(0)
     buf = _GEMM_PACK(
         A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, a_kc, b_kc, lda, ldb, ldc, batch, bdiv,
         sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], splitk, sCsplit, epi, alpha,
         0 if bias is None else bias.data_ptr(), 0 if aux is None else aux.data_ptr(), ldaux, sX[0], sX[1],
         0 if out2 is None else out2.data_ptr(), ldo2, p, seed, offset, ld_rng,
-        0 if rowsum is None else rowsum.data_ptr(), ld_rowsum, ws_p, ws_n, red_p, ld_red, red_b, red_c,
-        mask_p, ld_mask)
-    if tail:
-        return _gemm_tail_split(GemmArgs.from_buffer_copy(buf), tail, C.device)
+        0 if rowsum is None else rowsum.data_ptr(), ld_rowsum, ws_p, ws_n)
     call("mms2ut_gemm_f16", buf, _s())
 
 
 _GEMM_PACK = _lib.GEMM_ARGS.pack
-_SPLITK_FIX = os.environ.get("MMS2UT_SPLITK_FIX", "1") != "0"
-# Tail split (below) measured slower in the training step (19.03 vs 18.46 ms over three interleaved
-# pairs) although faster in isolation: opt-in, MMS2UT_GEMM_TAILSPLIT=1.
-_TAIL_SPLIT = os.environ.get("MMS2UT_GEMM_TAILSPLIT", "0") == "1"
-_SLOTS = 512      # 128x128 blocks resident at once: 2 per CU x 256 CUs
-
-
-def _tail_split_rows(M, N, K):
-    """Rows of a fused-epilogue 128x128 GEMM whose grid overflows the 512 block slots by at most a
-    quarter round: the head (whole rounds of row tiles) runs as usual and the tail rows run split-K
-    with the fixup, instead of a nearly empty last round of lone, latency-bound tiles (M = 11000,
-    N = 768, K = 768: 516 tiles take 31.7 us against 18 us for 474).  0 = no split.  The 256x256
-    kernel's shapes (gemm.hip use_256) are left alone."""
-    if K < 512 or N % 4 or (K >= 2048 and N >= 1536 and M >= 4096):
-        return 0
-    tn = (N + 127) // 128
-    tiles = ((M + 127) // 128) * tn
-    if tiles <= _SLOTS:
-        return 0
-    head_rows = ((tiles // _SLOTS) * _SLOTS // tn)        # whole row tiles in the full rounds
-    if tiles - head_rows * tn > _SLOTS // 4:
-        return 0
-    return head_rows * 128
-
-
-def _gemm_tail_split(a, M1, device):
-    """Launch rows [0, M1) of the GEMM described by ``a`` as is, rows [M1, M) split-K + fixup.  The
-    tail's operand / output pointers move by M1 rows and its dropout counters by M1 * ld_rng, so
-    every element keeps its counter (masks identical to the single launch)."""
-    M = a.M
-    t = GemmArgs.from_buffer_copy(a)
-    a.M = M1
-    call("mms2ut_gemm_f16", ctypes.byref(a), _s())
-    M2 = M - M1
-    t.M = M2
-    t.A = a.A + 2 * M1 * (a.lda if a.a_kcontig else 1)
-    t.C = a.C + 2 * M1 * a.ldc
-    if a.aux:
-        t.aux = a.aux + 2 * M1 * a.ldaux
-    if a.out2:
-        t.out2 = a.out2 + 2 * M1 * a.ldo2
-    t.offset = a.offset + M1 * (a.ld_rng if a.ld_rng > 0 else a.N)
-    s = max(2, _fixup_splits(M2, a.N, a.K))
-    ws = _workspace("splitk_fix", s * M2 * a.N, device)
-    t.splitk, t.splitk_ws, t.splitk_ws_floats = s, ws.data_ptr(), ws.numel()
-    call("mms2ut_gemm_f16", ctypes.byref(t), _s())
 
 
 def _fixup_splits(M, N, K):
@@ -215,26 +155,9 @@ def gemm_profile_durations(buf, n):
     return out
 
 
-def relu_mask_alloc(M, N, device):
-    """Buffer of the 1-bit ReLU/dropout activity mask of an [M, N] output (N % 8 == 0): N/8 byte
-    columns, rows padded to 64 (gemm.hip mask_byte: 64-row blocks, 8 rows of one column group per
-    8-byte word)."""
-    return torch.empty((M + 63) // 64 * 64, N // 8, dtype=torch.uint8, device=device)
-
-
-def relu_mask_unpack(mask, M, N):
-    """bool [M, N] from a relu_mask_alloc buffer (tests)."""
-    ld = N // 8
-    b = mask.reshape(-1, ld, 8, 8)                  # [m/64][n/8][m%8][(m%64)/8]
-    b = b.permute(0, 3, 2, 1).reshape(-1, ld)[:M]    # rows m = 64*blk + 8*(m%64/8) + m%8
-    bits = torch.stack([(b >> i) & 1 for i in range(8)], dim=-1)
-    return bits.reshape(M, N).bool()
-
-
 def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0, drop=None,
-           ldc=None, alpha=1.0, mask=None):
-    """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue).
-    mask: uint8 [M, N/8] written with EPI_RELU_DROP (bit n%8 of byte n/8 = out[m, n] > 0)."""
+           ldc=None, alpha=1.0):
+    """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias) — nn.Linear forward (fused epilogue)."""
     M, K = x.shape
     N = W.shape[0]
     assert W.shape[1] == K, (W.shape, x.shape)
@@ -246,7 +169,7 @@ def linear(x, W, bias=None, out=None, *, epi=EPI_F16, aux=None, out2=None, p=0.0
     gemm(x, W, out, M, N, K, lda=x.stride(0), ldb=W.stride(0), ldc=ldc or out.stride(0), epi=epi,
          bias=bias, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), out2=out2,
          ldo2=(out2.stride(0) if out2 is not None else 0), p=p, seed=seed, offset=off, ld_rng=N,
-         alpha=alpha, mask=mask)
+         alpha=alpha)
     return out
 
 
@@ -255,7 +178,7 @@ class TransposedWeights:
 
     dx = dy @ W reads W [N, K] N-contiguous (transposed LDS reads); with W^T [K, N] both GEMM
     operands are K-contiguous, the NT layout the forward uses (13-20 % faster on the step's dgrad
-    shapes, scripts/gemm_ab.py).  refresh() re-transposes every registered matrix in one launch on
+    shapes, round-2 A/B, scripts/gemm_ab.py in git history).  refresh() re-transposes every registered matrix in one launch on
     the side stream after each optimizer update (it runs beside the forward); the first dgrad of
     the backward makes the main stream wait for it.  linear_dgrad picks the image up by W's
     address and shape; unregistered weights keep the transposed-read path."""
@@ -443,11 +366,10 @@ class LayerCall:
         return dx, dxd
 
 
-def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None, mask=None):
+def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None):
     """dx[M,K] = dy[M,N] @ W[N,K]  (W row-major, reduction over N).  Reads the W^T image when one
     is registered (TransposedWeights), else W itself through transposed fragment reads.
-    drop=(seed, offset): the forward dropout mask of the [M, K] output (EPI_GELU_DROP_BWD).
-    mask: EPI_RELU_DROP_BWD reads the forward's 1-bit activity mask instead of aux."""
+    drop=(seed, offset): the forward dropout mask of the [M, K] output (EPI_GELU_DROP_BWD)."""
     M, N = dy.shape
     K = W.shape[1]
     if out is None:
@@ -459,27 +381,22 @@ def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=Fa
     if WT is not None:
         gemm(dy, WT, out, M, K, N, a_kc=True, b_kc=True, lda=dy.stride(0), ldb=WT.stride(0),
              ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p,
-             seed=seed, offset=off, ld_rng=K, mask=mask)
+             seed=seed, offset=off, ld_rng=K)
         return out
     gemm(dy, W, out, M, K, N, a_kc=True, b_kc=False, lda=dy.stride(0), ldb=W.stride(0),
          ldc=out.stride(0), epi=epi, aux=aux, ldaux=(aux.stride(0) if aux is not None else 0), p=p,
-         seed=seed, offset=off, ld_rng=K, mask=mask)
+         seed=seed, offset=off, ld_rng=K)
     return out
-
-
-_WGRAD_SPLITK_CAP = int(os.environ.get("MMS2UT_WGRAD_SPLITK", "16"))
-_WGRAD_SLOTS = os.environ.get("MMS2UT_WGRAD_SLOTS")
 
 
 def _splitk_for(tiles, kred, slots=512):
     """split-K count for a weight gradient (reduction over kred token rows): the largest s whose
     tiles*s blocks still fit one round of the 512 block slots (2 per CU), so every block runs
-    concurrently and no partial second round trails (scripts/wgrad_sweep.py, isolated GEMM +
+    concurrently and no partial second round trails (round-2 scripts/wgrad_sweep.py, git history, isolated GEMM +
     slab reduction on the step's shapes: fc 3072x768 s3 vs the old fixed s8, qkv 2304x768 s4
-    49 vs 60 us, cross-KV 9216x768 s1 174 vs 234 us).  MMS2UT_WGRAD_SPLITK caps s."""
-    cap = _WGRAD_SPLITK_CAP
-    slots = int(_WGRAD_SLOTS) if _WGRAD_SLOTS else slots
-    s = max(1, min(cap, slots // max(tiles, 1)))
+    49 vs 60 us, cross-KV 9216x768 s1 174 vs 234 us; the 512-slot budget re-checked against
+    256 / 1024 in round 2, profiles/round2_v3_wgrad_split_ab.txt).  Same rule as csrc/layers.hip."""
+    s = max(1, min(16, slots // max(tiles, 1)))
     while s > 1 and kred // s < 256:
         s -= 1
     return s
@@ -497,8 +414,7 @@ class _Side:
     lives in persistent per-stream workspaces (the side stream serialises its own reuse)."""
     stream = None      # torch.cuda.Stream (RCCL buckets are enqueued on it, parallel.py)
     ptr = 0
-    enabled = os.environ.get("MMS2UT_SIDE", "1") != "0"
-    wgrad_nosplit = os.environ.get("MMS2UT_WGRAD_SPLIT", "1") == "0"
+    enabled = True     # False: side jobs run in order on the current stream (bench roofline pass)
     used = False
     override = 0
     keep = []
@@ -523,23 +439,9 @@ _SIDE_REGION = _SideRegion()
 
 
 def make_side_stream(device):
-    """The weight-gradient side stream: lowest priority; with MMS2UT_SIDE_CUS=stride:K (every K-th
-    CU) or block:K (the first 1/K of the CUs) it is also confined to that CU subset."""
-    spec = os.environ.get("MMS2UT_SIDE_CUS", "")
-    if not spec:
-        return torch.cuda.Stream(device=device, priority=100)
-    import ctypes
-    kind, k = spec.split(":")
-    k = int(k)
-    n = torch.cuda.get_device_properties(device).multi_processor_count
-    on = [(i % k == 0) if kind == "stride" else (i < n // k) for i in range(n)]
-    words = (ctypes.c_uint32 * ((n + 31) // 32))()
-    for i, b in enumerate(on):
-        if b:
-            words[i // 32] |= 1 << (i % 32)
-    h = ctypes.c_void_p()
-    call("mms2ut_stream_create_cumask", ctypes.addressof(words), len(words), ctypes.addressof(h))
-    return torch.cuda.ExternalStream(h.value, device=device)
+    """The weight-gradient side stream: lowest priority, so the hardware dispatcher prefers the
+    critical path's workgroups (a CU-masked variant measured 5 % slower, round 1)."""
+    return torch.cuda.Stream(device=device, priority=100)
 
 
 def side_stream(device):
@@ -569,27 +471,6 @@ def side_join():
         call("mms2ut_stream_wait", torch._C._cuda_getCurrentRawStream(_dev()), _Side.ptr)
         _Side.used = False
         _Side.keep.clear()
-
-
-# In-launch split-K reduction of the weight gradients (gemm.hip splitk_inlaunch_reduce): bit-identical
-# to the splitk_reduce launch, but measured slower in the training step (19.6 vs 18.2 ms: the last
-# split of a tile reads 3-4 x 64 KiB of slabs serially while the side stream holds few CUs), so it
-# is opt-in (MMS2UT_WGRAD_INLAUNCH=1).
-_INLAUNCH_RED = os.environ.get("MMS2UT_WGRAD_INLAUNCH", "0") == "1"
-_RED_CNT = {}
-_RED_CNT_CAP = 1 << 16
-
-
-def _red_counters(device):
-    """Per-stream tile-arrival counters of the in-launch split-K reduction: zero-initialised once,
-    every launch leaves them at zero (the last split of a tile resets its counter).  Kernels on one
-    stream serialise, so one buffer per stream suffices."""
-    key = _s()
-    buf = _RED_CNT.get(key)
-    if buf is None:
-        buf = torch.zeros(_RED_CNT_CAP, dtype=torch.int32, device=device)
-        _RED_CNT[key] = buf
-    return buf
 
 
 def _workspace(key, numel, device, dtype=torch.float32):
@@ -625,28 +506,15 @@ def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
     M, N = dy.shape
     K = x.shape[1]
     assert dW is None or tuple(dW.shape) == (N, K)
-    if db is not None and (accumulate_f32 is not None or _Side.wgrad_nosplit or K % 64 or N % 4):
+    if db is not None and (accumulate_f32 is not None or K % 64 or N % 4):
         linear_wgrad(dy, x, dW, accumulate_f32=accumulate_f32, side=side)
         return bias_grad(dy, db, side=side)
     ctx = side_begin(dy, x) if side else None
     with (ctx or _NULLCTX):
         tiles = -(-N // 128) * -(-K // 128)
-        if ctx is not None and accumulate_f32 is None and _Side.wgrad_nosplit:
-            # On the side stream the weight gradient only has to finish before the optimizer: one
-            # block per output tile, fp16 straight into the flat gradient (no fp32 slabs, no
-            # reduction pass), leaving most CUs to the dgrad chain on the critical path.
-            gemm(dy, x, dW, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0),
-                 ldc=dW.stride(0), epi=EPI_F16)
-            return dW
         s = _splitk_for(tiles, M)
         slabs = _workspace("slab", s * N * K, dy.device)
         rs = _workspace("rowsum", s * N, dy.device) if db is not None else None
-        if accumulate_f32 is None and _INLAUNCH_RED and K % 4 == 0 and dW.stride(0) % 4 == 0 and tiles <= _RED_CNT_CAP:
-            # the last split of each tile reduces the slabs (and the bias partials) itself
-            gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
-                 epi=EPI_F32, splitk=s, sCsplit=N * K, rowsum=rs, ld_rowsum=N, red_out=dW, red_bias=db,
-                 red_cnt=_red_counters(dy.device))
-            return dW
         gemm(dy, x, slabs, N, K, M, a_kc=False, b_kc=False, lda=dy.stride(0), ldb=x.stride(0), ldc=K,
              epi=EPI_F32, splitk=s, sCsplit=N * K, rowsum=rs, ld_rowsum=N)
         if db is not None and accumulate_f32 is None and N % 4 == 0:

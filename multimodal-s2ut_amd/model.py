@@ -18,7 +18,6 @@ Reference path restated here:
   fairseq TransformerUnitDecoder             (6 pre-LN layers, tied output projection)
 """
 import math
-import os
 import re
 from collections import OrderedDict
 
@@ -29,16 +28,6 @@ from . import kernels as K
 from .kernels import F16, round_up
 
 # ============================================================================ config
-
-
-# encoder backward: enqueue each dgrad (main stream, critical path) before the weight gradient
-# (side stream) that reads the same dy; MMS2UT_DGRAD_FIRST=0 restores wgrad-first (A/B)
-DGRAD_FIRST = os.environ.get("MMS2UT_DGRAD_FIRST", "1") != "0"
-# MMS2UT_RELU_MASK=1: the fc1 forward also writes a 1-bit activity mask of its ReLU+dropout output
-# (K.relu_mask_alloc) and the fc2 dgrad epilogue reads it instead of the fp16 activation (1/16 of
-# those bytes, bit-identical output).  Measured 0.6 % slower per step than reading the activation
-# (18.67 vs 18.56 ms, two interleaved pairs, profiles/round2_v3_relu_mask_ab.txt), so opt-in.
-RELU_MASK = os.environ.get("MMS2UT_RELU_MASK", "0") == "1"
 
 
 def default_cfg(**over):
@@ -372,13 +361,6 @@ def sinusoidal_table(num, dim, padding_idx=1):
 # ============================================================================ attention core
 
 
-import os as _os
-
-# fused flash attention for the multi-head paths (head_dim 64/96/128, length-style padding);
-# MMS2UT_ATTN=unfused selects the materialised-scores path (A/B, and the reference check)
-FLASH = _os.environ.get("MMS2UT_ATTN", "flash") != "unfused"
-
-
 class AttnCtx:
     """What an attention forward saves for its backward (flash: lse; unfused: P, Pd)."""
     __slots__ = ("flash", "P", "Pd", "ldS", "lse", "key_len", "causal")
@@ -388,7 +370,7 @@ def attn_forward(q, k, v, ldq, ldk, ldv, B, H, Tq, Tk, hd, scale, out, ldo, *, k
                  key_mask=None, causal=False, extra_key=False, p=0.0, drop=None):
     ctx = AttnCtx()
     ctx.key_len, ctx.causal = key_len, causal
-    ctx.flash = FLASH and key_mask is None and not extra_key and hd in K.FLASH_HD
+    ctx.flash = key_mask is None and not extra_key and hd in K.FLASH_HD
     if ctx.flash:
         ctx.lse = K.mha_fwd(q, k, v, out, ldq, ldk, ldv, ldo, B, H, Tq, Tk, hd, scale, key_len=key_len,
                             causal=causal, p=p, drop=drop)
@@ -531,7 +513,7 @@ class MMS2UTModel:
 
     def refresh_transposed_weights(self):
         """Re-transpose the dgrad weights (side stream) for this step's backward."""
-        if not (self.training and self.params.flat.is_cuda) or os.environ.get("MMS2UT_WT", "1") == "0":
+        if not (self.training and self.params.flat.is_cuda):
             K.TransposedWeights.active = None
             return
         if self.wt is None:
@@ -811,9 +793,8 @@ class MMS2UTModel:
         pact = self._p("activation_dropout")
         c["drop_act"] = self._drop(pact, R * cfg["encoder_ffn_embed_dim"])
         F_ = cfg["encoder_ffn_embed_dim"]
-        c["f1m"] = K.relu_mask_alloc(R, F_, h2.device) if RELU_MASK and F_ % 8 == 0 else None
         f1 = K.linear(h2, self.P(p + ".fc1.weight"), self.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP,
-                      p=pact, drop=c["drop_act"], mask=c["f1m"])
+                      p=pact, drop=c["drop_act"])
         c["f1"] = f1
         c["drop2"] = self._drop(pd, R * d)
         x3 = K.linear(f1, self.P(p + ".fc2.weight"), self.P(p + ".fc2.bias"), epi=K.EPI_DROP_RESID,
@@ -835,31 +816,20 @@ class MMS2UTModel:
         # fc2 / fc1
         if dy2 is None:
             dy2 = K.dropout(dx3, pd, c["drop2"], out=torch.empty_like(dx3)) if pd > 0 else dx3
-        # DGRAD_FIRST: the critical-path dgrad is enqueued before the side-stream weight gradient
-        # that reads the same dy, so its blocks are dispatched first
-        if not DGRAD_FIRST:
-            K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"), db=self.G(p + ".fc2.bias"))
-        df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD,
-                             aux=c["f1"] if c.get("f1m") is None else None, mask=c.get("f1m"), p=pact)
-        if DGRAD_FIRST:
-            K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"), db=self.G(p + ".fc2.bias"))
-        else:
-            K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"), db=self.G(p + ".fc1.bias"))
+        # the critical-path dgrad is enqueued before the side-stream weight gradient that reads
+        # the same dy, so its blocks are dispatched first
+        df1 = K.linear_dgrad(dy2, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD, aux=c["f1"], p=pact)
+        K.linear_wgrad(dy2, c["f1"], self.G(p + ".fc2.weight"), db=self.G(p + ".fc2.bias"))
         dh2 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
-        if DGRAD_FIRST:
-            K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"), db=self.G(p + ".fc1.bias"))
+        K.linear_wgrad(df1, c["h2"], self.G(p + ".fc1.weight"), db=self.G(p + ".fc1.bias"))
         del df1
         dx2, dyo = K.layernorm_bwd(dh2, c["x2"], self.P(p + ".final_layer_norm.weight"), c["m2"], c["r2"],
                                    self.params.span(p + ".final_layer_norm.weight", p + ".final_layer_norm.bias", grad=True),
                                    dres=dx3, emit=(pd, c["drop1"]))
         # out proj (dyo = dropout(dx2) with the attention-branch mask, from the LN backward)
-        if not DGRAD_FIRST:
-            K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"),
-                           db=self.G(p + ".self_attn.out_proj.bias"))
         dO = K.linear_dgrad(dyo, self.P(p + ".self_attn.out_proj.weight"))
-        if DGRAD_FIRST:
-            K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"),
-                           db=self.G(p + ".self_attn.out_proj.bias"))
+        K.linear_wgrad(dyo, c["O"], self.G(p + ".self_attn.out_proj.weight"),
+                       db=self.G(p + ".self_attn.out_proj.bias"))
         qkv = c["qkv"]
         dqkv = torch.empty_like(qkv)
         attn_backward(c["attn"], dO, d, c["O"], qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d,
@@ -870,11 +840,8 @@ class MMS2UTModel:
         def qkv_wgrad():
             K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
                            db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
-        if not DGRAD_FIRST:
-            qkv_wgrad()
         dh1 = K.linear_dgrad(dqkv, Wqkv)
-        if DGRAD_FIRST:
-            qkv_wgrad()
+        qkv_wgrad()
         if emit is None:
             dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
                                  self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),
@@ -1256,9 +1223,8 @@ class MMS2UTModel:
         h3, c["m3"], c["r3"] = K.layernorm(x3, self.P(p + ".final_layer_norm.weight"), self.P(p + ".final_layer_norm.bias"))
         c["h3"] = h3
         c["drop_act"] = self._drop(pact, R * spec.F)
-        c["f1m"] = K.relu_mask_alloc(R, spec.F, h3.device) if RELU_MASK and spec.F % 8 == 0 else None
         f1 = K.linear(h3, self.P(p + ".fc1.weight"), self.P(p + ".fc1.bias"), epi=K.EPI_RELU_DROP, p=pact,
-                      drop=c["drop_act"], mask=c["f1m"])
+                      drop=c["drop_act"])
         c["f1"] = f1
         c["drop3"] = self._drop(pd, R * d)
         x4 = K.linear(f1, self.P(p + ".fc2.weight"), self.P(p + ".fc2.bias"), epi=K.EPI_DROP_RESID, aux=x3,
@@ -1280,7 +1246,7 @@ class MMS2UTModel:
         K.linear_wgrad(dy3, c["f1"], self.G(p + ".fc2.weight"),
                        db=self.G(p + ".fc2.bias"))
         df1 = K.linear_dgrad(dy3, self.P(p + ".fc2.weight"), epi=K.EPI_RELU_DROP_BWD,
-                             aux=c["f1"] if c.get("f1m") is None else None, mask=c.get("f1m"), p=pact)
+                             aux=c["f1"], p=pact)
         K.linear_wgrad(df1, c["h3"], self.G(p + ".fc1.weight"),
                        db=self.G(p + ".fc1.bias"))
         dh3 = K.linear_dgrad(df1, self.P(p + ".fc1.weight"))
@@ -1318,11 +1284,8 @@ class MMS2UTModel:
         def qkv_wgrad():
             K.linear_wgrad(dqkv, c["h1"], self.params.span(p + ".self_attn.q_proj.weight", p + ".self_attn.v_proj.weight", grad=True).view(3 * d, d),
                            db=self.params.span(p + ".self_attn.q_proj.bias", p + ".self_attn.v_proj.bias", grad=True))
-        if not DGRAD_FIRST:
-            qkv_wgrad()
         dh1 = K.linear_dgrad(dqkv, Wqkv)
-        if DGRAD_FIRST:
-            qkv_wgrad()
+        qkv_wgrad()
         if emit is None:
             dx = K.layernorm_bwd(dh1, c["x"], self.P(p + ".self_attn_layer_norm.weight"), c["m1"], c["r1"],
                                  self.params.span(p + ".self_attn_layer_norm.weight", p + ".self_attn_layer_norm.bias", grad=True),

@@ -10,7 +10,6 @@ Reference semantics (fairseq, invoked by textless/1_train.sh:105-125):
   --warmup-init-lr 1e-7 --warmup-updates 10000 --fp16 (init scale 128, scale window 2^14/world).
 """
 import math
-import os
 
 import torch
 
@@ -36,7 +35,7 @@ class FP16Adam:
         ost[K.OST_LAST_OVERFLOW] = -1.0
         ost[K.OST_CLIP_COEF] = 1.0
         self.ost = ost.to(params.flat.device)
-        self.defer = os.environ.get("MMS2UT_DEFER_ADAM", "1") == "1"
+        self.defer = True   # False: one Adam launch in stream order (tests compare both)
 
     def resync_master(self):
         """After loading fp16 weights: master := fp32 copy of the fp16 params."""
@@ -63,8 +62,8 @@ class FP16Adam:
         one per forward-consumption group of the parameter layout (subsampler, encoder layer 0, ...),
         each recording an event that the next forward waits on right before it reads that group
         (ParamStore.await_group), so the HBM-bound update can overlap the next step's first
-        layers (default; 1-1.5 % faster step, bit-identical).  MMS2UT_DEFER_ADAM=0 runs one
-        launch in stream order instead."""
+        layers (default; 1-1.5 % faster step, bit-identical).  defer = False runs one launch in
+        stream order instead."""
         b1, b2 = self.betas
         K.grad_norm(self.params.grad, self.ost, sample_size)
         if check is not None:

@@ -27,7 +27,6 @@ Buffer access: the Adam update and the gradient zeroing run deferred on the side
 ``params.flat`` / ``params.grad`` / ``opt.master`` directly after a step; ``state_dict``,
 ``opt.stats`` and the next forward wait by themselves.
 """
-import os
 
 import numpy as np
 import torch
@@ -78,7 +77,7 @@ class Trainer:
         # so the hardware dispatcher prefers its workgroups over the weight-gradient side stream's
         # (lowest priority), which only fills the CUs the critical path leaves idle.
         self.stream = None
-        if os.environ.get("MMS2UT_STREAM_PRIO", "1") != "0" and model.params.flat.is_cuda:
+        if model.params.flat.is_cuda:
             self.stream = torch.cuda.Stream(device=model.params.flat.device, priority=-100)
             if K._Side.stream is None:
                 K._Side.stream = K.make_side_stream(model.params.flat.device)

@@ -1,5 +1,5 @@
 """Warm vs cold-cache GEMM time on the step's shapes: the same operands re-used (L2 / MALL hot,
-what scripts/gemm_shapes.py measures) vs a rotation over operand sets larger than the 256 MiB
+what the retired scripts/gemm_shapes.py measured) vs a rotation over operand sets larger than the 256 MiB
 MALL with a 512 MiB sweep between calls (what the training step sees).
 
     python scripts/gemm_cold.py [M]

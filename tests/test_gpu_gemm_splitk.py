@@ -17,6 +17,18 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
+def _linear(K_, x, W, bias, fixup, epi, aux=None, out2=None, p=0.0, drop=None):
+    """K.linear with the split-K fixup on or off (kernels.gemm fixup=)."""
+    M, Kd = x.shape
+    N = W.shape[0]
+    out = torch.empty(M, N, dtype=torch.float16, device=x.device)
+    seed, off = drop if p > 0 else (0, 0)
+    K_.gemm(x, W, out, M, N, Kd, lda=Kd, ldb=Kd, ldc=N, epi=epi, bias=bias, aux=aux,
+            ldaux=0 if aux is None else aux.stride(0), out2=out2, ldo2=0 if out2 is None else out2.stride(0),
+            p=p, seed=seed, offset=off, ld_rng=N, fixup=fixup)
+    return out
+
+
 @pytest.mark.parametrize("M,N,K", [(466, 768, 3072), (466, 3072, 768), (300, 768, 768), (700, 2304, 768),
                                    (129, 768, 3072)])
 def test_fixup_matches_unsplit(M, N, K):
@@ -45,14 +57,10 @@ def test_fixup_matches_unsplit(M, N, K):
         bias = kw.pop("bias", b if kw["epi"] not in (K_.EPI_RELU_DROP_BWD,) else None)
         outs = []
         for fix in (False, True):
-            K_._SPLITK_FIX = fix
-            try:
-                o2 = kw.get("out2")
-                if o2 is not None:
-                    o2.zero_()
-                outs.append((K_.linear(x, W, bias, **kw).clone(), None if o2 is None else o2.clone()))
-            finally:
-                K_._SPLITK_FIX = True
+            o2 = kw.get("out2")
+            if o2 is not None:
+                o2.zero_()
+            outs.append((_linear(K_, x, W, bias, fix, **kw).clone(), None if o2 is None else o2.clone()))
         torch.cuda.synchronize()
         (ref, ref2), (got, got2) = outs
         assert _rel(got, ref) < 2e-3, (name, _rel(got, ref))
@@ -68,7 +76,7 @@ def test_fixup_matches_unsplit(M, N, K):
 
 
 def test_fixup_accumulate_dgrad():
-    """dgrad with accumulation (EPI_F16_ACC) at a decoder shape."""
+    """dgrad with accumulation (EPI_F16_ACC) at a decoder shape: fixup vs unsplit vs fp32."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     mm = pkg()
@@ -80,69 +88,10 @@ def test_fixup_accumulate_dgrad():
     base = torch.randn(M, K, device="cuda", generator=g).half()
     outs = []
     for fix in (False, True):
-        K_._SPLITK_FIX = fix
-        try:
-            o = base.clone()
-            K_.linear_dgrad(dy, W, o, accumulate=True)
-            outs.append(o)
-        finally:
-            K_._SPLITK_FIX = True
+        o = base.clone()
+        K_.gemm(dy, W, o, M, K, N, a_kc=True, b_kc=False, lda=N, ldb=K, ldc=K, epi=K_.EPI_F16_ACC, fixup=fix)
+        outs.append(o)
     torch.cuda.synchronize()
     exact = base.float() + dy.float() @ W.float()
     assert _rel(outs[1], outs[0]) < 2e-3
     assert _rel(outs[1], exact) < 2e-3
-
-
-@pytest.mark.parametrize("M,N,K", [(11000, 768, 768), (11000, 768, 3072), (11000, 2304, 768), (12000, 768, 768)])
-def test_tail_split_matches_single_launch(M, N, K):
-    """A grid that overflows the 512 block slots by a small tail: head rows as usual, tail rows
-    split-K + fixup (kernels._tail_split_rows) == one launch, masks identical."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    mm = pkg()
-    K_ = mm.kernels
-    M1 = K_._tail_split_rows(M, N, K)
-    assert 0 < M1 < M
-    g = torch.Generator(device="cuda").manual_seed(2)
-    x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
-    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).half()
-    aux = torch.randn(M, N, device="cuda", generator=g).half()
-    big = torch.full((N,), 30.0, device="cuda").half()
-    for name, kw in (("relu_drop_open", dict(epi=K_.EPI_RELU_DROP, p=0.1, drop=(3, 512))),
-                     ("drop_resid", dict(epi=K_.EPI_DROP_RESID, p=0.1, drop=(5, 0), aux=aux))):
-        outs = []
-        tail0 = K_._TAIL_SPLIT
-        for tail in (False, True):
-            K_._TAIL_SPLIT = tail
-            try:
-                outs.append(K_.linear(x, W, big, **kw).clone())
-            finally:
-                K_._TAIL_SPLIT = tail0
-        torch.cuda.synchronize()
-        assert _rel(outs[1], outs[0]) < 2e-3, name
-        assert torch.equal(outs[1][:M1], outs[0][:M1]), name        # the head is the same launch
-        if name == "relu_drop_open":
-            assert torch.equal(outs[1] == 0, outs[0] == 0)
-
-
-@pytest.mark.parametrize("M", [4096, 470, 1003])
-def test_relu_mask_roundtrip(M):
-    """fc1 forward writes the 1-bit ReLU+dropout activity mask (bit n%8 of byte n/8 = out > 0) and
-    the fc2 dgrad epilogue reading it is bit-identical to reading the fp16 activation — on the
-    LDS-staged fast path, the short-M split-K fixup path and an odd M."""
-    K = pkg().kernels
-    torch.manual_seed(0)
-    F, d = 3072, 768
-    x = torch.randn(M, d, device="cuda").half()
-    W1 = (0.05 * torch.randn(F, d, device="cuda")).half()
-    b1 = torch.randn(F, device="cuda").half()
-    mask = K.relu_mask_alloc(M, F, "cuda").fill_(0xAA)
-    f1 = K.linear(x, W1, b1, epi=K.EPI_RELU_DROP, p=0.1, drop=(11, 4096), mask=mask)
-    assert torch.equal(K.relu_mask_unpack(mask, M, F), f1 > 0)
-    f1b = K.linear(x, W1, b1, epi=K.EPI_RELU_DROP, p=0.1, drop=(11, 4096))
-    assert torch.equal(f1, f1b)          # writing the mask does not change the activation
-    dy = torch.randn(M, d, device="cuda").half()
-    W2 = (0.05 * torch.randn(d, F, device="cuda")).half()
-    ref = K.linear_dgrad(dy, W2, epi=K.EPI_RELU_DROP_BWD, aux=f1, p=0.1)
-    got = K.linear_dgrad(dy, W2, epi=K.EPI_RELU_DROP_BWD, mask=mask, p=0.1)
-    assert torch.equal(ref, got)

@@ -214,10 +214,10 @@ def test_linear_splitk_epilogue(M, N, Kd, s, relu, res):
 
 
 @pytest.mark.parametrize("M,N,Kd,s", [(160, 768, 3072, 8), (37, 768, 768, 3), (200, 256, 1024, 4)])
-def test_splitk_epilogue_ln_bit_identical(M, N, Kd, s, monkeypatch):
-    """Fused split-K reduction + residual + LayerNorm == the two-launch sequence, bit for bit (the
-    one-wave-per-row LayerNorm kernel, whose reduction order the fused epilogue follows)."""
-    monkeypatch.setenv("MMS2UT_LN_FWD16", "0")
+def test_splitk_epilogue_ln_matches_two_launch(M, N, Kd, s):
+    """Fused split-K reduction + residual + LayerNorm == the two-launch sequence: the residual sum
+    bit for bit, the LayerNorm output within one fp16 rounding (the fused epilogue reduces a row in
+    one wave, the standalone kernel for D % 256 == 0 in a half wave)."""
     K = pkg("kernels")
     g = torch.Generator().manual_seed(N + M)
     x = (torch.randn(M, Kd, generator=g) * 0.5).half().cuda()
@@ -229,17 +229,15 @@ def test_splitk_epilogue_ln_bit_identical(M, N, Kd, s, monkeypatch):
     xo, y = K.linear_splitk_ln(x, W, b, res, gam, bet, splitk=s)
     xr = K.linear_splitk(x, W, b, aux=res, splitk=s)
     yr = K.layernorm(xr, gam, bet)[0]
-    assert torch.equal(xo, xr) and torch.equal(y, yr)
+    assert torch.equal(xo, xr)
+    assert ((y.float() - yr.float()).abs() <= 2e-3 * (1 + yr.float().abs())).all()
 
 
 @pytest.mark.parametrize("bsz,beam,V,k,first", [(16, 10, 1004, 20, False), (3, 10, 1004, 19, True),
                                                 (5, 4, 37, 8, False), (2, 2, 9, 4, True)])
-@pytest.mark.parametrize("one_pass", ["0", "1"])
-def test_beam_topk_matches_sorted_selection(bsz, beam, V, k, first, one_pass, monkeypatch):
-    """HIP candidate selection (two-pass default, one-block variant) == stable sort of
-    (lprobs + cumulative score) descending, ties to the lower flat index; -inf candidates (pad)
-    included when finite ones run out."""
-    monkeypatch.setenv("MMS2UT_BEAM_TOPK_1PASS", one_pass)
+def test_beam_topk_matches_sorted_selection(bsz, beam, V, k, first):
+    """HIP candidate selection == stable sort of (lprobs + cumulative score) descending, ties to
+    the lower flat index; -inf candidates (pad) included when finite ones run out."""
     K = pkg("kernels")
     g = torch.Generator().manual_seed(V + k)
     lp = torch.log_softmax(torch.randn(bsz * beam, V, generator=g) * 3, -1)

@@ -143,10 +143,8 @@ def test_layernorm_padded_dropout(K, extra):
     assert torch.equal(dgb0, dgb1)
 
 
-@pytest.mark.parametrize("ln16", ["1", "0"])
-def test_layernorm_fwd_bwd(K, ln16, monkeypatch):
-    """ln16=1: D % 256 == 0 takes the 16-B half-wave-per-row backward; 0 forces the 8-B one."""
-    monkeypatch.setenv("MMS2UT_LN16", ln16)
+def test_layernorm_fwd_bwd(K):
+    """D % 256 == 0 takes the 16-B half-wave-per-row kernels, D = 96 the one-wave-per-row ones."""
     # 46160 rows (the image LayerNorm of a 80-utterance ViT batch): each 16-B-path block folds
     # several 8-row groups into one dgamma / dbeta partial row (ops.hip ln16_iters)
     for R, D in ((1000, 768), (37, 256), (5, 96), (3, 1024), (46160, 768)):
@@ -284,16 +282,16 @@ def _attn_ref(q, k, v, lens, causal, scale, mask=None):
     (False, 33, 200, [200, 64, 63], 0.1), (True, 128, 128, [128, 77, 5], 0.1),
     (False, 100, 128, [128, 100, 1], 0.2), (False, 1, 17, [17, 9, 1], 0.0),
     (False, 300, 100, [100, 57, 2], 0.1), (True, 256, 256, [256, 200, 9], 0.1),
-    (False, 301, 213, [213, 129, 1], 0.1), (True, 257, 257, [257, 130, 4], 0.0)])
-@pytest.mark.parametrize("fused", ["1", "0", "grid2"])
-def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p, fused, monkeypatch):
-    """fused=1: Tk <= 256 takes the one-launch chunked backward (any Tq); fused=0 forces the
-    three-kernel one.  Tk = 257 exercises the fallback to the three-kernel path.  grid2: the fused
-    kernel runs on 2 persistent blocks, so each block walks 3 heads (next-head prefetch path)."""
-    monkeypatch.setenv("MMS2UT_ATTN_FUSED", "0" if fused == "0" else "1")
-    if fused == "grid2":
-        monkeypatch.setenv("MMS2UT_ATTN_PERSIST", "2")
-    B, H = 3, 2
+    (False, 301, 213, [213, 129, 1], 0.1), (True, 257, 257, [257, 130, 4], 0.0),
+    (False, 70, 300, [300, 257, 3], 0.1), (True, 300, 300, [300, 129, 2], 0.2)])
+@pytest.mark.parametrize("heads", ["few", "many"])
+def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p, heads):
+    """Tk <= 256 takes the one-launch chunked backward (any Tq), Tk > 256 the three-kernel one.
+    heads=many: B*H = 3*96 = 288 heads > 256 CUs, so persistent blocks of the fused kernel walk
+    several heads (the next-head prefetch path)."""
+    B, H = 3, (2 if heads == "few" else 96)
+    if heads == "many" and (Tq > 130 or Tk > 256):
+        pytest.skip("the many-heads case only targets the fused kernel")
     d = H * hd
     g = torch.Generator(device="cuda").manual_seed(5)
     q = torch.randn(B * Tq, d, generator=g, device="cuda").half()
@@ -420,10 +418,10 @@ def test_wgrad_fused_bias(K, M, N, K_):
 
 
 @pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K_", [(300, 520, 192), (513, 96, 768), (64, 1004, 64)])
-def test_gemm_tile256(K, a_kc, b_kc, M, N, K_, monkeypatch):
-    """The 256x256-tile ring kernel on ragged shapes and every operand layout."""
-    monkeypatch.setenv("MMS2UT_GEMM_TILE", "256")
+@pytest.mark.parametrize("M,N,K_", [(4100, 1540, 2048), (4233, 1600, 2112)])
+def test_gemm_tile256(K, a_kc, b_kc, M, N, K_):
+    """The 256x256-tile ring kernel (taken for M >= 4096, N >= 1536, K >= 2048) on ragged shapes and
+    every operand layout."""
     A = _mat(M, K_, seed=1) if a_kc else _mat(K_, M, ld=(M + 7) // 8 * 8, seed=1)
     B = _mat(N, K_, seed=2) if b_kc else _mat(K_, N, ld=(N + 7) // 8 * 8, seed=2)
     Af = A.float() if a_kc else A.float().t()

@@ -206,13 +206,9 @@ def test_update_freq_accumulation_matches_union(tmp_path):
                for s, (L, T) in enumerate((([120, 90], [30, 22]), ([100, 77, 60], [25, 20, 15])))]
     grads = {}
     for name, uf in (("accum", 2), ("union", 1)):
-        os_env = __import__("os").environ
-        os_env["MMS2UT_DEFER_ADAM"] = "0"
-        try:
-            model = mm.MMS2UTModel(cfg, device="cuda").init_params(seed=5)
-            tr = mm.trainer.Trainer(model, lr=1e-4, update_freq=uf, init_scale=8.0)
-        finally:
-            os_env.pop("MMS2UT_DEFER_ADAM")
+        model = mm.MMS2UTModel(cfg, device="cuda").init_params(seed=5)
+        tr = mm.trainer.Trainer(model, lr=1e-4, update_freq=uf, init_scale=8.0)
+        tr.opt.defer = False
         if uf == 2:
             bs = [mm.runtime.prepare_batch(s, cfg, "cuda") for s in samples]
         else:

@@ -1,7 +1,6 @@
 """GPU: the trainer's deferred, chunked Adam (optimizer update on the side stream, awaited group
 by group by the next forward) gives bit-identical parameters and optimizer state to the
 in-order update over several steps; the forward-consumption groups tile the flat buffer."""
-import os
 
 import pytest
 import torch
@@ -14,20 +13,17 @@ pytestmark = pytest.mark.gpu
 
 def _run(defer, steps=3):
     mm = pkg()
-    os.environ["MMS2UT_DEFER_ADAM"] = "1" if defer else "0"
-    try:
-        cfg = mm.default_cfg(**R.no_dropout(R.tiny_config(conv_channels=256)))
-        model = mm.MMS2UTModel(cfg, device="cuda:0").init_params(seed=4)
-        tr = mm.trainer.Trainer(model, lr=1e-3, warmup_updates=2, world_size=1)
-        sample = mm.data.make_sample([61, 47, 30], [14, 11, 9], img_tokens=17, img_dim=cfg["image_feat_dim"], seed=2)
-        batch = mm.runtime.prepare_batch(sample, model.cfg, "cuda:0")
-        for _ in range(steps):
-            tr.train_step(batch)
-        st = tr.opt.stats()
-        torch.cuda.synchronize()
-        return model.params.flat.clone(), tr.opt.master.clone(), tr.opt.exp_avg_sq.clone(), st
-    finally:
-        os.environ.pop("MMS2UT_DEFER_ADAM", None)
+    cfg = mm.default_cfg(**R.no_dropout(R.tiny_config(conv_channels=256)))
+    model = mm.MMS2UTModel(cfg, device="cuda:0").init_params(seed=4)
+    tr = mm.trainer.Trainer(model, lr=1e-3, warmup_updates=2, world_size=1)
+    tr.opt.defer = defer
+    sample = mm.data.make_sample([61, 47, 30], [14, 11, 9], img_tokens=17, img_dim=cfg["image_feat_dim"], seed=2)
+    batch = mm.runtime.prepare_batch(sample, model.cfg, "cuda:0")
+    for _ in range(steps):
+        tr.train_step(batch)
+    st = tr.opt.stats()
+    torch.cuda.synchronize()
+    return model.params.flat.clone(), tr.opt.master.clone(), tr.opt.exp_avg_sq.clone(), st
 
 
 def test_deferred_adam_bit_identical():
