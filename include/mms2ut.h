@@ -85,6 +85,23 @@ typedef struct mms2ut_gemm_args {
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
 
+/* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the
+ * reference layer's projections): for each of the n <= 8 problems, dW[N, K] = dy[rows, N]^T @
+ * x[rows, K] (fp16, row stride K, overwritten) and, when db != NULL, db[N] = column sums of dy —
+ * all in ONE launch over the union of the problems' 128x128 tiles, unsplit (fp32 accumulation over
+ * all rows, no split-K slabs).  lddy, ldx multiples of 8; N, K multiples of 8; dy, x, dW 16-B
+ * aligned.  Deterministic (fixed reduction order per tile).                                      */
+typedef struct mms2ut_wgrad {
+  const mms2ut_half* dy;
+  int64_t lddy;
+  const mms2ut_half* x;
+  int64_t ldx;
+  mms2ut_half* dW;
+  mms2ut_half* db;
+  int N, K;
+} mms2ut_wgrad;
+int mms2ut_wgrad_group(const mms2ut_wgrad* w, int n, int64_t rows, hipStream_t stream);
+
 /* live GEMM timing for the benchmark roofline: between begin/end every mms2ut_gemm_f16 launch
  * is bracketed by HIP events on its own stream (or, in stamp mode below, timed by its own
  * workgroups); end() synchronises and returns the summed event time (0 in stamp mode), the launch
@@ -292,10 +309,12 @@ int mms2ut_add_f16(const mms2ut_half* a, const mms2ut_half* b, mms2ut_half* out,
 /* ---------------------------------------------------------------- label-smoothed CE
  * fairseq speech_to_unit -> LabelSmoothedCrossEntropyCriterion.compute_loss (reference copy
  * criterions/speech_to_speech_criterion.py:58-102): fp32 log_softmax over V, eps-smoothing,
- * pad targets ignored, reduce=sum.  loss_out[2] = {loss, nll} (fp32, accumulated atomically;
- * zero it first).  lse[rows] saved for the backward.                                        */
+ * pad targets ignored, reduce=sum.  loss_out[2] += {loss, nll} (fp32; per-block partials in
+ * part[2 * MMS_LS_XENT_PARTS] summed in a fixed order: bit-reproducible).  lse[rows] saved for
+ * the backward.                                                                              */
+#define MMS_LS_XENT_PARTS 512
 int mms2ut_ls_xent_fwd(const mms2ut_half* logits, int64_t ld, const int64_t* target, int64_t rows,
-                       int V, float eps, int pad_idx, float* lse, float* loss_out,
+                       int V, float eps, int pad_idx, float* lse, float* part, float* loss_out,
                        hipStream_t stream);
 /* dlogits = grad * ((1-eps-eps_i)(p - onehot) + eps_i(V p - 1)), 0 on pad rows; in place OK */
 int mms2ut_ls_xent_bwd(const mms2ut_half* logits, int64_t ld, const int64_t* target, int64_t rows,

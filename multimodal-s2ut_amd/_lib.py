@@ -90,6 +90,11 @@ class LayerArgs(C.Structure):
         [("x", vp), ("saved", vp)]
 
 
+class WgradArgs(C.Structure):
+    """mms2ut_wgrad (include/mms2ut.h): one problem of a grouped weight-gradient launch."""
+    _fields_ = [("dy", vp), ("lddy", i64), ("x", vp), ("ldx", i64), ("dW", vp), ("db", vp), ("N", i32), ("K", i32)]
+
+
 class LayerGradArgs(C.Structure):
     """mms2ut_layer_grad (include/mms2ut.h)."""
     _fields_ = [("dy", vp), ("dy_drop", vp), ("emit_p", f32), ("emit_seed", u64), ("emit_offset", u64),
@@ -105,6 +110,7 @@ SIGNATURES = {
     "mms2ut_last_error": (C.c_char_p, []),
     "mms2ut_version": (i32, []),
     "mms2ut_gemm_f16": (i32, [vp, vp]),   # GEMM_ARGS.pack(...) bytes or C.byref(GemmArgs)
+    "mms2ut_wgrad_group": (i32, [vp, i32, i64, vp]),
     "mms2ut_profile_begin": (i32, [i32]),
     "mms2ut_profile_end": (i32, [C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "mms2ut_profile_bytes": (i32, [C.POINTER(C.c_double)]),
@@ -154,7 +160,7 @@ SIGNATURES = {
     "mms2ut_col2im": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mms2ut_gate_bwd": (i32, [vp, vp, vp, vp, vp, i64, i32, vp]),
     "mms2ut_copy2d": (i32, [vp, i64, vp, i64, i64, i32, vp]),
-    "mms2ut_ls_xent_fwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp]),
+    "mms2ut_ls_xent_fwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp]),
     "mms2ut_ls_xent_bwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp]),
     "mms2ut_grad_sqnorm": (i32, [vp, i64, vp, i32, vp]),
     "mms2ut_grad_norm_finalize": (i32, [vp, i32, vp, vp, vp]),

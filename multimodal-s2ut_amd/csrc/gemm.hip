@@ -46,6 +46,7 @@ struct GemmP {
   float p; uint32_t thresh; uint64_t seed, offset; long ld_rng;
   int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity
   float* rowsum; long ld_rowsum;  // RS kernels: split-K partial A-row sums (bias gradient)
+  h16* rowsum16;                  // RS kernels, unsplit: the fp16 A-row sums (grouped wgrad)
   int group_m;  // tile-rows per L2 group (tile_coords)
   unsigned long long* stamps;  // profiling: per block {first, last} s_memrealtime tick, or null
 };
@@ -641,13 +642,10 @@ MMS_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
-__global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
-  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
-  if (P.thresh) P.seed = mms_step_seed(P.seed);
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
-  int z, tm, tn;
-  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
+// One 128x128 output tile of the LDS-DMA pipeline (z = batch * splitk + split).  PRI: raise the
+// wave priority around the MFMA blocks (critical-path GEMMs; not the side stream's weight gradients)
+template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS, bool PRI>
+MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
   const int zb = z / P.splitk, zs = z % P.splitk;
   const int z1 = zb / P.bdiv, z2 = zb % P.bdiv;
   const int kbeg = zs * P.kchunk;
@@ -678,7 +676,7 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   // RS: the first column of tiles also sums its A rows over k with one extra MFMA per A fragment
   // (B = ones): lane l ends up with sum_k A(bm + wm*64 + 16i + (l & 15), k) in every element of rs[i]
   f32x4 rs[4];
-  const bool do_rs = RS && tn == 0 && wn == 0;
+  const bool do_rs = RS && tn == 0 && wn == 0 && (P.rowsum || P.rowsum16);   // (grouped: db may be NULL)
   if (RS) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) rs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -715,13 +713,13 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
       for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
-      if (PRIO && EPI != MMS_EPI_F32) __builtin_amdgcn_s_setprio(1);
+      if (PRI) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-      if (PRIO && EPI != MMS_EPI_F32) __builtin_amdgcn_s_setprio(0);
+      if (PRI) __builtin_amdgcn_s_setprio(0);
       if (RS && do_rs) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) rs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, fa[i], rs[i], 0, 0, 0);
@@ -735,7 +733,8 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
     for (int i = 0; i < 4; ++i) {
       const int m = bm + wm * 64 + i * 16 + lane;
       if (m < P.M) {
-        P.rowsum[(long)zs * P.ld_rowsum + m] = rs[i][0] * P.alpha;
+        if (P.rowsum16) P.rowsum16[m] = (h16)(rs[i][0] * P.alpha);   // unsplit: the bias gradient itself
+        else P.rowsum[(long)zs * P.ld_rowsum + m] = rs[i][0] * P.alpha;   // (do_rs: one of them is set)
       }
     }
   }
@@ -749,7 +748,50 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   // last k-step waited for vmcnt(0))
   __syncthreads();
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+}
+
+template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
+__global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * 2 * TILE_BYTES];
+  int z, tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
+  dma_gemm_tile<A_KC, B_KC, EPI, STAGES, RS, PRIO && EPI != MMS_EPI_F32>(P, smem, z, tm, tn);
   stamp_end(P.stamps, t_start);
+}
+
+// Grouped weight gradients: the dW = dy^T x products of one transformer layer (QKV, out-proj, fc1,
+// fc2, and the decoder's cross-attention q / out) as ONE launch over the union of their 128x128
+// tiles, unsplit: fp16 dW and (first tile column) fp16 db written straight from the accumulators,
+// no fp32 split-K slabs and no reduction pass.  The layer's ~400-500 tiles fill the 512 block slots
+// in one round (2 per CU), each tile reducing over all of the layer's token rows.  The linear block
+// id is remapped as tile_coords does (each XCD one contiguous range of the grouped tile space),
+// then resolved to (problem, tile) by the prefix table.
+constexpr int kGroupMax = 8;
+struct GemmGroup {
+  GemmP p[kGroupMax];
+  int first[kGroupMax + 1];   // prefix sums of the problems' tile counts
+  int tiles_m[kGroupMax], tiles_n[kGroupMax];
+  int n;
+  unsigned long long* stamps;
+};
+
+__global__ void __launch_bounds__(NT, 2) gemm_group_wgrad_kernel(GemmGroup G, int total) {
+  const unsigned long long t_start = G.stamps ? stamp_now() : 0ull;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
+  const int q = total / 8, r = total % 8, x = blockIdx.x % 8;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
+  int g = 0;
+  while (g + 1 < G.n && id >= G.first[g + 1]) ++g;
+  const GemmP& P = G.p[g];
+  const int t = id - G.first[g], tiles_n = G.tiles_n[g];
+  const int per_group = P.group_m * tiles_n;
+  const int grp = t / per_group, first_m = grp * P.group_m;
+  const int gsize = min(G.tiles_m[g] - first_m, P.group_m);
+  const int w = t % per_group;
+  dma_gemm_tile<false, false, MMS_EPI_F16, 2, true, false>(P, smem, 0, first_m + w % gsize, w / gsize);
+  stamp_end(G.stamps, t_start);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1138,6 +1180,86 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
     if (a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_RELU_DROP_BWD || a->epi == MMS_EPI_F16_ACC) extra = 2.0 * a->M * a->N;
     if (a->epi == MMS_EPI_GATE) extra = 6.0 * a->M * a->N;  // o, t read; g written
     g_prof.bytes += nb * (2.0 * ((double)a->M * a->K + (double)a->N * a->K) + c_bytes + extra);
+  }
+  return rc;
+}
+
+static int wgrad_group_dispatch(const mms2ut_wgrad* w, int n, int64_t rows, hipStream_t stream) {
+  MMS_REQUIRE(w && n >= 1 && n <= kGroupMax, "wgrad_group: need 1..%d problems", kGroupMax);
+  MMS_REQUIRE(rows >= 0, "wgrad_group: rows < 0");
+  GemmGroup G{};
+  G.n = n;
+  int total = 0;
+  for (int i = 0; i < n; ++i) {
+    const mms2ut_wgrad& q = w[i];
+    MMS_REQUIRE((rows == 0 || (q.dy && q.x)) && q.dW && q.N > 0 && q.K > 0,
+                "wgrad_group: problem %d: null operand or empty shape", i);
+    MMS_REQUIRE(q.N % 8 == 0 && q.K % 8 == 0 && q.lddy % 8 == 0 && q.ldx % 8 == 0 && q.lddy >= q.N && q.ldx >= q.K,
+                "wgrad_group: problem %d: N, K, lddy, ldx must be multiples of 8 (N=%d K=%d)", i, q.N, q.K);
+    MMS_REQUIRE(((uintptr_t)q.dy & 15) == 0 && ((uintptr_t)q.x & 15) == 0 && ((uintptr_t)q.dW & 15) == 0 &&
+                    (!q.db || ((uintptr_t)q.db & 1) == 0),
+                "wgrad_group: problem %d: operands must be 16-B aligned", i);
+    MMS_REQUIRE(rows * q.lddy * 2 < (1L << 31) && rows * q.ldx * 2 < (1L << 31),
+                "wgrad_group: problem %d: operand extent exceeds a buffer descriptor", i);
+    GemmP& P = G.p[i];
+    P.A = q.dy; P.B = q.x; P.C = q.dW;
+    P.M = q.N; P.N = q.K; P.K = (int)rows;
+    P.lda = q.lddy; P.ldb = q.ldx; P.ldc = q.K;
+    P.bdiv = 1; P.splitk = 1;
+    P.kchunk = (int)((rows + BK - 1) / BK * BK);
+    if (P.kchunk == 0) P.kchunk = BK;
+    P.alpha = 1.f;
+    P.vec16 = 1;
+    P.rowsum16 = q.db;
+    P.group_m = kGroupM;
+    G.tiles_m[i] = (q.N + BM - 1) / BM;
+    G.tiles_n[i] = (q.K + BN - 1) / BN;
+    G.first[i] = total;
+    total += G.tiles_m[i] * G.tiles_n[i];
+  }
+  G.first[n] = total;
+  if (rows == 0) {   // empty batch: zero gradients (the GEMM's k loop would not run)
+    for (int i = 0; i < n; ++i) {
+      if (hipMemsetAsync(w[i].dW, 0, (size_t)w[i].N * w[i].K * 2, stream) != hipSuccess ||
+          (w[i].db && hipMemsetAsync(w[i].db, 0, (size_t)w[i].N * 2, stream) != hipSuccess)) {
+        mms::set_error("wgrad_group: hipMemsetAsync failed");
+        return 1;
+      }
+    }
+    return 0;
+  }
+  G.stamps = stamp_take(total);
+  hipLaunchKernelGGL(gemm_group_wgrad_kernel, dim3(total), dim3(NT), 0, stream, G, total);
+  return mms::check_launch("gemm_group_wgrad");
+}
+
+extern "C" int mms2ut_wgrad_group(const mms2ut_wgrad* w, int n, int64_t rows, hipStream_t stream) {
+  if (!g_prof.on || g_prof.n >= g_prof.cap) return wgrad_group_dispatch(w, n, rows, stream);
+  const int i = g_prof.n++;
+  int rc;
+  if (g_prof.stamps) {
+    g_prof.l_blk[2 * i] = g_prof.cursor;
+    rc = wgrad_group_dispatch(w, n, rows, stream);
+    g_prof.l_blk[2 * i + 1] = g_prof.cursor;
+  } else {
+    hipEventRecord(g_prof.ev[2 * i], stream);
+    rc = wgrad_group_dispatch(w, n, rows, stream);
+    hipEventRecord(g_prof.ev[2 * i + 1], stream);
+  }
+  if (w && n > 0) {
+    double fl = 0.0, by = 0.0;
+    int sumN = 0;
+    for (int j = 0; j < n; ++j) {
+      fl += 2.0 * w[j].N * w[j].K * (double)rows;
+      by += 2.0 * ((double)rows * (w[j].N + w[j].K) + (double)w[j].N * w[j].K + (w[j].db ? w[j].N : 0));
+      sumN += w[j].N;
+    }
+    g_prof.flops += fl;
+    g_prof.bytes += by;
+    g_prof.l_flops[i] = fl;
+    g_prof.l_mnk[4 * i] = sumN; g_prof.l_mnk[4 * i + 1] = w[0].K; g_prof.l_mnk[4 * i + 2] = (int)rows;
+    g_prof.l_mnk[4 * i + 3] = n;
+    g_prof.l_cls[i] = (MMS_EPI_F16 << 2) | (1 << 10);   // TN operands (bits 0, 1 clear), grouped
   }
   return rc;
 }

@@ -12,8 +12,14 @@
 // (and the layer output) into a caller-owned arena whose layout mms2ut_layer_arena() returns;
 // the backward writes its temporaries (and dx) into a caller-owned scratch block
 // (mms2ut_layer_scratch()) that must stay alive until the side stream has been joined, because
-// the weight-gradient GEMMs read from it; split-K slabs live in caller-owned per-stream
-// workspaces sized by mms2ut_layer_ws().
+// the weight-gradient GEMMs read from it; split-K workspaces (fixups on the main stream, and
+// weight-gradient slabs when a shape rules out the grouped launch) are caller-owned per-stream
+// buffers sized by mms2ut_layer_ws().
+//
+// Weight gradients: the layer's projections (QKV, out-proj, fc1, fc2, + the decoder's
+// cross-attention q / out) are collected during the dgrad chain and issued as ONE grouped, unsplit
+// launch (mms2ut_wgrad_group) on the side stream at the end of the layer's backward — no fp32
+// split-K slabs, no reduction launches; it overlaps the next layer's dgrad chain.
 #include <math.h>
 
 #include <algorithm>
@@ -86,6 +92,12 @@ enum {
 
 int ln_parts(int64_t R, int D) { return mms2ut_layernorm_bwd_nparts(R, D); }
 
+// the grouped weight-gradient launch takes N, K (= d, F) multiples of 8 and row extents a buffer
+// descriptor covers; otherwise each weight gradient is its own split-K launch
+bool group_ok(const Dims& D) {
+  return D.d % 8 == 0 && D.F % 8 == 0 && D.R * 3 * D.d * 2 < (1LL << 31) && D.R * D.F * 2 < (1LL << 31);
+}
+
 void scratch_sizes(const Dims& D, float emit_p, int64_t* sz) {
   const int64_t h = 2, f = 4, Rd = D.R * D.d * h;
   for (int i = 0; i < S_N; ++i) sz[i] = 0;
@@ -124,6 +136,11 @@ struct Ctx {
   float* side_ws;
   int64_t side_ws_floats;
   float* bpart;   // scratch for the bias-gradient fallback partials
+  // the layer's weight gradients, collected for one grouped launch (mms2ut_wgrad_group) at the end
+  // of the layer's backward; grouped = every problem meets the grouped kernel's shape rules
+  mms2ut_wgrad* group;
+  int* ngroup;
+  bool grouped;
 };
 
 int fixup_splits(int64_t M, int64_t N, int64_t K) {
@@ -194,6 +211,10 @@ int fork(const Ctx& c) { return c.side == c.main ? 0 : mms2ut_stream_wait(c.side
 // fp32 split-K slabs with the bias partials as A-row sums, one reduction launch
 int wgrad(const Ctx& c, const mms2ut_half* dy, int64_t lddy, const mms2ut_half* x, int64_t ldx, mms2ut_half* dW,
           mms2ut_half* db, int64_t M, int64_t N, int64_t K) {
+  if (c.grouped) {
+    c.group[(*c.ngroup)++] = mms2ut_wgrad{dy, lddy, x, ldx, dW, db, (int)N, (int)K};
+    return 0;
+  }
   int rc = fork(c);
   if (rc) return rc;
   const int64_t tiles = ((N + 127) / 128) * ((K + 127) / 128);
@@ -287,9 +308,12 @@ extern "C" int mms2ut_layer_ws(const mms2ut_layer* L, int64_t* main_floats, int6
   // forward / dgrad GEMMs (M, N, K)
   fw(R, 3 * d, d); fw(R, d, d); fw(R, F, d); fw(R, d, F);
   fw(R, d, 3 * d); fw(R, F, d); fw(R, d, F);
-  // weight gradients (rows M, out N, in K)
-  ww(R, 3 * d, d); ww(R, d, d); ww(R, F, d); ww(R, d, F);
-  if (D.dec) { fw(R, d, d); ww(R, d, d); }
+  // weight gradients (rows M, out N, in K): split-K slabs only without the grouped launch
+  if (!group_ok(D)) {
+    ww(R, 3 * d, d); ww(R, d, d); ww(R, F, d); ww(R, d, F);
+    if (D.dec) ww(R, d, d);
+  }
+  if (D.dec) fw(R, d, d);
   *main_floats = mw;
   *side_floats = sw;
   return 0;
@@ -366,8 +390,11 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
   layout(ssz, S_N, so);
   void* A = L->saved;
   void* S = G->scratch;
-  const Ctx c{main, side, G->main_ws, G->main_ws_floats, G->side_ws, G->side_ws_floats, at<float>(S, so, S_BPART)};
   const int64_t R = D.R, d = D.d, F = D.F;
+  mms2ut_wgrad group[8];
+  int ngroup = 0;
+  const Ctx c{main, side, G->main_ws, G->main_ws_floats, G->side_ws, G->side_ws_floats, at<float>(S, so, S_BPART),
+              group, &ngroup, group_ok(D)};
   const int hd = L->d / L->H, Dm = (int)d;
   const float pd = L->p_drop;
   int rc;
@@ -427,6 +454,11 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
     if ((rc = wgrad(c, dqkv, 3 * d, H_(MMS_SLOT_H1), d, L->g_w_qkv, L->g_b_qkv, R, 3 * d, d))) return rc;
   }
   // LN1 backward: the layer input's gradient (+ dropout for the layer below when asked)
-  return ln_bwd(c, SH(S_DH1), L->x, L->ln1_g, F_(MMS_SLOT_M1), F_(MMS_SLOT_R1), dxa, SH(S_DX), SH(S_DXD), G->emit_p,
-                G->emit_seed, G->emit_offset, SF(S_P1), L->g_ln1, R, Dm);
+  if ((rc = ln_bwd(c, SH(S_DH1), L->x, L->ln1_g, F_(MMS_SLOT_M1), F_(MMS_SLOT_R1), dxa, SH(S_DX), SH(S_DXD), G->emit_p,
+                   G->emit_seed, G->emit_offset, SF(S_P1), L->g_ln1, R, Dm))) return rc;
+  if (!c.grouped) return 0;
+  // the layer's weight gradients: one grouped launch on the side stream, behind everything the
+  // main stream enqueued for this layer (it overlaps the next layer's dgrad chain)
+  if ((rc = fork(c))) return rc;
+  return mms2ut_wgrad_group(group, ngroup, R, side);
 }

@@ -11,12 +11,13 @@ template <int CPL>
 __global__ void __launch_bounds__(256) ls_xent_fwd_kernel(const h16* __restrict__ z, long ld,
                                                           const int64_t* __restrict__ target, long rows,
                                                           int V, float eps, int pad, float* __restrict__ lse_out,
-                                                          float* __restrict__ loss_out) {
+                                                          float* __restrict__ part) {
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float loss = 0.f, nll = 0.f;
-  // grid-stride over rows: a bounded grid keeps the two same-address float atomics per block few
-  // (one per block for ~3k blocks serialised into a ~70 us tail)
+  // grid-stride over a bounded grid (<= MMS_LS_XENT_PARTS blocks); each block leaves its {loss, nll}
+  // partial, summed in block order by ls_xent_sum_kernel (no float atomics: the loss is
+  // bit-reproducible)
   for (long row = (long)blockIdx.x * 4 + w; row < rows; row += (long)gridDim.x * 4) {
     const h16* zr = z + row * ld;
     float v[CPL][4];
@@ -56,11 +57,19 @@ __global__ void __launch_bounds__(256) ls_xent_fwd_kernel(const h16* __restrict_
   if (lane == 0) { red[0][w] = loss; red[1][w] = nll; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float l = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    const float n = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    atomicAdd(loss_out, l);
-    atomicAdd(loss_out + 1, n);
+    part[blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    part[gridDim.x + blockIdx.x] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
   }
+}
+
+// loss_out[0..1] += the nb block partials, in a fixed order (one wave)
+__global__ void __launch_bounds__(64) ls_xent_sum_kernel(const float* __restrict__ part, int nb,
+                                                         float* __restrict__ loss_out) {
+  float l = 0.f, n = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 64) { l += part[i]; n += part[nb + i]; }
+  l = wave_sum(l);
+  n = wave_sum(n);
+  if (threadIdx.x == 0) { loss_out[0] += l; loss_out[1] += n; }
 }
 
 template <int CPL>
@@ -300,15 +309,20 @@ int pick_cpl_v(int V, F&& f) {
 }  // namespace
 
 extern "C" int mms2ut_ls_xent_fwd(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
-                                  float eps, int pad_idx, float* lse, float* loss_out, hipStream_t s) {
+                                  float eps, int pad_idx, float* lse, float* part, float* loss_out,
+                                  hipStream_t s) {
   MMS_REQUIRE(ld % 4 == 0 && ld >= V, "ls_xent: ld must be a multiple of 4 and >= V");
+  MMS_REQUIRE(part && loss_out, "ls_xent: null partials / loss");
   if (rows == 0) return 0;
-  return pick_cpl_v(V, [&](auto C) {
-    const long nb = std::min<long>((rows + 3) / 4, 512);
+  const int nb = (int)std::min<long>((rows + 3) / 4, MMS_LS_XENT_PARTS);
+  const int rc = pick_cpl_v(V, [&](auto C) {
     hipLaunchKernelGGL((ls_xent_fwd_kernel<decltype(C)::value>), dim3(nb), dim3(256), 0, s,
-                       logits, (long)ld, target, (long)rows, V, eps, pad_idx, lse, loss_out);
+                       logits, (long)ld, target, (long)rows, V, eps, pad_idx, lse, part);
     return mms::check_launch("ls_xent_fwd");
   });
+  if (rc) return rc;
+  hipLaunchKernelGGL(ls_xent_sum_kernel, dim3(1), dim3(64), 0, s, part, nb, loss_out);
+  return mms::check_launch("ls_xent_sum");
 }
 
 extern "C" int mms2ut_ls_xent_bwd(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,

@@ -498,14 +498,42 @@ class _nullctx:
 _NULLCTX = _nullctx()
 
 
+def _group_ok(dy, x, dW):
+    N, K = dy.shape[1], x.shape[1]
+    return (N % 8 == 0 and K % 8 == 0 and dy.stride(0) % 8 == 0 and x.stride(0) % 8 == 0 and
+            dy.stride(1) == 1 and x.stride(1) == 1 and dW.is_contiguous() and
+            all(t.data_ptr() % 16 == 0 for t in (dy, x, dW)) and
+            dy.shape[0] * max(dy.stride(0), x.stride(0)) * 2 < 2 ** 31)
+
+
+def wgrad_group(problems, rows):
+    """One grouped, unsplit weight-gradient launch (include/mms2ut.h mms2ut_wgrad_group):
+    problems = [(dy [rows, N], x [rows, K], dW [N, K], db [N] or None), ...] (<= 8) on the current
+    stream; dW / db overwritten."""
+    arr = (_lib.WgradArgs * len(problems))()
+    for i, (dy, x, dW, db) in enumerate(problems):
+        assert dy.shape[0] == rows and x.shape[0] == rows and tuple(dW.shape) == (dy.shape[1], x.shape[1])
+        assert _group_ok(dy, x, dW), "wgrad_group: shapes / strides / alignment outside the kernel's rules"
+        arr[i] = _lib.WgradArgs(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dW.data_ptr(),
+                                0 if db is None else db.data_ptr(), dy.shape[1], x.shape[1])
+    call("mms2ut_wgrad_group", arr, len(problems), int(rows), _s())
+
+
 def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
-    """dW[N,K] (fp16 view into the flat grad buffer) = dy[M,N]^T @ x[M,K] (split-K over M).
+    """dW[N,K] (fp16 view into the flat grad buffer) = dy[M,N]^T @ x[M,K].
     With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead.
     With db (fp16 [N]) the bias gradient sum_rows dy comes out of the same GEMM: its first column
-    of tiles sums the dy rows it stages anyway (split-K partials, reduced with the slabs)."""
+    of tiles sums the dy rows it stages anyway.  A product with >= 256 output tiles (one per CU)
+    runs unsplit through the grouped kernel (no fp32 slabs); smaller ones split K over the rows
+    into fp32 slabs, reduced by one launch."""
     M, N = dy.shape
     K = x.shape[1]
     assert dW is None or tuple(dW.shape) == (N, K)
+    if accumulate_f32 is None and -(-N // 128) * -(-K // 128) >= 256 and _group_ok(dy, x, dW):
+        ctx = side_begin(dy, x) if side else None
+        with (ctx or _NULLCTX):
+            wgrad_group([(dy, x, dW, db)], M)
+        return dW
     if db is not None and (accumulate_f32 is not None or K % 64 or N % 4):
         linear_wgrad(dy, x, dW, accumulate_f32=accumulate_f32, side=side)
         return bias_grad(dy, db, side=side)
@@ -764,10 +792,15 @@ def copy2d(src, dst, rows, cols):
 # ============================================================================ loss / optimizer
 
 
+LS_XENT_PARTS = 512   # include/mms2ut.h MMS_LS_XENT_PARTS
+
+
 def ls_xent_fwd(logits, ld, target, rows, V, eps, pad, loss_out):
+    """loss_out[0:2] += {label-smoothed loss, nll} (fixed-order sum); returns lse [rows]."""
     lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+    part = _workspace("ls_xent_part", 2 * LS_XENT_PARTS, logits.device)
     call("mms2ut_ls_xent_fwd", logits.data_ptr(), ld, target.data_ptr(), rows, V, float(eps), pad,
-         lse.data_ptr(), loss_out.data_ptr(), _s())
+         lse.data_ptr(), part.data_ptr(), loss_out.data_ptr(), _s())
     return lse
 
 

@@ -326,8 +326,8 @@ def test_layer_arena_layout_queries():
     rows = 4 * 151
     assert offs[K._lib.SLOT_OUT] + 2 * rows * 768 <= nb and offs[K._lib.SLOT_F1] >= 0 and offs[K._lib.SLOT_XB] >= 0
     assert all(o % 256 == 0 for o in offs if o >= 0)
-    assert mw > 0 and sw > 0          # short M: fixups on the main stream, split-K slabs on the side
+    assert mw > 0 and sw == 0         # short M: fixups on the main stream; weight gradients grouped, no slabs
     enc = K.LayerCall(K._lib.LAYER_ENC, 768, 8, 3072, {}, {}, {})
     enc.a.B, enc.a.T = 80, 125
     _, eo, emw, esw, _ = enc.sizes()
-    assert eo[K._lib.SLOT_XB] == -1 and eo[K._lib.SLOT_Q] == -1 and emw == 0 and esw > 0
+    assert eo[K._lib.SLOT_XB] == -1 and eo[K._lib.SLOT_Q] == -1 and emw == 0 and esw == 0

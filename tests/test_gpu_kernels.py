@@ -404,6 +404,35 @@ def test_glu_im2col_col2im(K):
     assert rel(dh, hf.grad) < 3e-3
 
 
+@pytest.mark.parametrize("rows", [9000, 777, 1, 0])
+def test_wgrad_group(K, rows):
+    """One grouped launch == each product in fp32 (encoder-layer shapes, ragged N / K multiples of
+    8, one problem without a bias, strided dy / x views as the layer scratch holds them); rows = 0
+    writes zeros.  Deterministic: a second launch is bit-identical."""
+    g = torch.Generator(device="cuda").manual_seed(rows)
+    shapes = [(2304, 768, True), (768, 768, True), (3072, 768, True), (768, 3072, True), (200, 136, False)]
+    probs = []
+    for N, K_, bias in shapes:
+        dyb = (torch.randn(rows, N + 8, device="cuda", generator=g) * 0.1).half()
+        xb = torch.randn(rows, K_ + 16, device="cuda", generator=g).half()
+        dW = torch.full((N, K_), 7.0, dtype=torch.float16, device="cuda")
+        db = torch.full((N,), 7.0, dtype=torch.float16, device="cuda") if bias else None
+        probs.append((dyb[:, :N], xb[:, :K_], dW, db))
+    K.wgrad_group(probs, rows)
+    first = [p[2].clone() for p in probs]
+    K.wgrad_group(probs, rows)
+    torch.cuda.synchronize()
+    for (dy, x, dW, db), f in zip(probs, first):
+        assert torch.equal(dW, f)
+        ref = dy.float().t() @ x.float()
+        if rows == 0:
+            assert not dW.any() and (db is None or not db.any())
+            continue
+        assert rel(dW, ref) < 2e-3
+        if db is not None:
+            assert rel(db, dy.float().sum(0)) < 2e-3
+
+
 @pytest.mark.parametrize("M,N,K_", [(5000, 96, 256), (8704, 768, 768), (1000, 200, 64), (77, 2304, 128)])
 def test_wgrad_fused_bias(K, M, N, K_):
     """dW and db from one GEMM launch (db = the A-row sums of the first tile column)."""
