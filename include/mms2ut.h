@@ -90,7 +90,9 @@ int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
  * x[rows, K] (fp16, row stride K, overwritten) and, when db != NULL, db[N] = column sums of dy —
  * all in ONE launch over the union of the problems' 128x128 tiles, unsplit (fp32 accumulation over
  * all rows, no split-K slabs).  lddy, ldx multiples of 8; N, K multiples of 8; dy, x, dW 16-B
- * aligned.  Deterministic (fixed reduction order per tile).                                      */
+ * aligned.  Deterministic (fixed reduction order per tile).  max_blocks > 0 caps the grid
+ * (rounded down to a multiple of 8): blocks then walk the tiles persistently, so a launch on a
+ * side stream never holds more than that many block slots (0: one block per tile).            */
 typedef struct mms2ut_wgrad {
   const mms2ut_half* dy;
   int64_t lddy;
@@ -100,7 +102,7 @@ typedef struct mms2ut_wgrad {
   mms2ut_half* db;
   int N, K;
 } mms2ut_wgrad;
-int mms2ut_wgrad_group(const mms2ut_wgrad* w, int n, int64_t rows, hipStream_t stream);
+int mms2ut_wgrad_group(const mms2ut_wgrad* w, int n, int64_t rows, int max_blocks, hipStream_t stream);
 
 /* live GEMM timing for the benchmark roofline: between begin/end every mms2ut_gemm_f16 launch
  * is bracketed by HIP events on its own stream (or, in stamp mode below, timed by its own
@@ -430,12 +432,14 @@ int mms2ut_kv_cache_gather(const mms2ut_half* src, mms2ut_half* dst, const int64
  * (data-config feature transform) and zero-padded fp16 collation [B][Tmax][nbins]
  * (_collate_frames).  wave: concatenated fp32 samples (x 2^15), wave_off[B+1].              */
 int mms2ut_fbank_frames(const int64_t* wave_off, int B, int32_t* n_frames_out, hipStream_t stream);
-/* mel_range[2*m], mel_range[2*m+1]: first / one-past-last nonzero FFT bin of filter m */
+/* mel_range[2*m], mel_range[2*m+1]: first / one-past-last nonzero FFT bin of filter m; at most
+ * 1024 nonzero weights over all filters (80 Kaldi bins: ~510)                                  */
 int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, const int32_t* frame_off, int B,
                      int total_frames, const float* mel_banks, const int32_t* mel_range, int nbins,
                      float* feats, hipStream_t stream);
+/* stats: caller-owned fp32 workspace [B][2][nbins] (per-utterance mean, std)                   */
 int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
-                              int nbins, int cmvn, mms2ut_half* out, hipStream_t stream);
+                              int nbins, int cmvn, float* stats, mms2ut_half* out, hipStream_t stream);
 /* fairseq SpecAugmentTransform (feature_transforms/specaugment.py, the `specaugment` entry of
  * the data config's `_train` transforms, applied after utterance_cmvn by
  * speech_to_speech_dataset.py:271-272), in place on the collated features x [B][Tmax][nbins].
@@ -508,6 +512,8 @@ typedef struct mms2ut_layer_grad {
   int64_t main_ws_floats;
   float* side_ws;
   int64_t side_ws_floats;
+  int side_blocks;                /* grid cap of the grouped weight-gradient launch on the side   */
+                                  /* stream (mms2ut_wgrad_group max_blocks; 0 = one per tile)      */
 } mms2ut_layer_grad;
 
 /* arena size (and the byte offset of every MMS_SLOT_*, -1 for slots the kind does not use)     */

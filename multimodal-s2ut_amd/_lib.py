@@ -44,7 +44,9 @@ def _packer(st):
     packing all fields in one call costs ~2 us where ~45 ctypes attribute stores cost ~10 us, and
     the training step issues a few hundred GEMMs per step from Python."""
     code = {vp: "P", i32: "i", i64: "q", f32: "f", u64: "Q"}
-    S = struct.Struct("@" + "".join(code[t] for _, t in st._fields_))
+    fmt = "@" + "".join(code[t] for _, t in st._fields_)
+    tail = C.sizeof(st) - struct.calcsize(fmt)          # the C struct's trailing alignment padding
+    S = struct.Struct(fmt + (f"{tail}x" if tail > 0 else ""))
     assert S.size == C.sizeof(st), (S.size, C.sizeof(st))
     return S
 
@@ -99,7 +101,7 @@ class LayerGradArgs(C.Structure):
     """mms2ut_layer_grad (include/mms2ut.h)."""
     _fields_ = [("dy", vp), ("dy_drop", vp), ("emit_p", f32), ("emit_seed", u64), ("emit_offset", u64),
                 ("dkv", vp), ("ld_dkv", i64), ("scratch", vp), ("main_ws", vp), ("main_ws_floats", i64),
-                ("side_ws", vp), ("side_ws_floats", i64)]
+                ("side_ws", vp), ("side_ws_floats", i64), ("side_blocks", i32)]
 
 
 LAYER_GRAD_ARGS = _packer(LayerGradArgs)
@@ -110,7 +112,7 @@ SIGNATURES = {
     "mms2ut_last_error": (C.c_char_p, []),
     "mms2ut_version": (i32, []),
     "mms2ut_gemm_f16": (i32, [vp, vp]),   # GEMM_ARGS.pack(...) bytes or C.byref(GemmArgs)
-    "mms2ut_wgrad_group": (i32, [vp, i32, i64, vp]),
+    "mms2ut_wgrad_group": (i32, [vp, i32, i64, i32, vp]),
     "mms2ut_profile_begin": (i32, [i32]),
     "mms2ut_profile_end": (i32, [C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
     "mms2ut_profile_bytes": (i32, [C.POINTER(C.c_double)]),
@@ -171,7 +173,7 @@ SIGNATURES = {
     "mms2ut_adam_fp16_master": (i32, [vp, vp, vp, vp, vp, i64, vp, f32, f32, f32, f32, vp]),
     "mms2ut_fbank_frames": (i32, [vp, i32, vp, vp]),
     "mms2ut_fbank_f32": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
-    "mms2ut_fbank_cmvn_collate": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "mms2ut_fbank_cmvn_collate": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     "mms2ut_specaugment_f16": (i32, [vp, vp, i32, i32, i32, vp, i32, i32, i32, f32, vp]),
     "mms2ut_layer_arena": (i32, [vp, vp, vp]),
     "mms2ut_layer_scratch": (i32, [vp, f32, vp, vp]),

@@ -1,9 +1,15 @@
 // Kaldi-compatible 80-bin log-mel filterbank (torchaudio.compliance.kaldi.fbank defaults, the
 // path the reference's get_fbank takes: mm_s2ut/data/audio_utils.py:326-349) + utterance CMVN +
-// zero-padded fp16 collation.  One wave per 25 ms frame: DC removal and pre-emphasis through
-// LDS, povey window, 512-point radix-2 complex FFT in LDS (twiddles from a table), power
-// spectrum, sparse triangular mel filters, log(max(x, FLT_EPSILON)).  HBM-bound: 640 B of wave
-// read (400 samples, hop 160 -> 4 B/sample amortised) + 320 B of features written per frame.
+// zero-padded fp16 collation.
+//
+// fbank_kernel: one wave per 25 ms frame, FPW frames per wave in turn, 4 waves per block.  DC
+// removal and pre-emphasis, povey window, then the 512-point real FFT as a 256-point complex FFT
+// of the even/odd sample pairs (z[n] = x[2n] + i x[2n+1]; radix-4, four in-place LDS stages, one
+// butterfly of 4 points per lane) and the standard split X[k] = E[k] + W^k O[k]; power spectrum,
+// triangular mel filters from a compact per-block LDS copy of their nonzero weights,
+// log(max(x, FLT_EPSILON)).  Twiddles, window and mel weights are staged in LDS once per block.
+// HBM-bound: 640 B of wave read (400 samples, hop 160 -> 4 B/sample amortised) + 4 * nbins B of
+// features written per frame.
 #include <algorithm>
 
 #include "common.h"
@@ -12,96 +18,159 @@
 namespace {
 
 constexpr int WIN = 400, SHIFT = 160, NFFT = 512, NBIN = 257;
+constexpr int NC = 256;                        // complex FFT points (the real 512-point FFT's half)
+constexpr int FPW = 4, FB_WAVES = 4, FPB = FPW * FB_WAVES;
+constexpr int MELW_MAX = 1024;                 // nonzero mel weights staged per block (80 bins: ~510)
 
 struct FbankConst {
   float window[WIN];
-  float tw_re[NFFT / 2], tw_im[NFFT / 2];
+  float tw_re[NFFT / 2], tw_im[NFFT / 2];      // exp(-2 pi i k / 512), k < 256
 };
 
 __constant__ FbankConst c_fb;
 static bool g_fb_init = false;
 
-MMS_DEV int bitrev9(int x) { return (int)(__builtin_bitreverse32((unsigned)x) >> 23); }
+// base-4 digit reversal of an 8-bit index (256 = 4^4)
+MMS_DEV int rev4(int x) { return ((x & 3) << 6) | ((x & 12) << 2) | ((x & 48) >> 2) | ((x & 192) >> 6); }
 
-__global__ void __launch_bounds__(256) fbank_kernel(const float* __restrict__ wave, const int64_t* __restrict__ wave_off,
-                                                    const int* __restrict__ frame_off, int B, int total,
-                                                    const float* __restrict__ banks,
-                                                    const int* __restrict__ mel_range, int nbins,
-                                                    float* __restrict__ feats) {
-  __shared__ float s_re[4][NFFT], s_im[4][NFFT], s_x[4][WIN + 4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int f = blockIdx.x * 4 + w;
-  if (f >= total) return;
-  // utterance of this frame (binary search over frame_off)
-  int lo = 0, hi = B;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (frame_off[mid] <= f) lo = mid; else hi = mid;
-  }
-  const int b = lo;
-  const int t = f - frame_off[b];
-  const float* src = wave + wave_off[b] + (long)t * SHIFT;
-  float* X = s_x[w];
-  float* re = s_re[w];
-  float* im = s_im[w];
-  float sum = 0.f;
-  for (int j = lane; j < WIN; j += 64) { const float v = src[j]; X[j] = v; sum += v; }
-  const float mean = wave_sum(sum) / WIN;
+struct FbankSmem {
+  float tw_re[NFFT / 2], tw_im[NFFT / 2];
+  float win[WIN];
+  float melw[MELW_MAX];
+  int mlo[256], mlen[256], moff[256];
+  float x[FB_WAVES][WIN];
+  float zr[FB_WAVES][NC], zi[FB_WAVES][NC];
+  float pw[FB_WAVES][NBIN + 3];
+};
+
+// exp(-2 pi i j / 512) for 0 <= j < 512 from the half table (W^(j+256) = -W^j)
+MMS_DEV void tw512(const FbankSmem& S, int j, float& c, float& s) {
+  const int jj = j & 255;
+  const float sg = (j & 256) ? -1.f : 1.f;
+  c = sg * S.tw_re[jj];
+  s = sg * S.tw_im[jj];
+}
+
+MMS_DEV void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // pre-emphasis (replicate-pad at j=0), window, scatter into bit-reversed order
-  for (int j = lane; j < NFFT; j += 64) {
-    float v = 0.f;
-    if (j < WIN) {
-      const float xj = X[j] - mean;
-      const float xp = (j > 0 ? X[j - 1] : X[0]) - mean;
-      v = (xj - 0.97f * xp) * c_fb.window[j];
+}
+
+__global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __restrict__ wave,
+                                                              const int64_t* __restrict__ wave_off,
+                                                              const int* __restrict__ frame_off, int B, int total,
+                                                              const float* __restrict__ banks,
+                                                              const int* __restrict__ mel_range, int nbins,
+                                                              float* __restrict__ feats) {
+  __shared__ FbankSmem S;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // per-block tables: twiddles, window, and the mel filters' nonzero weights (compact, prefix offsets)
+  for (int i = tid; i < NFFT / 2; i += blockDim.x) { S.tw_re[i] = c_fb.tw_re[i]; S.tw_im[i] = c_fb.tw_im[i]; }
+  for (int i = tid; i < WIN; i += blockDim.x) S.win[i] = c_fb.window[i];
+  if (tid == 0) {
+    int o = 0;
+    for (int m = 0; m < nbins; ++m) {
+      const int lo = mel_range[2 * m], hi = mel_range[2 * m + 1];
+      S.mlo[m] = lo;
+      S.mlen[m] = hi - lo;
+      S.moff[m] = o;
+      o += hi - lo;
     }
-    const int r = bitrev9(j);
-    re[r] = v;
-    im[r] = 0.f;
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // iterative radix-2 DIT, 9 stages, 256 butterflies per stage (4 per lane)
-  for (int s = 1; s <= 9; ++s) {
-    const int half = 1 << (s - 1);
-    const int tstride = NFFT >> s;  // twiddle index stride
-    float ar[4], ai[4], br[4], bi[4];
-    int i0s[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int bfly = lane + q * 64;
-      const int grp = bfly >> (s - 1), k = bfly & (half - 1);
-      const int i0 = grp * (half << 1) + k;
-      i0s[q] = i0;
-      const float wr = c_fb.tw_re[k * tstride], wi = c_fb.tw_im[k * tstride];
-      const float xr = re[i0 + half], xi = im[i0 + half];
-      const float tr = wr * xr - wi * xi, ti = wr * xi + wi * xr;
-      const float ur = re[i0], ui = im[i0];
-      ar[q] = ur + tr; ai[q] = ui + ti; br[q] = ur - tr; bi[q] = ui - ti;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      re[i0s[q]] = ar[q]; im[i0s[q]] = ai[q];
-      re[i0s[q] + half] = br[q]; im[i0s[q] + half] = bi[q];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
-  // power spectrum into X (reuse), bins 0..256
-  for (int k = lane; k < NBIN; k += 64) X[k] = re[k] * re[k] + im[k] * im[k];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __syncthreads();
+  for (int m = 0; m < nbins; ++m)
+    for (int j = tid; j < S.mlen[m]; j += blockDim.x) S.melw[S.moff[m] + j] = banks[(long)m * NBIN + S.mlo[m] + j];
+  __syncthreads();
+  float* X = S.x[w];
+  float* zr = S.zr[w];
+  float* zi = S.zi[w];
+  float* P = S.pw[w];
   const float flt_eps = 1.1920928955078125e-07f;
-  for (int m = lane; m < nbins; m += 64) {
-    const float* bk = banks + (long)m * NBIN;
-    float acc = 0.f;
-    const int k0 = mel_range[2 * m], k1 = mel_range[2 * m + 1];  // triangle support only
-    for (int k = k0; k < k1; ++k) acc += bk[k] * X[k];
-    feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
+  for (int i = 0; i < FPW; ++i) {
+    const int f = blockIdx.x * FPB + w * FPW + i;
+    if (f >= total) break;
+    // utterance of this frame (binary search over frame_off)
+    int lo = 0, hi = B;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (frame_off[mid] <= f) lo = mid; else hi = mid;
+    }
+    const float* src = wave + wave_off[lo] + (long)(f - frame_off[lo]) * SHIFT;
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int j = lane + 64 * q;
+      if (j < WIN) { const float v = src[j]; X[j] = v; sum += v; }
+    }
+    const float mean = wave_sum(sum) * (1.f / WIN);
+    wave_sync();
+    // pre-emphasis (replicate-pad at j = 0), window, zero pad to 512; pairs -> digit-reversed slots
+#pragma unroll
+    for (int q = 0; q < NC / 64; ++q) {
+      const int n = lane + 64 * q;
+      float v[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * n + e;
+        v[e] = 0.f;
+        if (j < WIN) {
+          const float xj = X[j] - mean;
+          const float xp = (j > 0 ? X[j - 1] : X[0]) - mean;
+          v[e] = (xj - 0.97f * xp) * S.win[j];
+        }
+      }
+      const int r = rev4(n);
+      zr[r] = v[0];
+      zi[r] = v[1];
+    }
+    wave_sync();
+    // radix-4 DIT: stage L combines four length-L DFTs into one of length 4L; lane = butterfly
+#pragma unroll
+    for (int L = 1; L < NC; L <<= 2) {
+      const int k = lane & (L - 1), base = (lane - k) * 4 + k;
+      float ar[4], ai[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ar[q] = zr[base + q * L];
+        ai[q] = zi[base + q * L];
+      }
+      // b_q = W_{4L}^{qk} a_q, W_{4L} = W_512^(128 / L)
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        float c, s;
+        tw512(S, (q * k * (128 / L)) & 511, c, s);
+        const float r = ar[q] * c - ai[q] * s, im = ar[q] * s + ai[q] * c;
+        ar[q] = r;
+        ai[q] = im;
+      }
+      const float s0r = ar[0] + ar[2], s0i = ai[0] + ai[2], d0r = ar[0] - ar[2], d0i = ai[0] - ai[2];
+      const float s1r = ar[1] + ar[3], s1i = ai[1] + ai[3], d1r = ar[1] - ar[3], d1i = ai[1] - ai[3];
+      zr[base] = s0r + s1r;            zi[base] = s0i + s1i;            // y0 = b0 + b1 + b2 + b3
+      zr[base + L] = d0r + d1i;        zi[base + L] = d0i - d1r;        // y1 = b0 - i b1 - b2 + i b3
+      zr[base + 2 * L] = s0r - s1r;    zi[base + 2 * L] = s0i - s1i;    // y2 = b0 - b1 + b2 - b3
+      zr[base + 3 * L] = d0r - d1i;    zi[base + 3 * L] = d0i + d1r;    // y3 = b0 + i b1 - b2 - i b3
+      wave_sync();
+    }
+    // real-FFT split: X[k] = E + W_512^k O, E = (Z[k] + conj Z[256-k]) / 2, O = -i (Z[k] - conj Z[256-k]) / 2
+    for (int k = lane; k < NBIN; k += 64) {
+      const int a = k & (NC - 1), b = (NC - k) & (NC - 1);
+      const float zkr = zr[a], zki = zi[a], znr = zr[b], zni = zi[b];
+      const float er = 0.5f * (zkr + znr), ei = 0.5f * (zki - zni);
+      const float orr = 0.5f * (zki + zni), oi = -0.5f * (zkr - znr);
+      float c, s;
+      tw512(S, k, c, s);
+      const float xr = er + (orr * c - oi * s), xi = ei + (orr * s + oi * c);
+      P[k] = xr * xr + xi * xi;
+    }
+    wave_sync();
+    for (int m = lane; m < nbins; m += 64) {
+      const float* wm = S.melw + S.moff[m];
+      const float* pm = P + S.mlo[m];
+      float acc = 0.f;
+      for (int j = 0; j < S.mlen[m]; ++j) acc += wm[j] * pm[j];
+      feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
+    }
+    wave_sync();
   }
 }
 
@@ -112,55 +181,63 @@ __global__ void fbank_frames_kernel(const int64_t* wave_off, int B, int* n_frame
   n_frames[b] = n < WIN ? 0 : (int)(1 + (n - WIN) / SHIFT);
 }
 
-constexpr int CMVN_CHUNK = 64;  // frames staged in LDS per round (64 x 256 x 4 B = 64 KiB max)
-
-__global__ void __launch_bounds__(256) cmvn_collate_kernel(const float* __restrict__ feats, const int* __restrict__ frame_off,
-                                    int B, int Tmax, int nbins, int cmvn, h16* __restrict__ out) {
+// fairseq UtteranceCMVN (numpy float32: mean over time, var = E[x^2] - mean^2,
+// std = sqrt(max(var, 1e-10)), x = (x - mean) / std).  cmvn_stats_kernel: one block per utterance,
+// thread t sums column t % nbins over the rows r = t / nbins (mod the row groups) in fp64, the
+// groups combined in a fixed order (deterministic; fp64 leaves only the reference's own fp32
+// cancellation error, which the parity test bounds) -> stats[b] = {mean[nbins], std[nbins]}.
+__global__ void __launch_bounds__(256) cmvn_stats_kernel(const float* __restrict__ feats, const int* __restrict__ frame_off,
+                                                         int nbins, int cmvn, float* __restrict__ stats) {
   const int b = blockIdx.x;
   const int f0 = frame_off[b], T = frame_off[b + 1] - f0;
-  __shared__ float s_mean[256], s_std[256];
-  __shared__ __attribute__((aligned(16))) float s_chunk[CMVN_CHUNK * 256];
-  // fairseq UtteranceCMVN in numpy float32: x.mean(0) and (x**2).sum(0) reduce over the outer
-  // (time) axis sequentially, var = sq/T - mean^2 (float32 cancellation included, as the
-  // reference), std = sqrt(max(var, 1e-10)), x = (x - mean) / std.
-  // The sums keep that sequential order per column; the frames are staged CMVN_CHUNK at a time
-  // into LDS by all threads with coalesced 16-B loads, so the per-column chains read LDS instead
-  // of waiting out one global round trip per frame.
-  float sm = 0.f, sq = 0.f;
-  const int c = threadIdx.x;
-  for (int t0 = 0; t0 < T; t0 += CMVN_CHUNK) {
-    const int nt = min(CMVN_CHUNK, T - t0);
-    const int nv = nt * nbins / 4;  // nbins % 4 == 0 (host check)
-    const f32x4* src = reinterpret_cast<const f32x4*>(feats + (long)(f0 + t0) * nbins);
-    for (int i = threadIdx.x; i < nv; i += blockDim.x) reinterpret_cast<f32x4*>(s_chunk)[i] = src[i];
-    __syncthreads();
-    if (c < nbins) {
-      for (int t = 0; t < nt; ++t) {
-        const float v = s_chunk[t * nbins + c];
-        sm = __fadd_rn(sm, v);
-        sq = __fadd_rn(sq, __fmul_rn(v, v));
-      }
+  const int groups = blockDim.x / nbins;          // >= 1 (nbins <= 256)
+  const int c = threadIdx.x % nbins, g = threadIdx.x / nbins;
+  __shared__ double s_sum[256], s_sq[256];
+  double sm = 0.0, sq = 0.0;
+  if (g < groups) {
+    const float* col = feats + (long)f0 * nbins + c;
+    for (int t = g; t < T; t += groups) {
+      const double v = col[(long)t * nbins];
+      sm += v;
+      sq += v * v;
     }
-    __syncthreads();
   }
-  if (c < nbins) {
-    const float mean = T > 0 ? __fdiv_rn(sm, (float)T) : 0.f;
-    const float var = T > 0 ? __fsub_rn(__fdiv_rn(sq, (float)T), __fmul_rn(mean, mean)) : 1.f;
-    s_mean[c] = cmvn ? mean : 0.f;
-    s_std[c] = cmvn ? __fsqrt_rn(fmaxf(var, 1e-10f)) : 1.f;
-  }
+  s_sum[threadIdx.x] = sm;
+  s_sq[threadIdx.x] = sq;
   __syncthreads();
-  // normalise + collate, 4 consecutive bins per thread (16-B loads, 8-B stores)
-  const long n = (long)Tmax * nbins;
-  for (long i = 4 * threadIdx.x; i < n; i += 4 * blockDim.x) {
-    const int t = (int)(i / nbins), c = (int)(i % nbins);
+  if (threadIdx.x < nbins) {
+    double a = 0.0, q = 0.0;
+    for (int k = 0; k < groups; ++k) { a += s_sum[k * nbins + threadIdx.x]; q += s_sq[k * nbins + threadIdx.x]; }
+    float mean = 0.f, sd = 1.f;
+    if (cmvn && T > 0) {
+      const double mu = a / T;
+      mean = (float)mu;
+      sd = (float)sqrt(fmax(q / T - mu * mu, 1e-10));
+    }
+    stats[(long)b * 2 * nbins + threadIdx.x] = mean;
+    stats[(long)b * 2 * nbins + nbins + threadIdx.x] = sd;
+  }
+}
+
+// normalise + collate [B][Tmax][nbins] fp16 (zero rows past each utterance's length): a flat
+// grid-stride pass, 4 consecutive bins per thread (16-B loads, 8-B stores)
+__global__ void __launch_bounds__(256) cmvn_apply_kernel(const float* __restrict__ feats, const int* __restrict__ frame_off,
+                                                         int B, int Tmax, int nbins, const float* __restrict__ stats,
+                                                         h16* __restrict__ out) {
+  const long per = (long)Tmax * nbins / 4, n4 = (long)B * per;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / per);
+    const long e = (i - (long)b * per) * 4;
+    const int t = (int)(e / nbins), c = (int)(e % nbins);
+    const int f0 = frame_off[b], T = frame_off[b + 1] - f0;
     h16x4 o = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
     if (t < T) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(feats + (long)(f0 + t) * nbins + c);
+      const float* st = stats + (long)b * 2 * nbins;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (h16)__fdiv_rn(__fsub_rn(v[e], s_mean[c + e]), s_std[c + e]);
+      for (int k = 0; k < 4; ++k) o[k] = (h16)((v[k] - st[c + k]) / st[nbins + c + k]);
     }
-    *reinterpret_cast<h16x4*>(out + (long)b * n + i) = o;
+    *reinterpret_cast<h16x4*>(out + (long)b * Tmax * nbins + e) = o;
   }
 }
 
@@ -256,18 +333,23 @@ extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, cons
   MMS_REQUIRE(mel_range != nullptr, "fbank: mel_range required");
   if (init_consts(s)) return 1;
   if (total_frames == 0) return 0;
-  hipLaunchKernelGGL(fbank_kernel, dim3((total_frames + 3) / 4), dim3(256), 0, s, wave, wave_off, frame_off, B,
-                     total_frames, mel_banks, mel_range, nbins, feats);
+  hipLaunchKernelGGL(fbank_kernel, dim3((total_frames + FPB - 1) / FPB), dim3(64 * FB_WAVES), 0, s, wave, wave_off,
+                     frame_off, B, total_frames, mel_banks, mel_range, nbins, feats);
   return mms::check_launch("fbank");
 }
 
 extern "C" int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
-                                         int nbins, int cmvn, h16* out, hipStream_t s) {
-  MMS_REQUIRE(nbins <= 256 && nbins % 4 == 0, "cmvn: nbins must be a multiple of 4, <= 256");
-  MMS_REQUIRE(((uintptr_t)feats & 15) == 0 && ((uintptr_t)out & 7) == 0, "cmvn: feats / out misaligned");
+                                         int nbins, int cmvn, float* stats, h16* out, hipStream_t s) {
+  MMS_REQUIRE(nbins > 0 && nbins <= 256 && nbins % 4 == 0, "cmvn: nbins must be a multiple of 4, <= 256");
+  MMS_REQUIRE(((uintptr_t)feats & 15) == 0 && ((uintptr_t)out & 7) == 0 && stats, "cmvn: feats / out misaligned");
   if (B == 0) return 0;
-  hipLaunchKernelGGL(cmvn_collate_kernel, dim3(B), dim3(256), 0, s, feats, frame_off, B, Tmax, nbins, cmvn, out);
-  return mms::check_launch("fbank_cmvn_collate");
+  hipLaunchKernelGGL(cmvn_stats_kernel, dim3(B), dim3(256), 0, s, feats, frame_off, nbins, cmvn, stats);
+  if (int rc = mms::check_launch("cmvn_stats")) return rc;
+  const long n4 = (long)B * Tmax * nbins / 4;
+  if (n4 == 0) return 0;
+  hipLaunchKernelGGL(cmvn_apply_kernel, dim3((unsigned)std::min<long>((n4 + 255) / 256, 4096)), dim3(256), 0, s,
+                     feats, frame_off, B, Tmax, nbins, stats, out);
+  return mms::check_launch("cmvn_apply");
 }
 
 extern "C" int mms2ut_specaugment_f16(h16* x, const int32_t* frame_off, int B, int Tmax, int nbins,

@@ -777,20 +777,27 @@ struct GemmGroup {
   unsigned long long* stamps;
 };
 
+// A capped grid (gridDim.x < total, a multiple of 8) walks the tiles persistently: block b takes
+// linear tiles b, b + grid, ... — on the side stream the weight gradients then hold at most that
+// many of the CUs' block slots, and the critical path's GEMMs keep the rest.
 __global__ void __launch_bounds__(NT, 2) gemm_group_wgrad_kernel(GemmGroup G, int total) {
   const unsigned long long t_start = G.stamps ? stamp_now() : 0ull;
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
-  const int q = total / 8, r = total % 8, x = blockIdx.x % 8;
-  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
-  int g = 0;
-  while (g + 1 < G.n && id >= G.first[g + 1]) ++g;
-  const GemmP& P = G.p[g];
-  const int t = id - G.first[g], tiles_n = G.tiles_n[g];
-  const int per_group = P.group_m * tiles_n;
-  const int grp = t / per_group, first_m = grp * P.group_m;
-  const int gsize = min(G.tiles_m[g] - first_m, P.group_m);
-  const int w = t % per_group;
-  dma_gemm_tile<false, false, MMS_EPI_F16, 2, true, false>(P, smem, 0, first_m + w % gsize, w / gsize);
+  const int q = total / 8, r = total % 8;
+  for (int lin = blockIdx.x; lin < total; lin += gridDim.x) {
+    if (lin != (int)blockIdx.x) __syncthreads();   // the previous tile's epilogue is done with the ring
+    const int x = lin % 8;
+    const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lin / 8;
+    int g = 0;
+    while (g + 1 < G.n && id >= G.first[g + 1]) ++g;
+    const GemmP& P = G.p[g];
+    const int t = id - G.first[g], tiles_n = G.tiles_n[g];
+    const int per_group = P.group_m * tiles_n;
+    const int grp = t / per_group, first_m = grp * P.group_m;
+    const int gsize = min(G.tiles_m[g] - first_m, P.group_m);
+    const int w = t % per_group;
+    dma_gemm_tile<false, false, MMS_EPI_F16, 2, true, false>(P, smem, 0, first_m + w % gsize, w / gsize);
+  }
   stamp_end(G.stamps, t_start);
 }
 
@@ -1184,7 +1191,7 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   return rc;
 }
 
-static int wgrad_group_dispatch(const mms2ut_wgrad* w, int n, int64_t rows, hipStream_t stream) {
+static int wgrad_group_dispatch(const mms2ut_wgrad* w, int n, int64_t rows, int max_blocks, hipStream_t stream) {
   MMS_REQUIRE(w && n >= 1 && n <= kGroupMax, "wgrad_group: need 1..%d problems", kGroupMax);
   MMS_REQUIRE(rows >= 0, "wgrad_group: rows < 0");
   GemmGroup G{};
@@ -1228,22 +1235,24 @@ static int wgrad_group_dispatch(const mms2ut_wgrad* w, int n, int64_t rows, hipS
     }
     return 0;
   }
-  G.stamps = stamp_take(total);
-  hipLaunchKernelGGL(gemm_group_wgrad_kernel, dim3(total), dim3(NT), 0, stream, G, total);
+  int grid = total;
+  if (max_blocks > 0 && max_blocks < total) grid = std::max(8, max_blocks / 8 * 8);
+  G.stamps = stamp_take(grid);
+  hipLaunchKernelGGL(gemm_group_wgrad_kernel, dim3(grid), dim3(NT), 0, stream, G, total);
   return mms::check_launch("gemm_group_wgrad");
 }
 
-extern "C" int mms2ut_wgrad_group(const mms2ut_wgrad* w, int n, int64_t rows, hipStream_t stream) {
-  if (!g_prof.on || g_prof.n >= g_prof.cap) return wgrad_group_dispatch(w, n, rows, stream);
+extern "C" int mms2ut_wgrad_group(const mms2ut_wgrad* w, int n, int64_t rows, int max_blocks, hipStream_t stream) {
+  if (!g_prof.on || g_prof.n >= g_prof.cap) return wgrad_group_dispatch(w, n, rows, max_blocks, stream);
   const int i = g_prof.n++;
   int rc;
   if (g_prof.stamps) {
     g_prof.l_blk[2 * i] = g_prof.cursor;
-    rc = wgrad_group_dispatch(w, n, rows, stream);
+    rc = wgrad_group_dispatch(w, n, rows, max_blocks, stream);
     g_prof.l_blk[2 * i + 1] = g_prof.cursor;
   } else {
     hipEventRecord(g_prof.ev[2 * i], stream);
-    rc = wgrad_group_dispatch(w, n, rows, stream);
+    rc = wgrad_group_dispatch(w, n, rows, max_blocks, stream);
     hipEventRecord(g_prof.ev[2 * i + 1], stream);
   }
   if (w && n > 0) {

@@ -460,5 +460,5 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
   // the layer's weight gradients: one grouped launch on the side stream, behind everything the
   // main stream enqueued for this layer (it overlaps the next layer's dgrad chain)
   if ((rc = fork(c))) return rc;
-  return mms2ut_wgrad_group(group, ngroup, R, side);
+  return mms2ut_wgrad_group(group, ngroup, R, side == main ? 0 : G->side_blocks, side);
 }

@@ -124,6 +124,8 @@ class FbankFrontend:
         hi = banks.shape[1] - nz[:, ::-1].argmax(1)
         lo[~nz.any(1)] = hi[~nz.any(1)] = 0
         rng = np.stack([lo, hi], 1).astype(np.int32)
+        if int((hi - lo).sum()) > 1024:
+            raise ValueError("fbank: more than 1024 nonzero mel weights (include/mms2ut.h mms2ut_fbank_f32)")
         self.mel_range = torch.from_numpy(rng.reshape(-1)).to(self.device)
 
     def upload(self, waves, pin=False):

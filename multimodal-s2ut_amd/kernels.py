@@ -324,9 +324,10 @@ class LayerCall:
         o = offsets[slot]
         return arena[o:o + n * torch.tensor([], dtype=dtype).element_size()].view(dtype).view(shape)
 
-    def bwd(self, snap, arena, dy, R, dy_drop=None, emit=None, dkv=None):
+    def bwd(self, snap, arena, dy, R, dy_drop=None, emit=None, dkv=None, last=False):
         """Backward of the forward whose argument snapshot is ``snap``.  emit = (p, (seed, offset)):
-        also return dropout(dx) for the layer below.  Returns (dx, dropout(dx) or dx)."""
+        also return dropout(dx) for the layer below.  last: nothing follows on the critical path
+        (the weight gradients may take the whole chip).  Returns (dx, dropout(dx) or dx)."""
         emit_p, (emit_seed, emit_off) = (emit[0], emit[1]) if emit is not None and emit[0] > 0 else (0.0, (0, 0))
         nb, offsets, mw, sw, scr = self.sizes()
         sk = emit_p > 0
@@ -353,12 +354,13 @@ class LayerCall:
             dy.data_ptr(), 0 if dy_drop is None else dy_drop.data_ptr(), float(emit_p), int(emit_seed),
             int(emit_off), 0 if dkv is None else dkv.data_ptr(), 0 if dkv is None else dkv.stride(0),
             scratch.data_ptr(), 0 if main_ws is None else main_ws.data_ptr(), mw,
-            0 if side_ws is None else side_ws.data_ptr(), sw)
+            0 if side_ws is None else side_ws.data_ptr(), sw, 0 if last else SIDE_WGRAD_BLOCKS)
         call("mms2ut_layer_bwd", snap, g, _s(), side)
         if side:
-            # the side stream reads the arena (saved activations) and the scratch: keep both until
-            # side_join; nothing else may reuse them before the weight gradients ran
-            _Side.keep.extend((arena, scratch))
+            # the side stream reads the arena (saved activations), the scratch and the incoming
+            # gradient (dy / its dropout: the grouped fc2 weight gradient runs after the layer's
+            # whole dgrad chain): keep them until side_join; nothing else may reuse them before
+            _Side.keep.extend((arena, scratch, dy) if dy_drop is None else (arena, scratch, dy, dy_drop))
             _Side.used = True
         d = self.d
         dx = scratch[dxo[0]:dxo[0] + 2 * R * d].view(F16).view(R, d)
@@ -506,17 +508,22 @@ def _group_ok(dy, x, dW):
             dy.shape[0] * max(dy.stride(0), x.stride(0)) * 2 < 2 ** 31)
 
 
-def wgrad_group(problems, rows):
+# block slots a grouped weight-gradient launch may hold while it runs beside the critical path
+# (side stream); folded into the main stream it takes one block per tile
+SIDE_WGRAD_BLOCKS = 128
+
+
+def wgrad_group(problems, rows, max_blocks=0):
     """One grouped, unsplit weight-gradient launch (include/mms2ut.h mms2ut_wgrad_group):
     problems = [(dy [rows, N], x [rows, K], dW [N, K], db [N] or None), ...] (<= 8) on the current
-    stream; dW / db overwritten."""
+    stream; dW / db overwritten; max_blocks > 0 caps the grid (persistent blocks)."""
     arr = (_lib.WgradArgs * len(problems))()
     for i, (dy, x, dW, db) in enumerate(problems):
         assert dy.shape[0] == rows and x.shape[0] == rows and tuple(dW.shape) == (dy.shape[1], x.shape[1])
         assert _group_ok(dy, x, dW), "wgrad_group: shapes / strides / alignment outside the kernel's rules"
         arr[i] = _lib.WgradArgs(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), dW.data_ptr(),
                                 0 if db is None else db.data_ptr(), dy.shape[1], x.shape[1])
-    call("mms2ut_wgrad_group", arr, len(problems), int(rows), _s())
+    call("mms2ut_wgrad_group", arr, len(problems), int(rows), int(max_blocks), _s())
 
 
 def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
@@ -532,7 +539,7 @@ def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
     if accumulate_f32 is None and -(-N // 128) * -(-K // 128) >= 256 and _group_ok(dy, x, dW):
         ctx = side_begin(dy, x) if side else None
         with (ctx or _NULLCTX):
-            wgrad_group([(dy, x, dW, db)], M)
+            wgrad_group([(dy, x, dW, db)], M, SIDE_WGRAD_BLOCKS if ctx is not None and _Side.enabled else 0)
         return dW
     if db is not None and (accumulate_f32 is not None or K % 64 or N % 4):
         linear_wgrad(dy, x, dW, accumulate_f32=accumulate_f32, side=side)
@@ -899,8 +906,9 @@ def fbank(wave, wave_off, frame_off, total_frames, banks, mel_range, nbins=80):
 
 def cmvn_collate(feats, frame_off, B, Tmax, nbins=80, cmvn=True):
     out = torch.empty(B, Tmax, nbins, dtype=F16, device=feats.device)
+    stats = torch.empty(B, 2, nbins, dtype=torch.float32, device=feats.device)
     call("mms2ut_fbank_cmvn_collate", feats.data_ptr(), frame_off.data_ptr(), B, Tmax, nbins,
-         int(cmvn), out.data_ptr(), _s())
+         int(cmvn), stats.data_ptr(), out.data_ptr(), _s())
     return out
 
 

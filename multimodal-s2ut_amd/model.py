@@ -723,7 +723,7 @@ class MMS2UTModel:
         """Backward of enc_layer_fwd (mms2ut_layer_bwd): dx3 = gradient of the layer output, dy2 =
         dropout(dx3) with the fc2-residual mask when the layer above produced it, emit = (p, drop)
         of the layer below's fc2 residual.  Returns (dx, masked dx or None)."""
-        dx, dxd = c["lc"].bwd(c["snap"], c["arena"], dx3, c["B"] * c["T"], dy_drop=dy2, emit=emit)
+        dx, dxd = c["lc"].bwd(c["snap"], c["arena"], dx3, c["B"] * c["T"], dy_drop=dy2, emit=emit, last=l == 0)
         return dx, (dxd if emit is not None else None)
 
     def dec_layer_fwd(self, l, x, kv_all, B, Tt, Te, tgt_mask, enc_len32, tgt_len32=None, spec=None):
