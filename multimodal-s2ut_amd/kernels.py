@@ -508,9 +508,11 @@ def _group_ok(dy, x, dW):
             dy.shape[0] * max(dy.stride(0), x.stride(0)) * 2 < 2 ** 31)
 
 
-# block slots a grouped weight-gradient launch may hold while it runs beside the critical path
-# (side stream); folded into the main stream it takes one block per tile
-SIDE_WGRAD_BLOCKS = 128
+# grid cap of a grouped weight-gradient launch on the side stream (0: one block per tile).  A cap
+# makes the launch persistent: 128 blocks held their slots for ~600 us per layer and pushed the
+# critical path's 474-564-tile GEMMs into second rounds (22.4 ms per step against 18.1 uncapped
+# or at 512, 18.5 with no side stream; profiles/round3_v1_side_blocks_ab.json)
+SIDE_WGRAD_BLOCKS = 0
 
 
 def wgrad_group(problems, rows, max_blocks=0):

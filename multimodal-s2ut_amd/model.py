@@ -44,6 +44,9 @@ def default_cfg(**over):
         SA_attention_dropout=0.1, modality_dropout=-0.5, audio_dropout=-0.5,
         max_source_positions=6000, max_target_positions=3000, no_scale_embedding=False,
         external_multimodal_transformer_layers=None,
+        # QFormer extractor (mm_s2s_transformer.py:194-209; multimodal_translation_config keys)
+        multimodal_extractor_type=None, num_queries=32, num_query_layers=4, num_multimodal_layers=2,
+        self_attention_first=False,
     )
     cfg.update(over)
     return cfg
@@ -129,22 +132,65 @@ def _external_param_specs(S, cfg, ln):
     backward-completion order, the shared layer_norm1 last."""
     d, Di, H, hd, F_, N = external_dims(cfg)
     for i in reversed(range(N)):
-        p = f"{EXT}.layers.{i}"
-        S.extend([(p + ".linear2.weight", (d, F_)), (p + ".linear2.bias", (d,)),
-                  (p + ".linear1.weight", (F_, d)), (p + ".linear1.bias", (F_,))])
-        ln(p + ".norm3", d)
+        _mml_param_specs(S, f"{EXT}.layers.{i}", d, Di, F_, ln)
+    ln(EXT + ".layer_norm1", d)
+
+QF = "encoder.q_former"
+
+
+def qformer_dims(cfg):
+    """(D, heads, FFN, queries, query layers, multimodal layers, self_attention_first) of the
+    QFormerModel built at mm_s2s_transformer.py:195-207 (TransformerLayerConfig(embed_dim = kdim =
+    vdim = 768, nhead = 768 // 64, FFN 4·768)): the width is the image feature width (768 for ViT)
+    and must equal encoder_embed_dim, since the query layers attend to the encoder output."""
+    D, d = cfg["image_feat_dim"], cfg["encoder_embed_dim"]
+    if D != d:
+        raise NotImplementedError(f"q_former: width {D} (image_feat_dim) must equal encoder_embed_dim {d}")
+    H = max(1, D // 64)
+    if D % H or (D // H) not in K.FLASH_HD:
+        raise NotImplementedError(f"q_former: head dim {D // H} not supported")
+    return (D, H, 4 * D, cfg["num_queries"], cfg["num_query_layers"], cfg["num_multimodal_layers"],
+            bool(cfg["self_attention_first"]))
+
+
+def _mml_param_specs(S, p, d, kdim, F_, ln, sa_first=True):
+    """One MultimodalTransformerDecoderLayer (fuse.py:187-221), backward-completion order."""
+    S.extend([(p + ".linear2.weight", (d, F_)), (p + ".linear2.bias", (d,)),
+              (p + ".linear1.weight", (F_, d)), (p + ".linear1.bias", (F_,))])
+    ln(p + ".norm3", d)
+
+    def ca():
         ln(p + ".norm2", d)
         S.extend([(p + ".multihead_attn.out_proj.weight", (d, d)), (p + ".multihead_attn.out_proj.bias", (d,))])
-        if Di == d:
+        if kdim == d:
             S.append((p + ".multihead_attn.in_proj_weight", (3 * d, d)))
         else:
-            S.extend([(p + ".multihead_attn.q_proj_weight", (d, d)), (p + ".multihead_attn.k_proj_weight", (d, Di)),
-                      (p + ".multihead_attn.v_proj_weight", (d, Di))])
+            S.extend([(p + ".multihead_attn.q_proj_weight", (d, d)), (p + ".multihead_attn.k_proj_weight", (d, kdim)),
+                      (p + ".multihead_attn.v_proj_weight", (d, kdim))])
         S.append((p + ".multihead_attn.in_proj_bias", (3 * d,)))
+
+    def sa():
         ln(p + ".norm1", d)
         S.extend([(p + ".self_attn.out_proj.weight", (d, d)), (p + ".self_attn.out_proj.bias", (d,)),
                   (p + ".self_attn.in_proj_weight", (3 * d, d)), (p + ".self_attn.in_proj_bias", (3 * d,))])
-    ln(EXT + ".layer_norm1", d)
+
+    if sa_first:
+        ca()
+        sa()
+    else:
+        sa()
+        ca()
+
+
+def _qformer_param_specs(S, cfg, ln):
+    """QFormerModel (fuse.py:769-818): multimodal layers then query layers in backward order, the
+    query embedding last."""
+    D, _, F_, Q, nq, nm, saf = qformer_dims(cfg)
+    for i in reversed(range(nm)):
+        _mml_param_specs(S, f"{QF}.multimodal_transformer_layers.{i}", D, D, F_, ln, saf)
+    for i in reversed(range(nq)):
+        _mml_param_specs(S, f"{QF}.query_transformer_layers.{i}", D, D, F_, ln, saf)
+    S.append((QF + ".query_embedding", (1, Q, D)))
 
 # ============================================================================ parameter layout
 
@@ -210,6 +256,8 @@ def param_specs(cfg):
             raise NotImplementedError(cfg["multimodal_attention_type"])
         if cfg["image_pre_norm"] and not ext:
             ln("encoder.image_pre_norm_module", Di)
+        if not ext and cfg["multimodal_extractor_type"] == "q_former":
+            _qformer_param_specs(S, cfg, ln)
     ln("encoder.layer_norm", d)
     for l in reversed(range(cfg["encoder_layers"])):
         p = f"encoder.transformer_layers.{l}"
@@ -487,13 +535,23 @@ class MMS2UTModel:
         for i in range(1, len(cfg["conv_kernel_sizes"])):
             W = P(f"encoder.subsample.conv_layers.{i}.weight")
             mats.append(W.view(W.shape[0], -1))
+        def mml(p, kdim, dmem):
+            Wq, Wkv, _, _ = self._mha_w(p + ".multihead_attn", d, kdim)
+            mats.extend([P(p + ".linear2.weight"), P(p + ".linear1.weight"), P(p + ".multihead_attn.out_proj.weight"),
+                         Wq, P(p + ".self_attn.out_proj.weight"), P(p + ".self_attn.in_proj_weight")])
+            if dmem:
+                mats.append(Wkv)
+
         if cfg["fusion"] and cfg["multimodal_attention_type"] == "external_multimodal_transformer":
             for i in range(cfg["external_multimodal_transformer_layers"]):
-                p = f"{EXT}.layers.{i}"
-                Wq, _, _, _ = self._ext_w(i)
-                mats.extend([P(p + ".linear2.weight"), P(p + ".linear1.weight"), P(p + ".multihead_attn.out_proj.weight"),
-                             Wq, P(p + ".self_attn.out_proj.weight"), P(p + ".self_attn.in_proj_weight")])
+                mml(f"{EXT}.layers.{i}", cfg["image_feat_dim"], False)
         elif cfg["fusion"]:
+            if cfg.get("multimodal_extractor_type") == "q_former":
+                D, _, _, _, nq, nm, _ = qformer_dims(cfg)
+                for i in range(nq):
+                    mml(f"{QF}.query_transformer_layers.{i}", D, True)
+                for i in range(nm):
+                    mml(f"{QF}.multimodal_transformer_layers.{i}", D, False)
             Di = cfg["image_feat_dim"]
             mats.append(P("encoder.gate_denses.0.weight"))
             if cfg["multimodal_attention_type"] == "multimodal_attention":
@@ -943,7 +1001,9 @@ class MMS2UTModel:
             res = K.linear(O, Wo, bo, epi=K.EPI_DROP_RESID, aux=textd)
         return res, c
 
-    def fusion_bwd(self, c, dres):
+    def fusion_bwd(self, c, dres, want_dimg=False):
+        """-> d(text) [B*Te, d]; with want_dimg also d(img) [B*Ti, Di] (the image features are not
+        leaves behind a QFormer)."""
         cfg = self.cfg
         d = cfg["encoder_embed_dim"]
         B, Te, Ti, Di, Tk, extra, pre = c["B"], c["Te"], c["Ti"], c["Di"], c["Tk"], c["extra"], c["pre"]
@@ -993,15 +1053,16 @@ class MMS2UTModel:
             rows.zero_()
         K.linear_wgrad(dkv, c["imgd"], gWkv,
                        db=gbkv)
+        dimg_in = None
         if c["ln_fused"]:
             # image LN gamma/beta grads read dimgd through the key layout + dropout directly
             dimgd = K.linear_dgrad(dkv, Wkv)
-            K.layernorm_bwd(dimgd, c["img_in"], self.P("encoder.image_pre_norm_module.weight"), c["im"], c["ir"],
-                            self.params.span("encoder.image_pre_norm_module.weight",
-                                             "encoder.image_pre_norm_module.bias", grad=True),
-                            want_dx=False, dy_grp=Ti if extra else 0, dy_grp_out=Tk if extra else 0,
-                            dy_p=c["pimg"], dy_drop=c["drop_img"])
-        elif cfg["image_pre_norm"]:
+            dimg_in = K.layernorm_bwd(dimgd, c["img_in"], self.P("encoder.image_pre_norm_module.weight"), c["im"],
+                                      c["ir"], self.params.span("encoder.image_pre_norm_module.weight",
+                                                                "encoder.image_pre_norm_module.bias", grad=True),
+                                      want_dx=want_dimg, dy_grp=Ti if extra else 0, dy_grp_out=Tk if extra else 0,
+                                      dy_p=c["pimg"], dy_drop=c["drop_img"])
+        elif cfg["image_pre_norm"] or want_dimg:
             dimgd = K.linear_dgrad(dkv, Wkv)
             if extra:
                 dimg = torch.empty(B * Ti, Di, dtype=F16, device=dkv.device)
@@ -1010,10 +1071,13 @@ class MMS2UTModel:
                 dimg = dimgd
             if c["pimg"] > 0:
                 dimg = K.dropout(dimg, c["pimg"], c["drop_img"])
-            K.layernorm_bwd(dimg, c["img_in"], self.P("encoder.image_pre_norm_module.weight"), c["im"], c["ir"],
-                            self.params.span("encoder.image_pre_norm_module.weight",
-                                             "encoder.image_pre_norm_module.bias", grad=True),
-                            want_dx=False)
+            if cfg["image_pre_norm"]:
+                dimg_in = K.layernorm_bwd(dimg, c["img_in"], self.P("encoder.image_pre_norm_module.weight"), c["im"],
+                                          c["ir"], self.params.span("encoder.image_pre_norm_module.weight",
+                                                                    "encoder.image_pre_norm_module.bias", grad=True),
+                                          want_dx=want_dimg)
+            else:
+                dimg_in = dimg
         K.linear_wgrad(dq, c["textd"], gWq,
                        db=gbq)
         dtext_total = torch.empty(B * Te, d, dtype=F16, device=dres.device)
@@ -1021,70 +1085,75 @@ class MMS2UTModel:
         K.linear_dgrad(dq, Wq, out=dtext_total, accumulate=True)
         if c["ptxt"] > 0:
             dtext_total = K.dropout(dtext_total, c["ptxt"], c["drop_txt"])
+        if want_dimg:
+            return dtext_total, dimg_in
         return dtext_total
 
-    # -------------------------------------------------------------- external multimodal transformer
-    def _ext_w(self, i):
-        """(Wq, Wkv, bq, bkv) of layer i's cross-attention (packed or separate q/k/v weights)."""
-        d, Di = self.cfg["encoder_embed_dim"], self.cfg["image_feat_dim"]
-        p = f"{EXT}.layers.{i}.multihead_attn"
-        b = self.P(p + ".in_proj_bias")
-        if Di == d:
-            W = self.P(p + ".in_proj_weight")
+    # -------------------------------------------------------------- post-LN multimodal decoder layers
+    def _mha_w(self, p, d, kdim, grad=False):
+        """(Wq, Wkv, bq, bkv) of nn.MultiheadAttention `p` (fuse.py:205-209): the packed
+        in_proj_weight when kdim == embed_dim, else q/k/v_proj_weight (k and v adjacent)."""
+        b = (self.G if grad else self.P)(p + ".in_proj_bias")
+        if kdim == d:
+            W = (self.G if grad else self.P)(p + ".in_proj_weight")
             return W[:d], W[d:], b[:d], b[d:]
-        return (self.P(p + ".q_proj_weight"), self.params.span(p + ".k_proj_weight", p + ".v_proj_weight").view(2 * d, Di),
-                b[:d], b[d:])
+        return ((self.G if grad else self.P)(p + ".q_proj_weight"),
+                self.params.span(p + ".k_proj_weight", p + ".v_proj_weight", grad=grad).view(2 * d, kdim), b[:d], b[d:])
 
-    def _ext_g(self, i):
-        d, Di = self.cfg["encoder_embed_dim"], self.cfg["image_feat_dim"]
-        p = f"{EXT}.layers.{i}.multihead_attn"
-        b = self.G(p + ".in_proj_bias")
-        if Di == d:
-            W = self.G(p + ".in_proj_weight")
-            return W[:d], W[d:], b[:d], b[d:]
-        return (self.G(p + ".q_proj_weight"),
-                self.params.span(p + ".k_proj_weight", p + ".v_proj_weight", grad=True).view(2 * d, Di), b[:d], b[d:])
+    def mml_fwd(self, p, x, mem2, B, Tq, Tm, d, kdim, H, pp, sa_first=True, self_len=None, mem_len=None,
+                mem_km=None):
+        """MultimodalTransformerDecoderLayer.forward (fuse.py:236-285; norm_first False, GELU):
+        self_attention_first: x = norm1(x + drop(SA(x))); x = norm2(x + drop(MHA(x, mem)))
+        else:                 x = norm2(x + drop(MHA(x, mem))); x = norm1(x + drop(SA(x)))
+        then                  x = norm3(x + drop(linear2(drop(gelu(linear1(x)))))).
+        x [B*Tq, d]; mem2 [B*Tm, kdim]; self_len: query lengths (None: every query valid); memory
+        keys masked by mem_len (lengths) or mem_km (uint8 key mask)."""
+        hd = d // H
+        R = B * Tq
+        dev = x.device
+        c = {"x": x, "pp": pp, "B": B, "Te": Tq, "Ti": Tm, "img2": mem2, "d": d, "kdim": kdim, "H": H, "p": p,
+             "sa_first": sa_first}
 
-    def ext_layer_fwd(self, i, x, img2, B, Te, Ti, lens32, img_km):
-        """MultimodalTransformerDecoderLayer.forward (fuse.py:237-285; norm_first False,
-        self-attention first): x = norm1(x + drop(SA(x))); x = norm2(x + drop(MHA(x, img)));
-        x = norm3(x + drop(linear2(drop(gelu(linear1(x)))))).  x [B*Te, d], img2 [B*Ti, Di]."""
-        d, Di, H, hd, F_, _ = external_dims(self.cfg)
-        R = B * Te
-        p = f"{EXT}.layers.{i}"
-        pp = self._p("SA_attention_dropout")
-        c = {"x": x, "pp": pp, "B": B, "Te": Te, "Ti": Ti, "img2": img2}
-        qkv = K.linear(x, self.P(p + ".self_attn.in_proj_weight"), self.P(p + ".self_attn.in_proj_bias"))
-        O = torch.empty(R, d, dtype=F16, device=x.device)
-        c["drop_sa"] = self._drop(pp, B * H * Te * Te)
-        c["sattn"] = attn_forward(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Te, Te, hd, hd ** -0.5,
-                                  O, d, key_len=lens32, p=pp, drop=c["drop_sa"])
-        c["qkv"], c["sO"] = qkv, O
-        c["drop1"] = self._drop(pp, R * d)
-        y1 = K.linear(O, self.P(p + ".self_attn.out_proj.weight"), self.P(p + ".self_attn.out_proj.bias"),
-                      epi=K.EPI_DROP_RESID, aux=x, p=pp, drop=c["drop1"])
-        x1, c["m1"], c["r1"] = K.layernorm(y1, self.P(p + ".norm1.weight"), self.P(p + ".norm1.bias"))
-        c["y1"], c["x1"] = y1, x1
-        Wq, Wkv, bq, bkv = self._ext_w(i)
-        q = K.linear(x1, Wq, bq)
-        kv = K.linear(img2, Wkv, bkv)
-        O2 = torch.empty(R, d, dtype=F16, device=x.device)
-        c["drop_ca"] = self._drop(pp, B * H * Te * Ti)
-        c["cattn"] = attn_forward(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Te, Ti, hd, hd ** -0.5, O2, d,
-                                  key_mask=img_km, p=pp, drop=c["drop_ca"])
-        c["q"], c["kv"], c["cO"] = q, kv, O2
-        c["drop2"] = self._drop(pp, R * d)
-        y2 = K.linear(O2, self.P(p + ".multihead_attn.out_proj.weight"), self.P(p + ".multihead_attn.out_proj.bias"),
-                      epi=K.EPI_DROP_RESID, aux=x1, p=pp, drop=c["drop2"])
-        x2, c["m2"], c["r2"] = K.layernorm(y2, self.P(p + ".norm2.weight"), self.P(p + ".norm2.bias"))
-        c["y2"], c["x2"] = y2, x2
+        def sa_block(xin):
+            qkv = K.linear(xin, self.P(p + ".self_attn.in_proj_weight"), self.P(p + ".self_attn.in_proj_bias"))
+            O = torch.empty(R, d, dtype=F16, device=dev)
+            c["drop_sa"] = self._drop(pp, B * H * Tq * Tq)
+            c["sattn"] = attn_forward(qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Tq, Tq, hd,
+                                      hd ** -0.5, O, d, key_len=self_len, p=pp, drop=c["drop_sa"])
+            c["qkv"], c["sO"], c["sa_in"] = qkv, O, xin
+            c["drop1"] = self._drop(pp, R * d)
+            y1 = K.linear(O, self.P(p + ".self_attn.out_proj.weight"), self.P(p + ".self_attn.out_proj.bias"),
+                          epi=K.EPI_DROP_RESID, aux=xin, p=pp, drop=c["drop1"])
+            x1, c["m1"], c["r1"] = K.layernorm(y1, self.P(p + ".norm1.weight"), self.P(p + ".norm1.bias"))
+            c["y1"], c["x1"] = y1, x1
+            return x1
+
+        def ca_block(xin):
+            Wq, Wkv, bq, bkv = self._mha_w(p + ".multihead_attn", d, kdim)
+            q = K.linear(xin, Wq, bq)
+            kv = K.linear(mem2, Wkv, bkv)
+            O2 = torch.empty(R, d, dtype=F16, device=dev)
+            c["drop_ca"] = self._drop(pp, B * H * Tq * Tm)
+            c["cattn"] = attn_forward(q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tq, Tm, hd, hd ** -0.5, O2, d,
+                                      key_len=mem_len, key_mask=mem_km, p=pp, drop=c["drop_ca"])
+            c["q"], c["kv"], c["cO"], c["ca_in"] = q, kv, O2, xin
+            c["drop2"] = self._drop(pp, R * d)
+            y2 = K.linear(O2, self.P(p + ".multihead_attn.out_proj.weight"), self.P(p + ".multihead_attn.out_proj.bias"),
+                          epi=K.EPI_DROP_RESID, aux=xin, p=pp, drop=c["drop2"])
+            x2, c["m2"], c["r2"] = K.layernorm(y2, self.P(p + ".norm2.weight"), self.P(p + ".norm2.bias"))
+            c["y2"], c["x2"] = y2, x2
+            return x2
+
+        xa = ca_block(sa_block(x)) if sa_first else sa_block(ca_block(x))
+        F_ = self.P(p + ".linear1.weight").shape[0]
+        c["ff_in"] = xa
         c["drop_act"] = self._drop(pp, R * F_)
-        z = torch.empty(R, F_, dtype=F16, device=x.device)
-        h = K.linear(x2, self.P(p + ".linear1.weight"), self.P(p + ".linear1.bias"), epi=K.EPI_GELU_DROP, out2=z,
+        z = torch.empty(R, F_, dtype=F16, device=dev)
+        h = K.linear(xa, self.P(p + ".linear1.weight"), self.P(p + ".linear1.bias"), epi=K.EPI_GELU_DROP, out2=z,
                      p=pp, drop=c["drop_act"])
         c["z"], c["h"] = z, h
         c["drop3"] = self._drop(pp, R * d)
-        y3 = K.linear(h, self.P(p + ".linear2.weight"), self.P(p + ".linear2.bias"), epi=K.EPI_DROP_RESID, aux=x2,
+        y3 = K.linear(h, self.P(p + ".linear2.weight"), self.P(p + ".linear2.bias"), epi=K.EPI_DROP_RESID, aux=xa,
                       p=pp, drop=c["drop3"])
         x3, c["m3"], c["r3"] = K.layernorm(y3, self.P(p + ".norm3.weight"), self.P(p + ".norm3.bias"))
         c["y3"] = y3
@@ -1093,46 +1162,68 @@ class MMS2UTModel:
     def _lnspan(self, n):
         return self.params.span(n + ".weight", n + ".bias", grad=True)
 
-    def ext_layer_bwd(self, i, c, dx3):
-        """Hand-written backward of ext_layer_fwd: returns d(layer input).  Post-LN: every
-        residual add happens before a LayerNorm, so each sublayer's input gradient is
-        (LayerNorm backward) + (the sublayer's dgrad), summed into a fresh buffer (the LayerNorm
-        output is still read by side-stream weight gradients)."""
-        d, Di, H, hd, F_, _ = external_dims(self.cfg)
-        p = f"{EXT}.layers.{i}"
-        B, Te, Ti, pp = c["B"], c["Te"], c["Ti"], c["pp"]
+    def mml_bwd(self, c, dx3, dmem=None, dmem_accumulate=False):
+        """Hand-written backward of mml_fwd: returns d(layer input).  Post-LN: every residual add
+        happens before a LayerNorm, so each sublayer's input gradient is (LayerNorm backward) + (the
+        sublayer's dgrad), summed into a fresh buffer (the LayerNorm output is still read by
+        side-stream weight gradients).  dmem [B*Tm, kdim]: receives the memory's gradient (added to
+        its contents with dmem_accumulate); None: the memory is a leaf (image features)."""
+        p, d, kdim, H = c["p"], c["d"], c["kdim"], c["H"]
+        hd = d // H
+        B, Tq, Tm, pp = c["B"], c["Te"], c["Ti"], c["pp"]
         dy3, dl2 = K.layernorm_bwd(dx3, c["y3"], self.P(p + ".norm3.weight"), c["m3"], c["r3"], self._lnspan(p + ".norm3"),
                                    emit=(pp, c["drop3"]))
         dz = K.linear_dgrad(dl2, self.P(p + ".linear2.weight"), epi=K.EPI_GELU_DROP_BWD, aux=c["z"], p=pp,
                             drop=c["drop_act"])
         K.linear_wgrad(dl2, c["h"], self.G(p + ".linear2.weight"), db=self.G(p + ".linear2.bias"))
-        dx2 = K.add_f16(K.linear_dgrad(dz, self.P(p + ".linear1.weight")), dy3)
-        K.linear_wgrad(dz, c["x2"], self.G(p + ".linear1.weight"), db=self.G(p + ".linear1.bias"))
-        dy2, dlo2 = K.layernorm_bwd(dx2, c["y2"], self.P(p + ".norm2.weight"), c["m2"], c["r2"], self._lnspan(p + ".norm2"),
-                                    emit=(pp, c["drop2"]))
-        dO2 = K.linear_dgrad(dlo2, self.P(p + ".multihead_attn.out_proj.weight"))
-        K.linear_wgrad(dlo2, c["cO"], self.G(p + ".multihead_attn.out_proj.weight"),
-                       db=self.G(p + ".multihead_attn.out_proj.bias"))
-        q, kv = c["q"], c["kv"]
-        dq, dkv = torch.empty_like(q), torch.empty_like(kv)
-        attn_backward(c["cattn"], dO2, d, c["cO"], q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Te, Ti, hd, hd ** -0.5,
-                      dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pp, drop=c["drop_ca"])
-        Wq, _, _, _ = self._ext_w(i)
-        gWq, gWkv, gbq, gbkv = self._ext_g(i)
-        dx1 = K.add_f16(K.linear_dgrad(dq, Wq), dy2)
-        K.linear_wgrad(dq, c["x1"], gWq, db=gbq)
-        K.linear_wgrad(dkv, c["img2"], gWkv, db=gbkv)   # the image features are leaves: no dgrad
-        dy1, dso = K.layernorm_bwd(dx1, c["y1"], self.P(p + ".norm1.weight"), c["m1"], c["r1"], self._lnspan(p + ".norm1"),
-                                   emit=(pp, c["drop1"]))
-        dO = K.linear_dgrad(dso, self.P(p + ".self_attn.out_proj.weight"))
-        K.linear_wgrad(dso, c["sO"], self.G(p + ".self_attn.out_proj.weight"), db=self.G(p + ".self_attn.out_proj.bias"))
-        qkv = c["qkv"]
-        dqkv = torch.empty_like(qkv)
-        attn_backward(c["sattn"], dO, d, c["sO"], qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Te, Te,
-                      hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pp, drop=c["drop_sa"])
-        dx = K.add_f16(K.linear_dgrad(dqkv, self.P(p + ".self_attn.in_proj_weight")), dy1)
-        K.linear_wgrad(dqkv, c["x"], self.G(p + ".self_attn.in_proj_weight"), db=self.G(p + ".self_attn.in_proj_bias"))
-        return dx
+        dxa = K.add_f16(K.linear_dgrad(dz, self.P(p + ".linear1.weight")), dy3)
+        K.linear_wgrad(dz, c["ff_in"], self.G(p + ".linear1.weight"), db=self.G(p + ".linear1.bias"))
+
+        def ca_bwd(dxo):
+            dy2, dlo2 = K.layernorm_bwd(dxo, c["y2"], self.P(p + ".norm2.weight"), c["m2"], c["r2"],
+                                        self._lnspan(p + ".norm2"), emit=(pp, c["drop2"]))
+            dO2 = K.linear_dgrad(dlo2, self.P(p + ".multihead_attn.out_proj.weight"))
+            K.linear_wgrad(dlo2, c["cO"], self.G(p + ".multihead_attn.out_proj.weight"),
+                           db=self.G(p + ".multihead_attn.out_proj.bias"))
+            q, kv = c["q"], c["kv"]
+            dq, dkv = torch.empty_like(q), torch.empty_like(kv)
+            attn_backward(c["cattn"], dO2, d, c["cO"], q, kv, kv[:, d:], d, 2 * d, 2 * d, B, H, Tq, Tm, hd, hd ** -0.5,
+                          dq, dkv, dkv[:, d:], d, 2 * d, 2 * d, p=pp, drop=c["drop_ca"])
+            Wq, Wkv, _, _ = self._mha_w(p + ".multihead_attn", d, kdim)
+            gWq, gWkv, gbq, gbkv = self._mha_w(p + ".multihead_attn", d, kdim, grad=True)
+            dx = K.add_f16(K.linear_dgrad(dq, Wq), dy2)
+            K.linear_wgrad(dq, c["ca_in"], gWq, db=gbq)
+            K.linear_wgrad(dkv, c["img2"], gWkv, db=gbkv)
+            if dmem is not None:
+                K.linear_dgrad(dkv, Wkv, out=dmem, accumulate=dmem_accumulate)
+            return dx
+
+        def sa_bwd(dxo):
+            dy1, dso = K.layernorm_bwd(dxo, c["y1"], self.P(p + ".norm1.weight"), c["m1"], c["r1"],
+                                       self._lnspan(p + ".norm1"), emit=(pp, c["drop1"]))
+            dO = K.linear_dgrad(dso, self.P(p + ".self_attn.out_proj.weight"))
+            K.linear_wgrad(dso, c["sO"], self.G(p + ".self_attn.out_proj.weight"), db=self.G(p + ".self_attn.out_proj.bias"))
+            qkv = c["qkv"]
+            dqkv = torch.empty_like(qkv)
+            attn_backward(c["sattn"], dO, d, c["sO"], qkv, qkv[:, d:], qkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, B, H, Tq, Tq,
+                          hd, hd ** -0.5, dqkv, dqkv[:, d:], dqkv[:, 2 * d:], 3 * d, 3 * d, 3 * d, p=pp, drop=c["drop_sa"])
+            dx = K.add_f16(K.linear_dgrad(dqkv, self.P(p + ".self_attn.in_proj_weight")), dy1)
+            K.linear_wgrad(dqkv, c["sa_in"], self.G(p + ".self_attn.in_proj_weight"),
+                           db=self.G(p + ".self_attn.in_proj_bias"))
+            return dx
+
+        return sa_bwd(ca_bwd(dxa)) if c["sa_first"] else ca_bwd(sa_bwd(dxa))
+
+    # -------------------------------------------------------------- external multimodal transformer
+    def ext_layer_fwd(self, i, x, img2, B, Te, Ti, lens32, img_km):
+        """Layer i of ExternalMultimodalTransformerEncoder (fuse.py:298-311: kdim = vdim = Di,
+        self-attention first); x [B*Te, d], img2 [B*Ti, Di]."""
+        d, Di, H, _, _, _ = external_dims(self.cfg)
+        return self.mml_fwd(f"{EXT}.layers.{i}", x, img2, B, Te, Ti, d, Di, H, self._p("SA_attention_dropout"),
+                            sa_first=True, self_len=lens32, mem_km=img_km)
+
+    def ext_layer_bwd(self, i, c, dx3):
+        return self.mml_bwd(c, dx3)   # the image features are leaves: no memory gradient
 
     def ext_fwd(self, states, img, img_km, B, Te, lens32):
         """ExternalMultimodalTransformerEncoder.forward (fuse.py:323-357) over the last N encoder
@@ -1171,6 +1262,42 @@ class MMS2UTModel:
                 out[i] = ds         # s = m1[i] + out_{i-1}: the same gradient for both
                 d = ds
         return out
+
+    # -------------------------------------------------------------- QFormer extractor
+    def qformer_fwd(self, enc, img, B, Te, lens32):
+        """QFormerModel.forward (fuse.py:829-874, norm None) as mm_s2s_transformer.py:481-486
+        calls it: learned queries (query_embedding broadcast over the batch) through the query
+        layers (memory = the encoder output enc [B*Te, D], keys masked by the source lengths) and
+        the multimodal layers (memory = the image features img [B, Ti, D], unmasked).
+        Returns ([B, Q, D], ctx)."""
+        D, H, _, Q, nq, nm, saf = qformer_dims(self.cfg)
+        pp = self._p("SA_attention_dropout")
+        Ti = img.shape[1]
+        x = torch.empty(B * Q, D, dtype=F16, device=enc.device)
+        K.copy2d(self.P(QF + ".query_embedding").view(1, Q * D).expand(B, Q * D), x.view(B, Q * D), B, Q * D)
+        img2 = img.reshape(B * Ti, D)
+        ctx = {"q": [], "m": [], "B": B, "Te": Te, "Q": Q}
+        for i in range(nq):
+            x, c = self.mml_fwd(f"{QF}.query_transformer_layers.{i}", x, enc, B, Q, Te, D, D, H, pp, saf,
+                                mem_len=lens32)
+            ctx["q"].append(c)
+        for i in range(nm):
+            x, c = self.mml_fwd(f"{QF}.multimodal_transformer_layers.{i}", x, img2, B, Q, Ti, D, D, H, pp, saf)
+            ctx["m"].append(c)
+        return x.view(B, Q, D), ctx
+
+    def qformer_bwd(self, ctx, dout, denc):
+        """Backward of qformer_fwd: dout [B*Q, D]; the encoder output's gradient is ADDED to denc
+        [B*Te, D]; the query embedding's gradient is the batch sum of the first layer's input
+        gradient."""
+        B, Q = ctx["B"], ctx["Q"]
+        d = dout
+        for c in reversed(ctx["m"]):
+            d = self.mml_bwd(c, d)
+        for c in reversed(ctx["q"]):
+            d = self.mml_bwd(c, d, dmem=denc, dmem_accumulate=True)
+        K.bias_grad(d.view(B, -1), self.G(QF + ".query_embedding").view(-1), side=False)
+        return denc
 
     # -------------------------------------------------------------- decoder layer
     def _sp(self, p):
@@ -1341,6 +1468,12 @@ class MMS2UTModel:
             return out, lens32, Te, ctx
         xl, ctx["lm"], ctx["lr"] = K.layernorm(x, self.P("encoder.layer_norm.weight"), self.P("encoder.layer_norm.bias"))
         out = xl
+        ctx["qformer"] = None
+        if cfg["fusion"] and imgs is not None and cfg["multimodal_extractor_type"] == "q_former":
+            # mm_s2s_transformer.py:479-494: the QFormer output replaces the image features before
+            # the modality-dropout draws; its Q query tokens are all valid (no image key mask)
+            imgs, ctx["qformer"] = self.qformer_fwd(xl, imgs, B, Te, lens32)
+            img_mask = None
         if cfg["fusion"] and imgs is not None:
             # modality dropout (mm_s2s_transformer.py:496-512): two host draws every training forward
             if self.training:
@@ -1352,6 +1485,7 @@ class MMS2UTModel:
                         out = torch.zeros_like(xl)
                     else:
                         imgs = torch.zeros_like(imgs)   # LN of zeros -> beta (Q5), as reference
+                        ctx["image_dropped"] = True     # (requires_grad=False: no QFormer gradient)
             res, ctx["fusion"] = self.fusion_fwd(out, imgs, img_mask, B, Te)
             out = res
         ctx["B"], ctx["Te"] = B, Te
@@ -1370,20 +1504,34 @@ class MMS2UTModel:
             self._ready(EXT + ".layer_norm1.bias")
             self._ready("encoder.layer_norm.bias")   # unused by this fusion type: its gradient stays 0
             return self._encoder_layers_bwd(ctx, dstates.pop(L - 1), None, dstates)
+        qf = ctx.get("qformer")
+        dimg = None
         if ctx["fusion"] is not None:
-            denc = self.fusion_bwd(ctx["fusion"], denc)
+            if qf is not None and not ctx.get("image_dropped"):
+                denc, dimg = self.fusion_bwd(ctx["fusion"], denc, want_dimg=True)
+            else:
+                denc = self.fusion_bwd(ctx["fusion"], denc)
+        if dimg is not None:
+            # the QFormer read the (pre-modality-dropout) encoder output as its query layers'
+            # memory: that gradient reaches the encoder even when the audio branch was dropped
+            if ctx.get("audio_dropped"):
+                denc = torch.zeros_like(denc)
+            self.qformer_bwd(qf, dimg.view(-1, dimg.shape[-1]), denc)
         last_fusion = [n for n, _ in self.params.specs if n.startswith(("encoder.gate", "encoder.multimodal",
-                                                                         "encoder.selective", "encoder.image"))]
+                                                                         "encoder.selective", "encoder.image",
+                                                                         "encoder.q_former"))]
         if last_fusion:
             self._ready(last_fusion[-1])
-        if ctx.get("audio_dropped") and not dstates:
+        if ctx.get("audio_dropped") and dimg is not None:
+            pass    # denc holds the QFormer's memory gradient: the encoder backward runs
+        elif ctx.get("audio_dropped") and not dstates:
             # the reference replaces encoder_out by zeros_like(..., requires_grad=False)
             # (mm_s2s_transformer.py:500): no gradient reaches the encoder, whose gradients stay
             # at the step's zeros -- skip its whole backward, only flush the reducer
             ctx["layers"] = None
             self._ready(None)
             return
-        if ctx.get("audio_dropped"):
+        elif ctx.get("audio_dropped"):
             denc = torch.zeros_like(denc)   # only the multitask heads' state gradients remain
         layers = ctx["layers"]
         emit = lambda l: (layers[l]["pd"], layers[l]["drop2"]) if l >= 0 else None  # noqa: E731

@@ -207,6 +207,51 @@ def _make_external_case(F, name, *, d, Di, N, B, Te, Ti, text_pad, img_pad, seed
     return res
 
 
+def _make_qformer_case(F, name, *, D, Q, nq, nm, B, Te, Ti, text_pad, sa_first, seed=0):
+    """The reference's QFormerModel (fuse.py:769-874) as MM_S2STransformerEncoder builds it
+    (mm_s2s_transformer.py:195-207: TransformerLayerConfig(embed_dim = kdim = vdim = D,
+    nhead = D // 64, FFN 4 D, batch_first=True), self_attention_first from the config) and calls it
+    (:481-486: m1 = encoder_out [B, Te, D] with its padding mask, m2 = image features [B, Ti, D],
+    no image mask).  Dropout 0; train mode; query_embedding drawn nonzero.  Inputs and parameters
+    are fp16-representable (the HIP run sees the same values); results are stored as float32."""
+    g = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    cfgl = F.TransformerLayerConfig(embed_dim=D, kdim=D, vdim=D, nhead=max(1, D // 64), dim_feedforward=4 * D,
+                                    dropout=0.0, batch_first=True)
+    qf = F.QFormerModel(num_queries=Q, layer_config=cfgl, num_query_layers=nq, num_multimodal_layers=nm,
+                        self_attention_first=sa_first)
+    with torch.no_grad():
+        for n, prm in qf.named_parameters():
+            if n == "query_embedding":
+                prm.copy_(0.5 * torch.randn(prm.shape, generator=g))
+            elif n.endswith("bias"):
+                prm.copy_(0.1 * torch.randn(prm.shape, generator=g))
+            elif "norm" in n:
+                prm.copy_(1.0 + 0.1 * torch.randn(prm.shape, generator=g))
+            prm.copy_(prm.half().float())
+    qf = qf.double().train()
+    m1 = torch.randn(B, Te, D, generator=g).half().double().requires_grad_(True)
+    m2 = torch.randn(B, Ti, D, generator=g).half().double().requires_grad_(True)
+    text_len = torch.full((B,), Te, dtype=torch.long)
+    if text_pad:
+        text_len = torch.randint(max(1, Te // 2), Te + 1, (B,), generator=g)
+        text_len[0] = Te
+    text_mask = torch.arange(Te)[None, :] >= text_len[:, None]
+    res = qf(m1=m1, m2=m2, m1_key_padding_mask=text_mask, m2_key_padding_mask=None)
+    gout = torch.randn(res.shape, generator=g).half().double()
+    (res * gout).sum().backward()
+    f32 = lambda t: t.detach().numpy().astype(np.float32)  # noqa: E731
+    out = dict(D=np.array(D), Q=np.array(Q), nq=np.array(nq), nm=np.array(nm), sa_first=np.array(sa_first),
+               m1=m1.detach().numpy().astype(np.float16), m2=m2.detach().numpy().astype(np.float16),
+               text_mask=text_mask.numpy(), res=f32(res), gout=gout.numpy().astype(np.float16),
+               grad_m1=f32(m1.grad), grad_m2=f32(m2.grad))
+    for k, v in qf.named_parameters():
+        out["param." + k] = v.detach().numpy().astype(np.float16)
+        out["grad." + k] = f32(v.grad)
+    np.savez_compressed(os.path.join(OUT, f"qformer_{name}.npz"), **out)
+    return res
+
+
 SHIPPED = dict(d=768, Di=768, B=2, Te=125, Ti=577, seed=300, probes=8)
 
 
@@ -345,6 +390,7 @@ def main():
     _install_shim()
     import mm_s2ut.models.fuse as F  # noqa: E402  (reference code, shimmed deps)
     import mm_s2ut.models.mm_s2s_transformer as M  # noqa: E402
+    only = sys.argv[1:]    # e.g. "qformer": regenerate that family only
     cases = [
         # name, attention, gate, d, Di, B, Te, Ti, text_pad, img_pad, dropout p's
         ("mma_gate_packed", "multimodal_attention", True, 64, 64, 3, 9, 17, True, False, 0, 0, 0),
@@ -357,7 +403,7 @@ def main():
         ("mma_gate_dropout", "multimodal_attention", True, 64, 64, 2, 9, 17, True, False, 0.5, 0.1, 0),
         ("mma_gate_detr", "multimodal_attention", True, 96, 32, 2, 6, 10, True, True, 0, 0, 0),
     ]
-    for i, (name, att, gate, d, Di, B, Te, Ti, tp, ip, pi, pt, pa) in enumerate(cases):
+    for i, (name, att, gate, d, Di, B, Te, Ti, tp, ip, pi, pt, pa) in enumerate(cases if not only else []):
         _make_case(M, F, name, att=att, gate=gate, d=d, Di=Di, B=B, Te=Te, Ti=Ti,
                    text_pad=tp, img_pad=ip, p_img=pi, p_txt=pt, p_attn=pa, seed=100 + i)
         print("wrote", name)
@@ -368,11 +414,23 @@ def main():
         ("heads2_2l", 64, 128, 2, 2, 6, 9, True, True),
         ("separate_2l", 96, 64, 2, 3, 7, 10, False, True),
     ]
-    for i, (name, d, Di, N, B, Te, Ti, tp, ip) in enumerate(ext):
+    for i, (name, d, Di, N, B, Te, Ti, tp, ip) in enumerate(ext if not only else []):
         _make_external_case(F, name, d=d, Di=Di, N=N, B=B, Te=Te, Ti=Ti, text_pad=tp, img_pad=ip, seed=200 + i)
         print("wrote external", name)
-    _make_shipped(M, F)
-    print("wrote shipped_fusion")
+    qf = [
+        # name, D, queries, query layers, multimodal layers, B, Te, Ti, text_pad, self_attention_first
+        ("d64_2q1m", 64, 5, 2, 1, 3, 9, 7, True, False),
+        ("d128_1q1m_safirst", 128, 4, 1, 1, 2, 11, 6, True, True),
+        ("d64_1q2m", 64, 8, 1, 2, 2, 13, 17, False, False),
+    ]
+    if not only or "qformer" in only:
+        for i, (name, D, Q, nq, nm, B, Te, Ti, tp, saf) in enumerate(qf):
+            _make_qformer_case(F, name, D=D, Q=Q, nq=nq, nm=nm, B=B, Te=Te, Ti=Ti, text_pad=tp, sa_first=saf,
+                               seed=400 + i)
+            print("wrote qformer", name)
+    if not only:
+        _make_shipped(M, F)
+        print("wrote shipped_fusion")
 
 
 if __name__ == "__main__":

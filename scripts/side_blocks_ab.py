@@ -1,5 +1,6 @@
 """A/B of the grid cap of the grouped weight-gradient launches on the side stream
-(kernels.SIDE_WGRAD_BLOCKS): one bench.py run per value, interleaved twice.
+(kernels.SIDE_WGRAD_BLOCKS): one bench.py run per value, interleaved twice.  cap -1: no side stream
+(every side job in order on the main stream).
 usage: python scripts/side_blocks_ab.py OUT_JSON [caps...]"""
 import json
 import os
@@ -11,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 out = sys.argv[1]
 caps = [int(c) for c in sys.argv[2:]] or [0, 128, 64, 256]
 child = ("import sys, runpy; sys.path.insert(0, {root!r}); import importlib; "
-         "K = importlib.import_module('multimodal-s2ut_amd').kernels; K.SIDE_WGRAD_BLOCKS = {cap}; "
+         "K = importlib.import_module('multimodal-s2ut_amd').kernels; K.SIDE_WGRAD_BLOCKS = max({cap}, 0); K._Side.enabled = {cap} >= 0; "
          "sys.argv = ['bench.py', '--steps', '20', '--warmup', '5', '--no-cpu-baseline', '--no-gemm-timing']; "
          "runpy.run_path({bench!r}, run_name='__main__')")
 res = {}

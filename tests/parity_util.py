@@ -76,6 +76,19 @@ def hip_masks(mm, cfg, ectx, dctx, B, Te, Tt, relu=True):
                 for s_ in ("drop1", "drop2", "drop3"):
                     out[f"{p}.{s_}"] = tb(m(c[s_], B * Te * d, pp), Te, d)
                 out[p + ".act"] = tb(m(c["drop_act"], B * Te * Fx, pp), Te, Fx)
+    qc = ectx.get("qformer")
+    if qc is not None:       # QFormer extractor (oracle qformer / multimodal_decoder_layer sites)
+        D = cfg["image_feat_dim"]
+        Hq, Q = max(1, D // 64), qc["Q"]
+        for grp, lst in (("query_transformer_layers", qc["q"]), ("multimodal_transformer_layers", qc["m"])):
+            for i, c in enumerate(lst):
+                p, pp, Tm = f"encoder.q_former.{grp}.{i}", c["pp"], c["Ti"]
+                if pp > 0:
+                    out[p + ".self_attn"] = m(c["drop_sa"], B * Hq * Q * Q, pp).view(B * Hq, Q, Q)
+                    out[p + ".cross_attn"] = m(c["drop_ca"], B * Hq * Q * Tm, pp).view(B * Hq, Q, Tm)
+                    for s_ in ("drop1", "drop2", "drop3"):
+                        out[f"{p}.{s_}"] = tb(m(c[s_], B * Q * D, pp), Q, D)
+                    out[p + ".act"] = tb(m(c["drop_act"], B * Q * 4 * D, pp), Q, 4 * D)
     fc = ectx.get("fusion")
     if fc is not None:
         Ti, Di, Tk = fc["Ti"], fc["Di"], fc["Tk"]

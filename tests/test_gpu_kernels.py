@@ -275,23 +275,26 @@ def _attn_ref(q, k, v, lens, causal, scale, mask=None):
     return p @ v
 
 
-@pytest.mark.parametrize("hd", [64, 96])
-@pytest.mark.parametrize("causal,Tq,Tk,lens,p", [
+_FLASH_CASES = [
     (False, 70, 90, [90, 50, 7], 0.0), (True, 70, 70, [70, 41, 3], 0.0),
     (False, 130, 130, [130, 129, 65], 0.0), (True, 150, 150, [150, 100, 1], 0.25),
     (False, 33, 200, [200, 64, 63], 0.1), (True, 128, 128, [128, 77, 5], 0.1),
     (False, 100, 128, [128, 100, 1], 0.2), (False, 1, 17, [17, 9, 1], 0.0),
     (False, 300, 100, [100, 57, 2], 0.1), (True, 256, 256, [256, 200, 9], 0.1),
     (False, 301, 213, [213, 129, 1], 0.1), (True, 257, 257, [257, 130, 4], 0.0),
-    (False, 70, 300, [300, 257, 3], 0.1), (True, 300, 300, [300, 129, 2], 0.2)])
-@pytest.mark.parametrize("heads", ["few", "many"])
+    (False, 70, 300, [300, 257, 3], 0.1), (True, 300, 300, [300, 129, 2], 0.2)]
+# the many-heads variant only where it targets the fused kernel (Tq <= 130, Tk <= 256)
+_FLASH_PARAMS = [c + ("few",) for c in _FLASH_CASES] + \
+    [c + ("many",) for c in _FLASH_CASES if c[1] <= 130 and c[2] <= 256]
+
+
+@pytest.mark.parametrize("hd", [64, 96])
+@pytest.mark.parametrize("causal,Tq,Tk,lens,p,heads", _FLASH_PARAMS)
 def test_flash_attention_fwd_bwd(K, hd, causal, Tq, Tk, lens, p, heads):
     """Tk <= 256 takes the one-launch chunked backward (any Tq), Tk > 256 the three-kernel one.
     heads=many: B*H = 3*96 = 288 heads > 256 CUs, so persistent blocks of the fused kernel walk
     several heads (the next-head prefetch path)."""
     B, H = 3, (2 if heads == "few" else 96)
-    if heads == "many" and (Tq > 130 or Tk > 256):
-        pytest.skip("the many-heads case only targets the fused kernel")
     d = H * hd
     g = torch.Generator(device="cuda").manual_seed(5)
     q = torch.randn(B * Tq, d, generator=g, device="cuda").half()

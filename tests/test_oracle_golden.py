@@ -110,3 +110,36 @@ def test_shipped_shape_oracle_matches_reference(att):
             R_, L_ = probes[key]
             np.testing.assert_allclose(g @ R_, z[k], rtol=1e-5, atol=1e-5, err_msg=k)
             np.testing.assert_allclose(L_.T @ g, z[f"{tag}.gskT.{n}"], rtol=1e-5, atol=1e-5, err_msg=k)
+
+
+def qformer_case(path):
+    """A reference-run QFormerModel case (oracle/gen_golden.py _make_qformer_case): the oracle
+    config, the parameters under the model's names (encoder.q_former.*), inputs time-major."""
+    z = np.load(path)
+    D = int(z["D"])
+    cfg = R.base_config(encoder_embed_dim=D, image_feat_dim=D, multimodal_extractor_type="q_former",
+                        num_queries=int(z["Q"]), num_query_layers=int(z["nq"]), num_multimodal_layers=int(z["nm"]),
+                        self_attention_first=bool(z["sa_first"]), SA_attention_dropout=0.0)
+    P = {R.QF + "." + k[len("param."):]: torch.from_numpy(z[k].astype(np.float64))
+         for k in z.files if k.startswith("param.")}
+    return z, cfg, P
+
+
+@pytest.mark.parametrize("path", golden_files("qformer_"), ids=lambda p: p.split("/")[-1])
+def test_qformer_oracle_matches_reference(path):
+    """the oracle's QFormerModel restatement (oracle/ref_model.py
+    qformer, both self_attention_first branches of fuse.py:254-259) vs the reference's own fuse.py
+    run in float64 on fp16-representable inputs; results stored as float32, hence rtol 1e-5."""
+    z, cfg, P = qformer_case(path)
+    P = {k: v.clone().requires_grad_(True) for k, v in P.items()}
+    m1 = torch.from_numpy(z["m1"].astype(np.float64)).transpose(0, 1).requires_grad_(True)
+    m2 = torch.from_numpy(z["m2"].astype(np.float64)).transpose(0, 1).requires_grad_(True)
+    res = R.qformer(P, m1, m2, torch.from_numpy(z["text_mask"]), cfg, dtype=torch.float64).transpose(0, 1)
+    np.testing.assert_allclose(res.detach().numpy(), z["res"], rtol=1e-5, atol=1e-6)
+    (res * torch.from_numpy(z["gout"].astype(np.float64))).sum().backward()
+    np.testing.assert_allclose(m1.grad.transpose(0, 1).numpy(), z["grad_m1"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(m2.grad.transpose(0, 1).numpy(), z["grad_m2"], rtol=1e-5, atol=1e-6)
+    for k in z.files:
+        if k.startswith("grad.") and k != "grad_m1":
+            name = R.QF + "." + k[len("grad."):]
+            np.testing.assert_allclose(P[name].grad.numpy(), z[k], rtol=1e-5, atol=1e-6, err_msg=name)
