@@ -138,16 +138,16 @@ def _external_param_specs(S, cfg, ln):
 QF = "encoder.q_former"
 
 
-def qformer_dims(cfg):
+def qformer_dims(cfg, check=True):
     """(D, heads, FFN, queries, query layers, multimodal layers, self_attention_first) of the
     QFormerModel built at mm_s2s_transformer.py:195-207 (TransformerLayerConfig(embed_dim = kdim =
     vdim = 768, nhead = 768 // 64, FFN 4·768)): the width is the image feature width (768 for ViT)
     and must equal encoder_embed_dim, since the query layers attend to the encoder output."""
     D, d = cfg["image_feat_dim"], cfg["encoder_embed_dim"]
-    if D != d:
+    if check and D != d:
         raise NotImplementedError(f"q_former: width {D} (image_feat_dim) must equal encoder_embed_dim {d}")
     H = max(1, D // 64)
-    if D % H or (D // H) not in K.FLASH_HD:
+    if check and (D % H or (D // H) not in K.FLASH_HD):
         raise NotImplementedError(f"q_former: head dim {D // H} not supported")
     return (D, H, 4 * D, cfg["num_queries"], cfg["num_query_layers"], cfg["num_multimodal_layers"],
             bool(cfg["self_attention_first"]))
@@ -182,10 +182,10 @@ def _mml_param_specs(S, p, d, kdim, F_, ln, sa_first=True):
         ca()
 
 
-def _qformer_param_specs(S, cfg, ln):
+def _qformer_param_specs(S, cfg, ln, check=True):
     """QFormerModel (fuse.py:769-818): multimodal layers then query layers in backward order, the
     query embedding last."""
-    D, _, F_, Q, nq, nm, saf = qformer_dims(cfg)
+    D, _, F_, Q, nq, nm, saf = qformer_dims(cfg, check)
     for i in reversed(range(nm)):
         _mml_param_specs(S, f"{QF}.multimodal_transformer_layers.{i}", D, D, F_, ln, saf)
     for i in reversed(range(nq)):
@@ -218,6 +218,7 @@ def param_specs(cfg):
         S.extend([(f"{p}.weight", (n,)), (f"{p}.bias", (n,))])
 
     tasks = aux_tasks(cfg)
+    qf_unused = []
     # multitask heads on the unit decoder's inner states complete their backward first, then the
     # unit decoder, then the heads on encoder states, then the encoder (runtime._ModelFn.backward)
     for t in tasks:
@@ -258,6 +259,10 @@ def param_specs(cfg):
             ln("encoder.image_pre_norm_module", Di)
         if not ext and cfg["multimodal_extractor_type"] == "q_former":
             _qformer_param_specs(S, cfg, ln)
+        elif not ext and cfg.get("qformer_unused"):
+            # built by the reference without a visual extractor, never called (mm_s2s_transformer.py:475)
+            _qformer_param_specs(qf_unused, cfg, lambda p, n: qf_unused.extend([(f"{p}.weight", (n,)), (f"{p}.bias", (n,))]),
+                                 check=False)
     ln("encoder.layer_norm", d)
     for l in reversed(range(cfg["encoder_layers"])):
         p = f"encoder.transformer_layers.{l}"
@@ -271,7 +276,7 @@ def param_specs(cfg):
         co = C if i < len(ks) - 1 else 2 * d
         S.extend([(f"encoder.subsample.conv_layers.{i}.weight", (co, ci, ks[i])),
                   (f"encoder.subsample.conv_layers.{i}.bias", (co,))])
-    unused = [("encoder.proj_768_to_512.weight", (512, 768)), ("encoder.proj_768_to_512.bias", (512,)),
+    unused = qf_unused + [("encoder.proj_768_to_512.weight", (512, 768)), ("encoder.proj_768_to_512.bias", (512,)),
               ("encoder.proj_1024_to_512.weight", (512, 1024)), ("encoder.proj_1024_to_512.bias", (512,)),
               ("encoder.proj_1024_to_768.weight", (768, 1024)), ("encoder.proj_1024_to_768.bias", (768,))]
     for j in range(3):

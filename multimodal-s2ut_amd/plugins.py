@@ -141,8 +141,12 @@ def cfg_from_args(args, fusion_cfg=None, vocab_size=1004):
         att = fusion_cfg.multimodal_attention_type
         if att not in ("selective_attention", "multimodal_attention", "external_multimodal_transformer"):
             raise NotImplementedError(f"multimodal_attention_type={att!r} (out of scope: SURVEY §2)")
-        if att == "external_multimodal_transformer" and getattr(fusion_cfg, "load_visual_extractor_type", None):
+        extractor = getattr(fusion_cfg, "load_visual_extractor_type", None) or None
+        if att == "external_multimodal_transformer" and extractor:
             raise NotImplementedError("on-line visual extractors (ViT / CLIP) are out of scope: pre-extracted features")
+        qformer = getattr(fusion_cfg, "multimodal_extractor_type", None) == "q_former"
+        if qformer and att == "external_multimodal_transformer":
+            raise NotImplementedError("q_former with the external multimodal transformer")
         if getattr(fusion_cfg, "is_merge_text_img", False):
             raise NotImplementedError("is_merge_text_img=True")
         cfg.update(fusion=bool(fusion_cfg.is_fusion_top), multimodal_attention_type=att,
@@ -154,6 +158,17 @@ def cfg_from_args(args, fusion_cfg=None, vocab_size=1004):
                    modality_dropout=float(fusion_cfg.modality_dropout),
                    audio_dropout=float(fusion_cfg.audio_dropout),
                    external_multimodal_transformer_layers=getattr(fusion_cfg, "external_multimodal_transformer_layers", None))
+        if qformer:
+            # mm_s2s_transformer.py:194-209 builds the QFormer whenever multimodal_extractor_type is
+            # q_former, but calls it (:479-494) only on the on-line visual extractor's output.  With
+            # an extractor configured, the image features fed here stand for that (frozen)
+            # extractor's last hidden state and run through the QFormer; without one, the QFormer
+            # is built and never used (its parameters stay in the state dict, as SURVEY Q3)
+            cfg.update(multimodal_extractor_type="q_former" if extractor else None, qformer_unused=not extractor,
+                       num_queries=int(getattr(fusion_cfg, "num_queries", 32)),
+                       num_query_layers=int(getattr(fusion_cfg, "num_query_layers", 4)),
+                       num_multimodal_layers=int(getattr(fusion_cfg, "num_multimodal_layers", 2)),
+                       self_attention_first=bool(getattr(fusion_cfg, "self_attention_first", False)))
     return cfg
 
 # ------------------------------------------------------------------------------------ task

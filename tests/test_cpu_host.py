@@ -59,7 +59,9 @@ def test_gemm_args_pack_layout():
 def test_param_layout_matches_reference_state_dict():
     mm = pkg()
     for cfg_o in (R.base_config(), R.tiny_config(image_feat_dim=768),
-                  R.base_config(multimodal_attention_type="selective_attention")):
+                  R.base_config(multimodal_attention_type="selective_attention"),
+                  R.base_config(multimodal_extractor_type="q_former", num_queries=8, num_query_layers=2,
+                                num_multimodal_layers=1, self_attention_first=False)):
         specs, unused = mm.param_specs(mm.default_cfg(**cfg_o))
         names = {n for n, _ in specs} | {n for n, _ in unused}
         ref = R.init_params(cfg_o, include_unused=True)

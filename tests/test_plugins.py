@@ -120,6 +120,27 @@ def test_selective_attention_yaml(tmp_path):
     assert cfg["use_selective_gate"] is False and cfg["fusion"] is True
 
 
+def test_qformer_yaml(tmp_path):
+    """multimodal_extractor_type: q_former (mm_s2s_transformer.py:194-209): with a visual extractor
+    configured the QFormer runs on the image features (its parameters are trained); without one the
+    reference builds it and never calls it (:475), so its parameters are kept but unused."""
+    P, mm = _plugins(), pkg()
+    a = P.build_parser().parse_args(["/d", "--fp16", "--share-decoder-input-output-embed", "--encoder-embed-dim", "768"])
+    base = FUSION_YAML + "multimodal_extractor_type: q_former\nnum_queries: 16\nnum_query_layers: 2\n"
+    for extractor, active in (("vit_huggingface", True), ("null", False)):
+        y = tmp_path / f"qf_{extractor}.yaml"
+        y.write_text(base.replace("load_visual_extractor_type: null", f"load_visual_extractor_type: {extractor}"))
+        cfg = P.cfg_from_args(a, P.load_fusion_yaml(str(y)))
+        specs, unused = mm.param_specs(cfg)
+        used = {n for n, _ in specs if n.startswith("encoder.q_former.")}
+        idle = {n for n, _ in unused if n.startswith("encoder.q_former.")}
+        assert cfg["num_queries"] == 16 and cfg["num_query_layers"] == 2 and cfg["num_multimodal_layers"] == 2
+        assert (cfg["multimodal_extractor_type"] == "q_former") == active
+        assert bool(used) == active and bool(idle) == (not active)
+        assert dict(specs + unused)["encoder.q_former.query_embedding"] == (1, 16, 768)
+        assert len(used | idle) == 1 + 4 * 18   # query embedding + 18 tensors per layer
+
+
 def test_cli_rejects_non_fp16_and_missing_data():
     cli = pkg("cli")
     with pytest.raises(SystemExit, match="fp16"):
