@@ -437,7 +437,11 @@ int mms2ut_fbank_frames(const int64_t* wave_off, int B, int32_t* n_frames_out, h
 int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, const int32_t* frame_off, int B,
                      int total_frames, const float* mel_banks, const int32_t* mel_range, int nbins,
                      float* feats, hipStream_t stream);
-/* stats: caller-owned fp32 workspace [B][2][nbins] (per-utterance mean, std)                   */
+/* stats: caller-owned workspace of MMS_CMVN_WS_FLOATS(B, nbins) floats: [B][2][nbins] fp32
+ * (per-utterance mean, std), then 8-B aligned fp64 slice partials [B][MMS_CMVN_SPLIT][2][nbins]   */
+#define MMS_CMVN_SPLIT 8
+#define MMS_CMVN_WS_FLOATS(B, nbins) ((((int64_t)2 * (B) * (nbins) + 1) & ~(int64_t)1) + \
+                                      (int64_t)2 * (B) * MMS_CMVN_SPLIT * 2 * (nbins))
 int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* frame_off, int B, int Tmax,
                               int nbins, int cmvn, float* stats, mms2ut_half* out, hipStream_t stream);
 /* fairseq SpecAugmentTransform (feature_transforms/specaugment.py, the `specaugment` entry of

@@ -2,7 +2,8 @@
 // path the reference's get_fbank takes: mm_s2ut/data/audio_utils.py:326-349) + utterance CMVN +
 // zero-padded fp16 collation.
 //
-// fbank_kernel: one wave per 25 ms frame, FPW frames per wave in turn, 4 waves per block.  DC
+// fbank_kernel: one wave per 25 ms frame, 4 waves per block, a persistent grid (frames dealt to the
+// waves round-robin), so the per-block LDS tables are built once per block, not per 16 frames.  DC
 // removal and pre-emphasis, povey window, then the 512-point real FFT as a 256-point complex FFT
 // of the even/odd sample pairs (z[n] = x[2n] + i x[2n+1]; radix-4, four in-place LDS stages, one
 // butterfly of 4 points per lane) and the standard split X[k] = E[k] + W^k O[k]; power spectrum,
@@ -19,7 +20,7 @@ namespace {
 
 constexpr int WIN = 400, SHIFT = 160, NFFT = 512, NBIN = 257;
 constexpr int NC = 256;                        // complex FFT points (the real 512-point FFT's half)
-constexpr int FPW = 4, FB_WAVES = 4, FPB = FPW * FB_WAVES;
+constexpr int FB_WAVES = 4;
 constexpr int MELW_MAX = 1024;                 // nonzero mel weights staged per block (80 bins: ~510)
 
 struct FbankConst {
@@ -37,7 +38,7 @@ struct FbankSmem {
   float tw_re[NFFT / 2], tw_im[NFFT / 2];
   float win[WIN];
   float melw[MELW_MAX];
-  int mlo[256], mlen[256], moff[256];
+  int mlo[256], mlen[256], moff[256], ntot;
   float x[FB_WAVES][WIN];
   float zr[FB_WAVES][NC], zi[FB_WAVES][NC];
   float pw[FB_WAVES][NBIN + 3];
@@ -51,9 +52,11 @@ MMS_DEV void tw512(const FbankSmem& S, int j, float& c, float& s) {
   s = sg * S.tw_im[jj];
 }
 
+// intra-wave LDS hand-off: this wave's LDS writes are complete (no wait on its global stores, so
+// a frame's feature stores stay in flight under the next frame's work)
 MMS_DEV void wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
 __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __restrict__ wave,
@@ -64,44 +67,87 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
                                                               float* __restrict__ feats) {
   __shared__ FbankSmem S;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // per-block tables: twiddles, window, and the mel filters' nonzero weights (compact, prefix offsets)
+  // per-block tables, built once per (persistent) block, every step parallel over the threads:
+  // twiddles, window, and the mel filters' nonzero weights (compact, prefix offsets)
   for (int i = tid; i < NFFT / 2; i += blockDim.x) { S.tw_re[i] = c_fb.tw_re[i]; S.tw_im[i] = c_fb.tw_im[i]; }
   for (int i = tid; i < WIN; i += blockDim.x) S.win[i] = c_fb.window[i];
-  if (tid == 0) {
-    int o = 0;
-    for (int m = 0; m < nbins; ++m) {
-      const int lo = mel_range[2 * m], hi = mel_range[2 * m + 1];
-      S.mlo[m] = lo;
-      S.mlen[m] = hi - lo;
-      S.moff[m] = o;
-      o += hi - lo;
-    }
+  for (int m = tid; m < nbins; m += blockDim.x) {
+    const int lo = mel_range[2 * m], hi = mel_range[2 * m + 1];
+    S.mlo[m] = lo;
+    S.mlen[m] = hi - lo;
   }
   __syncthreads();
-  for (int m = 0; m < nbins; ++m)
-    for (int j = tid; j < S.mlen[m]; j += blockDim.x) S.melw[S.moff[m] + j] = banks[(long)m * NBIN + S.mlo[m] + j];
+  if (w == 0) {
+    // exclusive prefix sum of the filter lengths (nbins <= 256: 4 per lane, then a wave scan)
+    int len4[4], loc = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = 4 * lane + e;
+      len4[e] = m < nbins ? S.mlen[m] : 0;
+      loc += len4[e];
+    }
+    int inc = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    int run = inc - loc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = 4 * lane + e;
+      if (m < nbins) S.moff[m] = run;
+      run += len4[e];
+    }
+    if (lane == 63) S.ntot = inc;
+  }
+  __syncthreads();
+  const int nw = S.ntot;   // <= 2 * 257: each FFT bin lies in at most two triangular filters
+  // every weight by a flat index: its filter by binary search over the prefix offsets
+  for (int i = tid; i < nw && i < MELW_MAX; i += blockDim.x) {
+    int a = 0, b = nbins;
+    while (b - a > 1) {
+      const int mid = (a + b) >> 1;
+      if (S.moff[mid] <= i) a = mid; else b = mid;
+    }
+    S.melw[i] = banks[(long)a * NBIN + S.mlo[a] + (i - S.moff[a])];
+  }
   __syncthreads();
   float* X = S.x[w];
   float* zr = S.zr[w];
   float* zi = S.zi[w];
   float* P = S.pw[w];
   const float flt_eps = 1.1920928955078125e-07f;
-  for (int i = 0; i < FPW; ++i) {
-    const int f = blockIdx.x * FPB + w * FPW + i;
-    if (f >= total) break;
-    // utterance of this frame (binary search over frame_off)
-    int lo = 0, hi = B;
+  // persistent: wave (block, w) takes frames w + FB_WAVES * block, + FB_WAVES * gridDim.x, ...;
+  // the next frame's 400 samples are loaded into registers while the current one is transformed
+  const int fstep = gridDim.x * FB_WAVES;
+  auto frame_src = [&](int f) {
+    int lo = 0, hi = B;   // utterance of frame f (binary search over frame_off)
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
       if (frame_off[mid] <= f) lo = mid; else hi = mid;
     }
-    const float* src = wave + wave_off[lo] + (long)(f - frame_off[lo]) * SHIFT;
+    return wave + wave_off[lo] + (long)(f - frame_off[lo]) * SHIFT;
+  };
+  float xs[7];
+  auto load_frame = [&](int f) {
+    if (f >= total) return;
+    const float* src = frame_src(f);
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int j = lane + 64 * q;
+      xs[q] = j < WIN ? src[j] : 0.f;
+    }
+  };
+  load_frame(blockIdx.x * FB_WAVES + w);
+  for (int f = blockIdx.x * FB_WAVES + w; f < total; f += fstep) {
     float sum = 0.f;
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
       const int j = lane + 64 * q;
-      if (j < WIN) { const float v = src[j]; X[j] = v; sum += v; }
+      if (j < WIN) { X[j] = xs[q]; sum += xs[q]; }
     }
+    load_frame(f + fstep);
     const float mean = wave_sum(sum) * (1.f / WIN);
     wave_sync();
     // pre-emphasis (replicate-pad at j = 0), window, zero pad to 512; pairs -> digit-reversed slots
@@ -182,21 +228,24 @@ __global__ void fbank_frames_kernel(const int64_t* wave_off, int B, int* n_frame
 }
 
 // fairseq UtteranceCMVN (numpy float32: mean over time, var = E[x^2] - mean^2,
-// std = sqrt(max(var, 1e-10)), x = (x - mean) / std).  cmvn_stats_kernel: one block per utterance,
-// thread t sums column t % nbins over the rows r = t / nbins (mod the row groups) in fp64, the
-// groups combined in a fixed order (deterministic; fp64 leaves only the reference's own fp32
-// cancellation error, which the parity test bounds) -> stats[b] = {mean[nbins], std[nbins]}.
-__global__ void __launch_bounds__(256) cmvn_stats_kernel(const float* __restrict__ feats, const int* __restrict__ frame_off,
-                                                         int nbins, int cmvn, float* __restrict__ stats) {
-  const int b = blockIdx.x;
+// std = sqrt(max(var, 1e-10)), x = (x - mean) / std).  cmvn_partial_kernel: grid (B, MMS_CMVN_SPLIT),
+// block (b, s) sums the s-th slice of utterance b's frames; thread t takes column t % nbins over
+// the slice's rows r = t / nbins (mod the row groups), in fp64; the groups are combined in a fixed
+// order -> part[b][s] = {sum[nbins], sumsq[nbins]}.  cmvn_fold_kernel folds the slices in order ->
+// stats[b] = {mean[nbins], std[nbins]}.  Deterministic; fp64 leaves only the reference's own fp32
+// cancellation error, which the parity test bounds.
+__global__ void __launch_bounds__(256) cmvn_partial_kernel(const float* __restrict__ feats, const int* __restrict__ frame_off,
+                                                           int nbins, double* __restrict__ part) {
+  const int b = blockIdx.x, sl = blockIdx.y, ns = gridDim.y;
   const int f0 = frame_off[b], T = frame_off[b + 1] - f0;
+  const int t0 = (int)((long)T * sl / ns), t1 = (int)((long)T * (sl + 1) / ns);
   const int groups = blockDim.x / nbins;          // >= 1 (nbins <= 256)
   const int c = threadIdx.x % nbins, g = threadIdx.x / nbins;
   __shared__ double s_sum[256], s_sq[256];
   double sm = 0.0, sq = 0.0;
   if (g < groups) {
     const float* col = feats + (long)f0 * nbins + c;
-    for (int t = g; t < T; t += groups) {
+    for (int t = t0 + g; t < t1; t += groups) {
       const double v = col[(long)t * nbins];
       sm += v;
       sq += v * v;
@@ -208,15 +257,31 @@ __global__ void __launch_bounds__(256) cmvn_stats_kernel(const float* __restrict
   if (threadIdx.x < nbins) {
     double a = 0.0, q = 0.0;
     for (int k = 0; k < groups; ++k) { a += s_sum[k * nbins + threadIdx.x]; q += s_sq[k * nbins + threadIdx.x]; }
-    float mean = 0.f, sd = 1.f;
-    if (cmvn && T > 0) {
-      const double mu = a / T;
-      mean = (float)mu;
-      sd = (float)sqrt(fmax(q / T - mu * mu, 1e-10));
-    }
-    stats[(long)b * 2 * nbins + threadIdx.x] = mean;
-    stats[(long)b * 2 * nbins + nbins + threadIdx.x] = sd;
+    double* out = part + ((long)b * ns + sl) * 2 * nbins;
+    out[threadIdx.x] = a;
+    out[nbins + threadIdx.x] = q;
   }
+}
+
+__global__ void __launch_bounds__(256) cmvn_fold_kernel(const double* __restrict__ part, const int* __restrict__ frame_off,
+                                                        int nbins, int ns, int cmvn, float* __restrict__ stats) {
+  const int b = blockIdx.x, c = threadIdx.x;
+  if (c >= nbins) return;
+  const int T = frame_off[b + 1] - frame_off[b];
+  double a = 0.0, q = 0.0;
+  for (int sl = 0; sl < ns; ++sl) {
+    const double* p = part + ((long)b * ns + sl) * 2 * nbins;
+    a += p[c];
+    q += p[nbins + c];
+  }
+  float mean = 0.f, sd = 1.f;
+  if (cmvn && T > 0) {
+    const double mu = a / T;
+    mean = (float)mu;
+    sd = (float)sqrt(fmax(q / T - mu * mu, 1e-10));
+  }
+  stats[(long)b * 2 * nbins + c] = mean;
+  stats[(long)b * 2 * nbins + nbins + c] = sd;
 }
 
 // normalise + collate [B][Tmax][nbins] fp16 (zero rows past each utterance's length): a flat
@@ -333,7 +398,15 @@ extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, cons
   MMS_REQUIRE(mel_range != nullptr, "fbank: mel_range required");
   if (init_consts(s)) return 1;
   if (total_frames == 0) return 0;
-  hipLaunchKernelGGL(fbank_kernel, dim3((total_frames + FPB - 1) / FPB), dim3(64 * FB_WAVES), 0, s, wave, wave_off,
+  // persistent: 4 blocks (16 waves) per CU at most, each building its LDS tables once
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int grid = std::min((total_frames + FB_WAVES - 1) / FB_WAVES, 4 * ncu);
+  hipLaunchKernelGGL(fbank_kernel, dim3(grid), dim3(64 * FB_WAVES), 0, s, wave, wave_off,
                      frame_off, B, total_frames, mel_banks, mel_range, nbins, feats);
   return mms::check_launch("fbank");
 }
@@ -343,8 +416,12 @@ extern "C" int mms2ut_fbank_cmvn_collate(const float* feats, const int32_t* fram
   MMS_REQUIRE(nbins > 0 && nbins <= 256 && nbins % 4 == 0, "cmvn: nbins must be a multiple of 4, <= 256");
   MMS_REQUIRE(((uintptr_t)feats & 15) == 0 && ((uintptr_t)out & 7) == 0 && stats, "cmvn: feats / out misaligned");
   if (B == 0) return 0;
-  hipLaunchKernelGGL(cmvn_stats_kernel, dim3(B), dim3(256), 0, s, feats, frame_off, nbins, cmvn, stats);
-  if (int rc = mms::check_launch("cmvn_stats")) return rc;
+  // fp64 slice partials after the fp32 stats (8-B aligned): see include/mms2ut.h
+  double* part = reinterpret_cast<double*>(stats + ((2L * B * nbins + 1) & ~1L));
+  hipLaunchKernelGGL(cmvn_partial_kernel, dim3(B, MMS_CMVN_SPLIT), dim3(256), 0, s, feats, frame_off, nbins, part);
+  if (int rc = mms::check_launch("cmvn_partial")) return rc;
+  hipLaunchKernelGGL(cmvn_fold_kernel, dim3(B), dim3(nbins), 0, s, part, frame_off, nbins, MMS_CMVN_SPLIT, cmvn, stats);
+  if (int rc = mms::check_launch("cmvn_fold")) return rc;
   const long n4 = (long)B * Tmax * nbins / 4;
   if (n4 == 0) return 0;
   hipLaunchKernelGGL(cmvn_apply_kernel, dim3((unsigned)std::min<long>((n4 + 255) / 256, 4096)), dim3(256), 0, s,

@@ -906,9 +906,14 @@ def fbank(wave, wave_off, frame_off, total_frames, banks, mel_range, nbins=80):
     return feats
 
 
+CMVN_SPLIT = 8   # include/mms2ut.h MMS_CMVN_SPLIT
+
+
 def cmvn_collate(feats, frame_off, B, Tmax, nbins=80, cmvn=True):
     out = torch.empty(B, Tmax, nbins, dtype=F16, device=feats.device)
-    stats = torch.empty(B, 2, nbins, dtype=torch.float32, device=feats.device)
+    # include/mms2ut.h MMS_CMVN_WS_FLOATS: fp32 stats, then fp64 slice partials
+    stats = torch.empty(((2 * B * nbins + 1) & ~1) + 2 * B * CMVN_SPLIT * 2 * nbins, dtype=torch.float32,
+                        device=feats.device)
     call("mms2ut_fbank_cmvn_collate", feats.data_ptr(), frame_off.data_ptr(), B, Tmax, nbins,
          int(cmvn), stats.data_ptr(), out.data_ptr(), _s())
     return out
