@@ -682,6 +682,8 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
       float* Dr = sD[buf];
       const uint64_t zctr = P.offset + (uint64_t)z * Tq * (uint64_t)P.Tk;  // RNG counter of (z, 0, 0)
       const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)Tq * P.Tk - 1);  // uniform
+      // every row's counters start even (even base, even key length): key pairs 2m, 2m+1 share a hash
+      const bool hi_pairs = hi_fast && (zctr & 1) == 0 && (P.Tk & 1) == 0;
       const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
       // ---- phase 1: staged rows -> LDS, D = rowsum(dO*O); prefetch the next chunk / head
       PH_STAMP(1 + 5 * gc);
@@ -765,7 +767,21 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
             bool keep[4] = {true, true, true, true};
             if (P.thresh) {
               const uint64_t c0 = zctr + (uint32_t)((qbase + q0 + 4 * g) * P.Tk + key_own);
-              if (hi_fast) {
+              if (hi_pairs) {
+                // lanes l, l^1 hold keys 2m, 2m+1 whose counters form one hash pair on every row
+                // (even row stride and base): each lane mixes two of the four rows' pairs and the
+                // lanes swap results (DPP quad_perm [1,0,3,2]) -- one mixer per two elements,
+                // bit-identical to mms_keep_hi
+                const bool odd = (lane & 1) != 0;
+                const uint32_t p0 = (uint32_t)(c0 >> 1), st = (uint32_t)P.Tk >> 1;
+                const uint32_t ha = mms_mix32((p0 + (odd ? 2 * st : 0u)) ^ hi_mix);
+                const uint32_t hb = mms_mix32((p0 + (odd ? 3 * st : st)) ^ hi_mix);
+                const uint32_t pa = (uint32_t)__builtin_amdgcn_mov_dpp((int)ha, 0xB1, 0xF, 0xF, false);
+                const uint32_t pb = (uint32_t)__builtin_amdgcn_mov_dpp((int)hb, 0xB1, 0xF, 0xF, false);
+                const uint32_t h4[4] = {odd ? pa : ha, odd ? pb : hb, odd ? ha : pa, odd ? hb : pb};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) keep[r] = (odd ? h4[r] >> 16 : h4[r] & 0xffffu) >= P.thresh;
+              } else if (hi_fast) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) keep[r] = mms_keep_hi(hi_mix, c0 + (uint32_t)(r * P.Tk), P.thresh);
               } else {
