@@ -18,6 +18,8 @@ shapes = [("qkv fwd", 10000, 2304, 768, "f16"), ("out-proj fwd", 10000, 768, 768
           ("fc1 fwd", 10000, 3072, 768, "relu_drop"), ("fc2 fwd", 10000, 768, 3072, "drop_resid"),
           ("qkv dgrad", 10000, 768, 2304, "f16"), ("fc1 dgrad", 10000, 768, 3072, "f16"),
           ("fc2 dgrad", 10000, 3072, 768, "relu_drop_bwd"), ("out-proj M11000", 11000, 768, 768, "f16"),
+          ("out-proj M12000", 12000, 768, 768, "drop_resid"), ("fc2 fwd M12000", 12000, 768, 3072, "drop_resid"),
+          ("qkv dgrad M12000", 12000, 768, 2304, "f16"),
           ("dec fc1 fwd", 3000, 3072, 768, "relu_drop")]
 EPI = {"f16": K.EPI_F16, "drop_resid": K.EPI_DROP_RESID, "relu_drop": K.EPI_RELU_DROP, "relu_drop_bwd": K.EPI_RELU_DROP_BWD}
 for name, M, N, Kd, epi in shapes:
