@@ -680,50 +680,74 @@ __global__ void token_embed_fwd_kernel(const int64_t* __restrict__ tok, const h1
 }
 
 // Embedding-gradient scatter dE[v] += sum_{p: tok[p] = v} scale * dropout(dx[p]), deterministic:
-// one block per vocabulary row walks the token positions in order, 256 at a time (a wave ballot
-// per chunk marks the matches), and each thread accumulates its own columns over the matches in
-// ascending position order — no float atomics, so the gradient is bit-reproducible run to run.
-constexpr int TEB_NT = 256, TEB_COLS = 4;   // D <= 1024
+// one block per vocabulary row, its 4 waves each walking a contiguous quarter of the token
+// positions in order (4 x 64 token ids loaded per step, one ballot per 64) with no block barrier
+// in the walk.  A lane owns 8 consecutive columns (16-B row loads; D/8 lane slots over TEB_PASS
+// passes); every match row is added in ascending position order, then the 4 wave partials are
+// summed in wave order through LDS — no float atomics, so the gradient is bit-reproducible.
+constexpr int TEB_NT = 256, TEB_PASS = 2, TEB_UNROLL = 4;   // D <= 64 * 8 * TEB_PASS = 1024, D % 8 == 0
 __global__ void __launch_bounds__(TEB_NT) token_embed_bwd_kernel(
     const int64_t* __restrict__ tok, const h16* __restrict__ dx, float* __restrict__ dE, long N, int D, int pad,
     float scale, float p, uint32_t thresh, uint64_t seed, uint64_t offset) {
   if (thresh) seed = mms_step_seed(seed);
   const int v = blockIdx.x;
   if (v == pad) return;  // nn.Embedding(padding_idx): no grad to the pad row
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __shared__ uint64_t sm[TEB_NT / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(16))) float part[TEB_NT / 64][64 * 8 * TEB_PASS];
   const float ds = thresh ? 1.f / (1.f - p) : 1.f;
-  float acc[TEB_COLS] = {0.f, 0.f, 0.f, 0.f};
-  for (long c0 = 0; c0 < N; c0 += TEB_NT) {
-    const long q = c0 + tid;
-    const uint64_t bits = __ballot(q < N && tok[q] == v);
-    if (lane == 0) sm[w] = bits;
-    __syncthreads();
+  float acc[TEB_PASS][8];
 #pragma unroll
-    for (int ww = 0; ww < TEB_NT / 64; ++ww) {
-      uint64_t b = sm[ww];
+  for (int k = 0; k < TEB_PASS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
+  const long q = ((N + 4 * 64 - 1) / (4 * 64)) * 64;   // positions per wave, whole 64-id chunks
+  const long beg = w * q, end = min(N, beg + q);
+  for (long c0 = beg; c0 < end; c0 += 64 * TEB_UNROLL) {
+    uint64_t bits[TEB_UNROLL];
+    int64_t t[TEB_UNROLL];
+#pragma unroll
+    for (int u = 0; u < TEB_UNROLL; ++u) {
+      const long i = c0 + u * 64 + lane;
+      t[u] = i < end ? tok[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < TEB_UNROLL; ++u) bits[u] = __ballot(t[u] == v);
+#pragma unroll
+    for (int u = 0; u < TEB_UNROLL; ++u) {
+      uint64_t b = bits[u];
       while (b) {
-        const int l = __ffsll((unsigned long long)b) - 1;
+        const long row = c0 + u * 64 + (__ffsll((unsigned long long)b) - 1);
         b &= b - 1;
-        const long row = c0 + ww * 64 + l;
 #pragma unroll
-        for (int k = 0; k < TEB_COLS; ++k) {
-          const int d = tid + k * TEB_NT;
+        for (int k = 0; k < TEB_PASS; ++k) {
+          const int d = (lane + 64 * k) * 8;
           if (d < D) {
-            float x = (float)dx[row * D + d] * scale;
-            if (thresh) x = mms_keep(seed, offset + row * D + d, thresh) ? x * ds : 0.f;
-            acc[k] += x;
+            const h16x8 x8 = *reinterpret_cast<const h16x8*>(dx + row * D + d);
+            bool kp[8] = {true, true, true, true, true, true, true, true};
+            if (thresh) {
+              bool k0[4], k1[4];
+              mms_keep4(seed, offset + (uint64_t)(row * D + d), thresh, k0);
+              mms_keep4(seed, offset + (uint64_t)(row * D + d) + 4, thresh, k1);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) { kp[e] = k0[e]; kp[e + 4] = k1[e]; }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float xv = (float)x8[e] * scale;
+              acc[k][e] += thresh ? (kp[e] ? xv * ds : 0.f) : xv;
+            }
           }
         }
       }
     }
-    __syncthreads();
   }
 #pragma unroll
-  for (int k = 0; k < TEB_COLS; ++k) {
-    const int d = tid + k * TEB_NT;
-    if (d < D) dE[(long)v * D + d] += acc[k];
-  }
+  for (int k = 0; k < TEB_PASS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[w][(lane + 64 * k) * 8 + e] = acc[k][e];
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += TEB_NT)
+    dE[(long)v * D + d] += ((part[0][d] + part[1][d]) + part[2][d]) + part[3][d];
 }
 
 __global__ void add_f32_to_f16_kernel(const h16* __restrict__ a, const float* __restrict__ b,
@@ -1150,8 +1174,9 @@ extern "C" int mms2ut_token_embed_fwd(const int64_t* tok, const h16* E, const h1
 extern "C" int mms2ut_token_embed_bwd(const int64_t* tok, const h16* dx, float* dE32, int B, int T,
                                       int D, int V, int pad_idx, float scale, float p, uint64_t seed,
                                       uint64_t offset, hipStream_t s) {
-  MMS_REQUIRE(D > 0 && D <= TEB_NT * TEB_COLS && V > 0, "token_embed_bwd: D=%d (max %d) V=%d", D,
-              TEB_NT * TEB_COLS, V);
+  MMS_REQUIRE(D > 0 && D <= 64 * 8 * TEB_PASS && D % 8 == 0 && V > 0,
+              "token_embed_bwd: D=%d (max %d, a multiple of 8) V=%d", D, 64 * 8 * TEB_PASS, V);
+  MMS_REQUIRE(((uintptr_t)dx & 15) == 0, "token_embed_bwd: dx must be 16-B aligned");
   const long n = (long)B * T;
   if (n == 0) return 0;
   hipLaunchKernelGGL(token_embed_bwd_kernel, dim3(V), dim3(TEB_NT), 0, s, tok, dx, dE32, n, D,

@@ -17,9 +17,14 @@ __global__ void __launch_bounds__(256) transpose_batch_kernel(const h16* __restr
                                                               const mms2ut_transpose_desc* __restrict__ d, int n) {
   __shared__ __attribute__((aligned(16))) h16 tile[TT * TLD];
   const int b = blockIdx.x;
-  // matrix of this block: the descriptors are sorted by first tile (n is small: one scalar scan)
-  int i = 0;
-  while (i + 1 < n && d[i + 1].tile0 <= b) ++i;
+  // matrix of this block: the descriptors are sorted by first tile; binary search for the last one
+  // with tile0 <= b (a linear scan is a chain of up to n dependent scalar loads per block)
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].tile0 <= b) lo = mid; else hi = mid - 1;
+  }
+  const int i = lo;
   const mms2ut_transpose_desc D = d[i];
   const int tiles_c = (D.cols + TT - 1) / TT;
   const int t = b - D.tile0, r0 = (t / tiles_c) * TT, c0 = (t % tiles_c) * TT;

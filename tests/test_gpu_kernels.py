@@ -486,3 +486,31 @@ def test_transposed_weight_images(K):
         K.TransposedWeights.active = None
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("B,T,D,V,p", [(37, 301, 768, 1004, 0.1), (3, 50, 256, 40, 0.0), (1, 1, 512, 7, 0.3),
+                                       (64, 200, 1024, 1004, 0.1)])
+def test_token_embed_bwd(K, B, T, D, V, p):
+    """Embedding-gradient scatter (csrc/ops.hip token_embed_bwd_kernel) against torch index_add of the
+    scaled, dropout-masked rows (mask from the library's own counter RNG); the pad row gets nothing;
+    run twice into the same accumulator: bit-identical increments (deterministic order)."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    pad = 1
+    tok = torch.randint(0, V, (B, T), generator=g, device="cuda")
+    tok[:, -T // 5:] = pad
+    dx = torch.randn(B * T, D, generator=g, device="cuda").half()
+    scale, seed, off = math.sqrt(D), 123, 4096
+    dE = torch.zeros(V, D, device="cuda")
+    K.token_embed_bwd(tok, dx, dE, B, T, D, pad, scale, p, (seed, off))
+    first = dE.clone()
+    K.token_embed_bwd(tok, dx, dE, B, T, D, pad, scale, p, (seed, off))
+    torch.cuda.synchronize()
+    x = dx.float() * scale
+    if p > 0:
+        keep = K.dropout_mask(B * T * D, p, seed, off, "cuda").view(B * T, D).bool()
+        x = torch.where(keep, x / (1 - p), torch.zeros_like(x))
+    ref = torch.zeros(V, D, device="cuda").index_add_(0, tok.reshape(-1), x)
+    ref[pad] = 0
+    assert rel(first, ref) < 1e-5
+    assert torch.equal(first[pad], torch.zeros_like(first[pad]))
+    assert torch.equal(dE, first + first)
