@@ -615,6 +615,27 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int t
 // Out-of-range rows/k-rows read as zero through the buffer descriptor's range check, so tails
 // need no predication; a K-contiguous operand needs K % 64 == 0 (host routing).
 // ------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------
+// BK = 32 variant: 16 KiB stages, a 4-deep ring in the same 64 KiB (2 blocks per CU), so two
+// k-tiles stay in flight across every barrier (counted vmcnt, raw s_barrier) instead of one.
+// K-contiguous images are [128 rows][32 k] (64-B rows, chunk ^ f(row), f = bits 1,2 of the
+// row: conflict-free for ds_read_b128's lane groups); MN-contiguous images are the BK = 64
+// layout's first 32 k-rows.
+// ------------------------------------------------------------------------------------------
+constexpr int BK32 = 32, T32_BYTES = 128 * 32 * 2, ST32 = 4;
+MMS_DEV int swz32(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1); }
+
+template <bool KC>
+MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
+  if (KC) {
+    const int r = sub + (lane & 15);
+    const int c = lane >> 4;
+    s16x8 v = *reinterpret_cast<const s16x8*>(lds + r * 64 + ((c ^ swz32(r)) << 4));
+    return __builtin_bit_cast(h16x8, v);
+  }
+  return read_frag<false>(lds, sub, 0, lane);
+}
+
 typedef __attribute__((address_space(3))) void lds_void;
 
 template <bool KC>
@@ -694,25 +715,46 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
       dma_tile<B_KC>(rb, SB(s), P.ldb, bn, k_rel(s, B_KC), wid, lane);
     }
   }
+  // An MN-contiguous operand is read with ds_read_b64_tr_b16, and the compiler cannot tell those
+  // reads from the LDS-DMA writes still in flight: it puts a vmcnt(0) in front of any such read
+  // issued after a DMA, which would make every k-step wait for the NEXT stage's DMA to land.  With
+  // a transpose-read operand the k-step therefore reads both k-halves' fragments first and issues
+  // the next stage's DMA behind them (the DMA then overlaps the MFMAs, as in the K-contiguous form).
+  constexpr bool READ_FIRST = !A_KC || !B_KC;
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt must have landed; leave the younger stages (issued earlier) in flight
     const int younger = min(STAGES - 2, nk - 1 - kt);
     if (STAGES >= 3 && younger >= 1) wait_vm<8>(); else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     const int nxt = kt + STAGES - 1;
+    const int cur = kt % STAGES;
+    h16x8 fa2[2][4], fb2[2][4];
+    if (READ_FIRST) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa2[kk][i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
+      }
+    }
     if (nxt < nk) {
       const int sb = nxt % STAGES;
       dma_tile<A_KC>(ra, SA(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
       dma_tile<B_KC>(rb, SB(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
     }
-    const int cur = kt % STAGES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       h16x8 fa[4], fb[4];
+      if (READ_FIRST) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
+        for (int i = 0; i < 4; ++i) { fa[i] = fa2[kk][i]; fb[i] = fb2[kk][i]; }
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
+        for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
+      }
       if (PRI) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -799,27 +841,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_group_wgrad_kernel(GemmGroup G, in
     dma_gemm_tile<false, false, MMS_EPI_F16, 2, true, false>(P, smem, 0, first_m + w % gsize, w / gsize);
   }
   stamp_end(G.stamps, t_start);
-}
-
-// ------------------------------------------------------------------------------------------
-// BK = 32 variant: 16 KiB stages, a 4-deep ring in the same 64 KiB (2 blocks per CU), so two
-// k-tiles stay in flight across every barrier (counted vmcnt, raw s_barrier) instead of one.
-// K-contiguous images are [128 rows][32 k] (64-B rows, chunk ^ f(row), f = bits 1,2 of the
-// row: conflict-free for ds_read_b128's lane groups); MN-contiguous images are the BK = 64
-// layout's first 32 k-rows.
-// ------------------------------------------------------------------------------------------
-constexpr int BK32 = 32, T32_BYTES = 128 * 32 * 2, ST32 = 4;
-MMS_DEV int swz32(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 1); }
-
-template <bool KC>
-MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
-  if (KC) {
-    const int r = sub + (lane & 15);
-    const int c = lane >> 4;
-    s16x8 v = *reinterpret_cast<const s16x8*>(lds + r * 64 + ((c ^ swz32(r)) << 4));
-    return __builtin_bit_cast(h16x8, v);
-  }
-  return read_frag<false>(lds, sub, 0, lane);
 }
 
 // ------------------------------------------------------------------------------------------

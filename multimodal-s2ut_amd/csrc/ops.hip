@@ -265,13 +265,17 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const h16* __restrict__ dy,
   }
 }
 
-// LayerNorm backward for D % 256 == 0 (the step's D = 768): a half-wave per row so every global
-// access is a 16-B lane access (whole 512-B row segments per half-wave instruction).  Same row
-// blocking as ln_bwd_kernel (16 rows per block, part[block][2][D]); wave w takes row pairs w and
-// w + 4, all their loads (x, dy, dres) in flight at once.  dgamma / dbeta column partials are
-// folded across the two half-waves by a lane-32 shuffle and across the 4 waves through LDS.
-template <int C8, int NP>  // 16-B chunks per lane per row = D / 256; row pairs per wave (8*NP rows per block)
-__global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ dy, const h16* __restrict__ x,
+// LayerNorm backward for D % 256 == 0 (the step's D = 768), one wave per row: lane l owns the
+// 4-column quads l, l + 64, ... (C = D / 256 of them, 8-B accesses; every wave instruction covers a
+// whole 512-B row segment).  Blocks take `iters` groups of 8 rows and fold their dgamma / dbeta
+// into one partial row (reduced by colsum_parts on the side stream); wave w takes rows 2w, then
+// 2w + 1 of each group.  Per lane: gamma, dgamma, dbeta (12 floats each at D = 768) and one row's
+// x / dy / dres quads — 114-126 VGPRs, 4 waves per SIMD.  Measured against the half-wave layout
+// (a half-wave per row, 24 columns per lane: 213 VGPRs, 2 waves per SIMD) and this kernel with two
+// rows in flight per wave (181 VGPRs): 17.61-17.64 vs 17.69-17.71 / 17.71-17.73 ms per step
+// (profiles/round3_v5_ln_bwd_ab.txt).
+template <int C>
+__global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ dy, const h16* __restrict__ x,
                                                        const h16* __restrict__ g, const float* __restrict__ mean,
                                                        const float* __restrict__ rstd, const h16* __restrict__ dres,
                                                        h16* __restrict__ dx, float* __restrict__ part,
@@ -279,134 +283,126 @@ __global__ void __launch_bounds__(256) ln_bwd16_kernel(const h16* __restrict__ d
                                                        uint32_t thresh, uint64_t seed, uint64_t offset,
                                                        long dgrp, long dgrp_out, float pin, uint32_t thin,
                                                        uint64_t sin, uint64_t oin, int iters) {
+  constexpr int NR = 1;   // rows in flight per wave
   if (thresh) seed = mms_step_seed(seed);
   if (thin) sin = mms_step_seed(sin);
-  __shared__ __attribute__((aligned(16))) float red[4][2][C8 * 256];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
+  __shared__ __attribute__((aligned(16))) float red[4][2][C * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float dscale = thresh ? 1.f / (1.f - p) : 1.f;
   const float invD = 1.f / D;
-  float gam[C8][8], dg[C8][8], db[C8][8];
+  float gam[C][4], dg[C][4], db[C][4];
 #pragma unroll
-  for (int c = 0; c < C8; ++c) {
-    const h16x8 gg = *reinterpret_cast<const h16x8*>(g + (hl + 32 * c) * 8);
+  for (int c = 0; c < C; ++c) {
+    const h16x4 gg = ld4(g + (lane + 64 * c) * 4);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { gam[c][e] = (float)gg[e]; dg[c][e] = 0.f; db[c][e] = 0.f; }
+    for (int e = 0; e < 4; ++e) { gam[c][e] = (float)gg[e]; dg[c][e] = 0.f; db[c][e] = 0.f; }
   }
-  // the block walks `iters` consecutive groups of 8*NP rows, keeping its dgamma / dbeta column sums
-  // in registers across them: one partial row per block instead of one per group
-  for (int it = 0; it < iters; ++it) {
-    const long rb = ((long)blockIdx.x * iters + it) * 8 * NP;
+  const h16x4 z4 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+#pragma unroll 1
+  for (int it = 0; it < iters * (2 / NR); ++it) {
+    const long rb = ((long)blockIdx.x * iters + it / (2 / NR)) * 8 + (it % (2 / NR));
     if (rb >= rows) break;
-    const h16x8 z8 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
-    h16x8 xv[NP][C8], dv[NP][C8], rv[NP][C8];
-    float mu[NP], rs[NP];
-    long row[NP];
-  #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      row[k] = rb + 2 * (w + 4 * k) + half;
+    h16x4 xv[NR][C], dv[NR][C], rv[NR][C];
+    float mu[NR], rs[NR];
+    long row[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      row[k] = rb + 2 * w + k;   // NR = 1: rb carries the row's parity
       const bool ok = row[k] < rows;
       mu[k] = ok ? mean[row[k]] : 0.f;
       rs[k] = ok ? rstd[row[k]] : 0.f;
-  #pragma unroll
-      for (int c = 0; c < C8; ++c) {
-        const long off = row[k] * D + (hl + 32 * c) * 8;
-        xv[k][c] = ok ? *reinterpret_cast<const h16x8*>(x + off) : z8;
-        // optional dy layout remap (rows grouped dgrp at a time into dgrp_out-row groups)
-        const long drow = dgrp ? (row[k] / dgrp) * dgrp_out + row[k] % dgrp : row[k];
-        dv[k][c] = ok ? *reinterpret_cast<const h16x8*>(dy + drow * D + (hl + 32 * c) * 8) : z8;
-        rv[k][c] = (ok && dres && dx) ? *reinterpret_cast<const h16x8*>(dres + off) : z8;
+      // (32-bit row arithmetic: the host guarantees rows * D < 2^31)
+      const int r32 = (int)row[k], g32 = (int)dgrp;
+      const int drow = g32 ? (r32 / g32) * (int)dgrp_out + r32 % g32 : r32;
+      const h16* xr = x + (long)(r32 * D + lane * 4);
+      const h16* dr = dy + (long)(drow * D + lane * 4);
+      const h16* rr = dres + (long)(r32 * D + lane * 4);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        xv[k][c] = ok ? ld4(xr + 256 * c) : z4;
+        dv[k][c] = ok ? ld4(dr + 256 * c) : z4;
+        rv[k][c] = (ok && dres && dx) ? ld4(rr + 256 * c) : z4;
       }
     }
     if (thin) {
       // dy = dropout(dy_in) with the counters of the unpadded element index, rounded to fp16 as a
       // separate dropout pass would store it
       const float dsi = 1.f / (1.f - pin);
-  #pragma unroll
-      for (int k = 0; k < NP; ++k)
-  #pragma unroll
-        for (int c = 0; c < C8; ++c) {
-          bool k0[4], k1[4];
-          const uint64_t ctr = oin + (uint64_t)(row[k] * D + (hl + 32 * c) * 8);
-          mms_keep4(sin, ctr, thin, k0);
-          mms_keep4(sin, ctr + 4, thin, k1);
-  #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            dv[k][c][e] = (h16)(k0[e] ? (float)dv[k][c][e] * dsi : 0.f);
-            dv[k][c][e + 4] = (h16)(k1[e] ? (float)dv[k][c][e + 4] * dsi : 0.f);
-          }
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          bool kp[4];
+          mms_keep4(sin, oin + (uint64_t)((int)row[k] * D + (lane + 64 * c) * 4), thin, kp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dv[k][c][e] = (h16)(kp[e] ? (float)dv[k][c][e] * dsi : 0.f);
         }
     }
-  #pragma unroll
-    for (int k = 0; k < NP; ++k) {
-      float s1 = 0.f, s2 = 0.f;
-  #pragma unroll
-      for (int c = 0; c < C8; ++c)
-  #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+    float s1[NR], s2[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      s1[k] = 0.f;
+      s2[k] = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
           const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
           const float d = (float)dv[k][c][e];
           const float gd = d * gam[c][e];
-          s1 += gd * xh;
-          s2 += gd;
+          s1[k] += gd * xh;
+          s2[k] += gd;
           dg[c][e] += d * xh;
           db[c][e] += d;
         }
-      if (!dx) continue;
-  #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) {
-        s1 += __shfl_xor(s1, o, 64);
-        s2 += __shfl_xor(s2, o, 64);
+    }
+    if (!dx) continue;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      s1[k] = wave_sum(s1[k]) * invD;
+      s2[k] = wave_sum(s2[k]) * invD;
+    }
+    // re-derive x-hat and dy from the fp16 quads below instead of keeping the first pass's fp32
+    // copies alive across the reductions (they would double the per-row registers)
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
+        u32x2_ a = __builtin_bit_cast(u32x2_, xv[k][c]), b = __builtin_bit_cast(u32x2_, dv[k][c]);
+        asm volatile("" : "+v"(a), "+v"(b));
+        xv[k][c] = __builtin_bit_cast(h16x4, a);
+        dv[k][c] = __builtin_bit_cast(h16x4, b);
       }
-      s1 *= invD;
-      s2 *= invD;
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
       if (row[k] >= rows) continue;
-  #pragma unroll
-      for (int c = 0; c < C8; ++c) {
-        const long off = row[k] * D + (hl + 32 * c) * 8;
-        float o8[8];
-        h16x8 ov;
-  #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+      const int off0 = (int)row[k] * D + lane * 4;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const int off = off0 + 256 * c;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
           const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
-          o8[e] = rs[k] * ((float)dv[k][c][e] * gam[c][e] - xh * s1 - s2) + (float)rv[k][c][e];
-          ov[e] = (h16)o8[e];
+          o[e] = rs[k] * ((float)dv[k][c][e] * gam[c][e] - xh * s1[k] - s2[k]) + (float)rv[k][c][e];
         }
-        *reinterpret_cast<h16x8*>(dx + off) = ov;
+        st4(dx + (long)off0 + 256 * c, o[0], o[1], o[2], o[3]);
         if (dxd) {
-          bool k0[4] = {true, true, true, true}, k1[4] = {true, true, true, true};
-          if (thresh) {
-            mms_keep4(seed, offset + (uint64_t)off, thresh, k0);
-            mms_keep4(seed, offset + (uint64_t)off + 4, thresh, k1);
-          }
-  #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            ov[e] = (h16)(k0[e] ? o8[e] * dscale : 0.f);
-            ov[e + 4] = (h16)(k1[e] ? o8[e + 4] * dscale : 0.f);
-          }
-          *reinterpret_cast<h16x8*>(dxd + off) = ov;
+          bool kp[4] = {true, true, true, true};
+          if (thresh) mms_keep4(seed, offset + (uint64_t)off, thresh, kp);
+          st4(dxd + (long)off0 + 256 * c, kp[0] ? o[0] * dscale : 0.f, kp[1] ? o[1] * dscale : 0.f, kp[2] ? o[2] * dscale : 0.f,
+              kp[3] ? o[3] * dscale : 0.f);
         }
       }
     }
   }
-  // fold the two half-waves (same columns), then the 4 waves through LDS
 #pragma unroll
-  for (int c = 0; c < C8; ++c)
+  for (int c = 0; c < C; ++c)
+    *reinterpret_cast<f32x4*>(&red[w][0][(lane + 64 * c) * 4]) = f32x4{dg[c][0], dg[c][1], dg[c][2], dg[c][3]};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      dg[c][e] += __shfl_xor(dg[c][e], 32, 64);
-      db[c][e] += __shfl_xor(db[c][e], 32, 64);
-    }
-  if (half == 0) {
-#pragma unroll
-    for (int c = 0; c < C8; ++c)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        *reinterpret_cast<f32x4*>(&red[w][0][(hl + 32 * c) * 8 + 4 * h]) =
-            f32x4{dg[c][4 * h], dg[c][4 * h + 1], dg[c][4 * h + 2], dg[c][4 * h + 3]};
-        *reinterpret_cast<f32x4*>(&red[w][1][(hl + 32 * c) * 8 + 4 * h]) =
-            f32x4{db[c][4 * h], db[c][4 * h + 1], db[c][4 * h + 2], db[c][4 * h + 3]};
-      }
-  }
+  for (int c = 0; c < C; ++c)
+    *reinterpret_cast<f32x4*>(&red[w][1][(lane + 64 * c) * 4]) = f32x4{db[c][0], db[c][1], db[c][2], db[c][3]};
   __syncthreads();
   float* out = part + (long)blockIdx.x * 2 * D;
   for (int i = threadIdx.x; i < 2 * D / 4; i += 256) {
@@ -979,31 +975,25 @@ extern "C" int mms2ut_layernorm_fwd_ex(const h16* x, const h16* gamma, const h16
   });
 }
 
-// row pairs per wave of ln_bwd16 (D % 256 == 0): one — 8 rows per block, twice the blocks of the
-// 16-row layout: 18.95 vs 19.26 ms per training step over three interleaved A/B pairs (round 2,
-// round-2 scripts/ln_np_ab2.sh, git history; the in-step LN backward shares the CUs with the side-stream weight
-// gradients, where the shorter blocks interleave better)
-constexpr int kLnNP = 1;
-
 static bool ln16_path(int D) { return D % 256 == 0 && D <= 1024; }
 
 extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
   return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
 }
 
-// groups of 8*NP rows per ln_bwd16 block: enough blocks to fill the chip (1024), each folding its
-// groups' dgamma / dbeta into one partial row — the partials (rows / 8 x 6 KB
-// at D = 768, ~35 MB for the image LayerNorm) are what colsum_parts reads back on the side stream
+// groups of 8 rows per ln_bwd_w block: enough blocks to fill the chip (1024), each folding its
+// groups' dgamma / dbeta into one partial row — the partials (rows / 8 x 6 KB at D = 768 before
+// the folding) are what colsum_parts reads back on the side stream
 static int ln16_iters(int64_t rows) {
   constexpr long target = 1024;
-  const long groups = (rows + 8 * kLnNP - 1) / (8 * kLnNP);
+  const long groups = (rows + 7) / 8;
   const long it = (groups + target - 1) / target;
   return (int)(it > 1 ? it : 1);
 }
 
 extern "C" int mms2ut_layernorm_bwd_nparts(int64_t rows, int D) {
   if (!ln16_path(D)) return (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
-  const long rpb = 8L * kLnNP * ln16_iters(rows);
+  const long rpb = 8L * ln16_iters(rows);
   return (int)((rows + rpb - 1) / rpb);
 }
 
@@ -1018,14 +1008,13 @@ extern "C" int mms2ut_layernorm_bwd(const h16* dy, const h16* x, const h16* gamm
   if (rows == 0) return 0;
   const int nb = mms2ut_layernorm_bwd_nparts(rows, D);
   if (ln16_path(D)) {
-#define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
-                                          gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
-                                          offset, 0L, 0L, 0.f, 0u, (uint64_t)0, (uint64_t)0, ln16_iters(rows)); break;
-    switch ((D / 256) * 8 + kLnNP) {
-      CASE(1, kLnNP) CASE(2, kLnNP) CASE(3, kLnNP) CASE(4, kLnNP)
-    }
+    MMS_REQUIRE(rows * D < (1LL << 31), "layernorm_bwd: rows * D must be < 2^31 (32-bit row offsets)");
+#define CASE(C) case C: hipLaunchKernelGGL((ln_bwd_w_kernel<C>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, \
+                                           rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset, 0L, \
+                                           0L, 0.f, 0u, (uint64_t)0, (uint64_t)0, ln16_iters(rows)); break;
+    switch (D / 256) { CASE(1) CASE(2) CASE(3) CASE(4) }
 #undef CASE
-    return mms::check_launch("layernorm_bwd16");
+    return mms::check_launch("layernorm_bwd_w");
   }
   return pick_cpl(D / 4, [&](auto C) {
     constexpr int CPL = decltype(C)::value;
@@ -1052,13 +1041,13 @@ extern "C" int mms2ut_layernorm_bwd_ex(const h16* dy, const h16* x, const h16* g
   if (rows == 0) return 0;
   const int nb = mms2ut_layernorm_bwd_nparts(rows, D);
   const uint32_t thresh = mms_drop_thresh(p), thin = mms_drop_thresh(dy_p);
-#define CASE(C, NP) case C * 8 + NP: hipLaunchKernelGGL((ln_bwd16_kernel<C, NP>), dim3(nb), dim3(256), 0, s, dy, x, \
-                                          gamma, mean, rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, \
-                                          offset, (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset, \
-                                          ln16_iters(rows)); break;
-  switch ((D / 256) * 8 + kLnNP) {
-    CASE(1, kLnNP) CASE(2, kLnNP) CASE(3, kLnNP) CASE(4, kLnNP)
-  }
+  MMS_REQUIRE(rows * D < (1LL << 31) && (dy_grp == 0 || (rows / dy_grp + 1) * dy_grp_out * D < (1LL << 31)),
+              "layernorm_bwd_ex: row offsets must fit 32 bits");
+#define CASE(C) case C: hipLaunchKernelGGL((ln_bwd_w_kernel<C>), dim3(nb), dim3(256), 0, s, dy, x, gamma, mean, \
+                                           rstd, dres, dx, part, (long)rows, D, dxd, p, thresh, seed, offset, \
+                                           (long)dy_grp, (long)dy_grp_out, dy_p, thin, dy_seed, dy_offset, \
+                                           ln16_iters(rows)); break;
+  switch (D / 256) { CASE(1) CASE(2) CASE(3) CASE(4) }
 #undef CASE
   return mms::check_launch("layernorm_bwd_ex");
 }
