@@ -721,6 +721,9 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
   // a transpose-read operand the k-step therefore reads both k-halves' fragments first and issues
   // the next stage's DMA behind them (the DMA then overlaps the MFMAs, as in the K-contiguous form).
   constexpr bool READ_FIRST = !A_KC || !B_KC;
+  // All 16 fragments of the stage are read before its MFMAs (the second k-half's reads no longer
+  // wait behind the first half's MFMAs): 0-5 % faster isolated on the step's NT shapes, step flat
+  // (profiles/round3_v5_gemm_read_all_ab.txt).
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt must have landed; leave the younger stages (issued earlier) in flight
     const int younger = min(STAGES - 2, nk - 1 - kt);
@@ -728,8 +731,13 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
     __builtin_amdgcn_s_barrier();
     const int nxt = kt + STAGES - 1;
     const int cur = kt % STAGES;
+    if (!READ_FIRST && nxt < nk) {
+      const int sb = nxt % STAGES;
+      dma_tile<A_KC>(ra, SA(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
+      dma_tile<B_KC>(rb, SB(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
+    }
     h16x8 fa2[2][4], fb2[2][4];
-    if (READ_FIRST) {
+    {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
@@ -738,7 +746,7 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
         for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
       }
     }
-    if (nxt < nk) {
+    if (READ_FIRST && nxt < nk) {
       const int sb = nxt % STAGES;
       dma_tile<A_KC>(ra, SA(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
       dma_tile<B_KC>(rb, SB(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
@@ -746,15 +754,8 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       h16x8 fa[4], fb[4];
-      if (READ_FIRST) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { fa[i] = fa2[kk][i]; fb[i] = fb2[kk][i]; }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = read_frag<A_KC>(SA(cur), wm * 64 + i * 16, kk, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = read_frag<B_KC>(SB(cur), wn * 64 + j * 16, kk, lane);
-      }
+      for (int i = 0; i < 4; ++i) { fa[i] = fa2[kk][i]; fb[i] = fb2[kk][i]; }
       if (PRI) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
