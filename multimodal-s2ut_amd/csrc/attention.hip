@@ -139,6 +139,15 @@ MMS_DEV s16x8 ld16b(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(s16x8, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
 }
 
+// key length of batch row b (b wave-uniform) through the scalar cache: a vector load here would
+// share vmcnt with the register prefetches in flight, and waiting for it (the value feeds buffer
+// descriptors and loop bounds at once) would drain them all
+MMS_DEV int key_len_of(const AttnP& P, int b) {
+  if (!P.key_len) return P.Tk;
+  typedef const __attribute__((address_space(4))) int cint4;
+  const int v = ((cint4*)(unsigned long)P.key_len)[b];
+  return min(v, P.Tk);
+}
 MMS_DEV f32x4 mfma(h16x8 a, h16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
 
 MMS_DEV h16x8 pack8(f32x4 a, f32x4 b) {
@@ -182,7 +191,7 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
   const int qblk = blockIdx.x * OWN;
   const int w_row0 = qblk + w * 16, q_own = w_row0 + (lane & 15);  // this lane's query row
-  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+  const int klen = key_len_of(P, b);
   int kmax = klen;
   if (P.causal) kmax = min(kmax, qblk + OWN);
   const h16* Q = P.q + b * P.sqb + h * HD;
@@ -243,6 +252,11 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
     if constexpr (!SHORT) {
       __syncthreads();
       pf.store(sK, sV);
+      // every load issued so far has landed (the stores above waited for the tile's): re-define the
+      // Q fragments here, or the compiler -- unable to prove across the loop that their loads are
+      // done -- puts vmcnt(0) in front of the first QK^T MFMA, draining the next tile's prefetch
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
       __syncthreads();
       if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
     }
@@ -381,7 +395,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_kv_kernel(AttnP P) {
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
   const int kblk = blockIdx.x * OWN;
   const int key_own = kblk + w * 16 + (lane & 15);
-  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+  const int klen = key_len_of(P, b);
   const h16* Q = P.q + b * P.sqb + h * HD;
   const h16* K = P.k + b * P.skb + h * HD;
   const h16* V = P.v + b * P.svb + h * HD;
@@ -480,7 +494,7 @@ __global__ void __launch_bounds__(64 * NW) attn_bwd_q_kernel(AttnP P) {
   const int z = blockIdx.y, b = z / P.H, h = z % P.H;
   const int qblk = blockIdx.x * OWN;
   const int q_own = qblk + w * 16 + (lane & 15);
-  const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+  const int klen = key_len_of(P, b);
   int kmax = klen;
   if (P.causal) kmax = min(kmax, qblk + OWN);
   const h16* Q = P.q + b * P.sqb + h * HD;
@@ -622,12 +636,14 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
         (void*)(P.lse + (long)zc * Tq + qbase), (short)0, rows > 0 ? rows * 4 : 0, 0x00020000);
     rl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rL, tid * 4, 0, 0));
   };
-  auto load_kv = [&](int zc) {
+  // live = false: the same load instructions over an empty range (they return zeros without
+  // touching memory) -- see the LAST chunk below
+  auto load_kv = [&](int zc, bool live) {
     int tid_ = tid;
     asm volatile("" : "+v"(tid_));
     const int tid = tid_, lane = tid & 63, g = lane >> 4, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int bc = zc / P.H, hc = zc % P.H;
-    const int kl = P.key_len ? min(P.key_len[bc], P.Tk) : P.Tk;
+    const int kl = live ? key_len_of(P, bc) : 0;
     const auto rK = rsrc_rows(P.k + bc * P.skb + hc * HD, kl, P.ldk);
     const auto rV = rsrc_rows(P.v + bc * P.svb + hc * HD, kl, P.ldv);
 #pragma unroll
@@ -651,18 +667,25 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
   (void)ph_blk;
   PH_STAMP(0);
   load_chunk(z, 0);
-  load_kv(z);
+  load_kv(z, true);
   static_assert(QC * CH * sizeof(float) <= sizeof(sDS), "D partials must fit the dS^T buffer");
   int gc = 0;  // running chunk counter: parity selects the sL / sD buffer
   for (; z < Z; z += gridDim.x) {
     const int b = z / P.H, h = z % P.H, znext = z + gridDim.x;
-    const int klen = P.key_len ? min(P.key_len[b], P.Tk) : P.Tk;
+    const int klen = key_len_of(P, b);
     __syncthreads();  // the previous head's phase 3 is done with sK
 #pragma unroll
     for (int n = 0; n < NLK; ++n) {
       const int i = tid + n * 512, r = i / CH, c = i % CH;
       if (i < TKP * CH) *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
     }
+    // vf arrived with rk (same load_kv), which the stores above have waited for; re-define vf here
+    // so the compiler's wait tracking, which loses count across the head loop, does not put
+    // vmcnt(1..3) waits (draining the next chunk's prefetch) in front of phase 2's dV MFMAs
+#pragma unroll
+    for (int j = 0; j < NKC; ++j)
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(vf[j][kk]));
     f32x4 dk[NKC][NDT], dv[NKC][NDT];
 #pragma unroll
     for (int j = 0; j < NKC; ++j)
@@ -705,8 +728,12 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
         }
       }
       if (tid < QC) L[tid] = rl * 1.4426950408889634f;   // LSE in log2 units
+      // The prefetch is issued unconditionally (past the last head: an empty row range, so the
+      // loads return zeros without touching memory).  A conditional issue leaves the compiler
+      // unsure how many loads are in flight, and it then waits for all of them (vmcnt(0)) at the
+      // first MFMA of phase 2 -- exposing the next head's load latency on every head's last chunk.
       if (!LAST) load_chunk(z, qbase + QC);
-      else if (znext < Z) load_chunk(znext, 0);
+      else load_chunk(znext < Z ? znext : z, znext < Z ? 0 : Tq);
       __syncthreads();
       if (tid < QC) {
         const float* part = reinterpret_cast<const float*>(sDS) + tid * CH;
@@ -869,7 +896,7 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
           }
         }
         }
-        if (znext < Z) load_kv(znext);
+        load_kv(znext < Z ? znext : z, znext < Z);
       }
       PH_STAMP(4 + 5 * gc);
       __syncthreads();

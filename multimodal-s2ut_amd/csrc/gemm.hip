@@ -720,7 +720,10 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
   // issued after a DMA, which would make every k-step wait for the NEXT stage's DMA to land.  With
   // a transpose-read operand the k-step therefore reads both k-halves' fragments first and issues
   // the next stage's DMA behind them (the DMA then overlaps the MFMAs, as in the K-contiguous form).
-  constexpr bool READ_FIRST = !A_KC || !B_KC;
+#ifndef MMS_GEMM_DMA_AFTER_READS
+#define MMS_GEMM_DMA_AFTER_READS 0
+#endif
+  constexpr bool READ_FIRST = !A_KC || !B_KC || MMS_GEMM_DMA_AFTER_READS;
   // All 16 fragments of the stage are read before its MFMAs (the second k-half's reads no longer
   // wait behind the first half's MFMAs): 0-5 % faster isolated on the step's NT shapes, step flat
   // (profiles/round3_v5_gemm_read_all_ab.txt).
