@@ -1,31 +1,29 @@
 #!/bin/bash
-# Fused attention backward: unconditional next-head prefetch, scalar key lengths, V fragments
-# re-defined after the head-top wait (no compiler vmcnt drains of the register prefetch).
-# Bit-identity vs the previous attention build, attention tests, isolated timings, step A/B.
+# Round-3 v6: GPU tests + smoke + bench at HEAD first, then the attention-prefetch A/B (bit-identity vs
+# the previous attention build, isolated timings, step A/B), kernel trace, PMC traffic, NT
+# DMA-after-reads A/B, gloo DP2 rehearsal.  Each step under its own limit; stop at the first failure.
 export TMPDIR=/tmp
-O=gpurun_out/r3o; mkdir -p $O
-L0=multimodal-s2ut_amd/lib/libmms2ut_hip_attnold.so
-step() { local name=$1 secs=$2; shift 2; echo "=== [$name]"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?
-         echo "=== [$name] rc=$rc"; tail -n 12 "$O/$name.log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
-step dump_new 120 python scripts/attn_bits.py /tmp/new.npz
-step dump_old 120 env MMS2UT_LIB=$L0 python scripts/attn_bits.py /tmp/old.npz
-step cmp 60 python scripts/wgrad_bits.py cmp /tmp/new.npz /tmp/old.npz
-step ktests 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread
-step attn_new 200 python scripts/attn_bench.py
-step attn_old 200 env MMS2UT_LIB=$L0 python scripts/attn_bench.py
-step ab 600 python scripts/lib_ab.py $O/attn_ab.json 2 new= attnold=$L0
-L2=multimodal-s2ut_amd/lib/libmms2ut_hip_dar.so
-step gemm_new 180 python scripts/gemm_bits.py /tmp/g_new.npz
-step gemm_dar 180 env MMS2UT_LIB=$L2 python scripts/gemm_bits.py /tmp/g_dar.npz
-step gcmp 60 python scripts/wgrad_bits.py cmp /tmp/g_new.npz /tmp/g_dar.npz
-step ab2 600 python scripts/lib_ab.py $O/dar_ab.json 2 new= dar=$L2
 O=gpurun_out/ev6; mkdir -p $O
+L0=multimodal-s2ut_amd/lib/libmms2ut_hip_attnold.so
+L2=multimodal-s2ut_amd/lib/libmms2ut_hip_dar.so
+step() { local name=$1 secs=$2; shift 2; echo "=== [$name]"; timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1; local rc=$?
+         echo "=== [$name] rc=$rc"; tail -n 10 "$O/$name.log"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 step tests 480 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 300 python bench.py
+step dump_new 120 python scripts/attn_bits.py /tmp/new.npz
+step dump_old 120 env MMS2UT_LIB=$L0 python scripts/attn_bits.py /tmp/old.npz
+step cmp 60 python scripts/wgrad_bits.py cmp /tmp/new.npz /tmp/old.npz
+step attn_new 200 python scripts/attn_bench.py
+step attn_old 200 env MMS2UT_LIB=$L0 python scripts/attn_bench.py
+step ab 600 python scripts/lib_ab.py $O/attn_ab.json 2 new= attnold=$L0
+step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 6 --warmup 3 --no-cpu-baseline
 B="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-gemm-timing"
 step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python $B
 step pmc_write 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python $B
 step traffic 60 python scripts/pmc_traffic.py $O/pmc_fetch $O/pmc_write --out $O/gemm_traffic.json
-step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python bench.py --steps 6 --warmup 3 --no-cpu-baseline
+step gemm_new 180 python scripts/gemm_bits.py /tmp/g_new.npz
+step gemm_dar 180 env MMS2UT_LIB=$L2 python scripts/gemm_bits.py /tmp/g_dar.npz
+step gcmp 60 python scripts/wgrad_bits.py cmp /tmp/g_new.npz /tmp/g_dar.npz
+step ab2 600 python scripts/lib_ab.py $O/dar_ab.json 2 new= dar=$L2
 step dp2 600 scripts/_dp2_rehearsal.sh $O/dp2
