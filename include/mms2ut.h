@@ -84,6 +84,11 @@ typedef struct mms2ut_gemm_args {
 } mms2ut_gemm_args;
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
+/* NT shapes (both operands K-contiguous, batch 1, no split) may run on the ping-pong 256-column
+ * kernel instead of the 128x128 one (bit-identical results).  mode -1: automatic choice by shape,
+ * 0: never (default; env MMS2UT_GEMM_PP overrides it at first use), 128 / 192 / 256: always, with
+ * that tile height.  Process-global; for A/B measurements and tests.                            */
+int mms2ut_gemm_set_pp(int mode);
 
 /* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the
  * reference layer's projections): for each of the n <= 8 problems, dW[N, K] = dy[rows, N]^T @

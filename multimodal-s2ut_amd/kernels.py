@@ -243,12 +243,16 @@ _STREAM_WS = {}
 
 def stream_workspace(numel, device):
     """fp32 scratch private to the current stream (grow-only; a regrown buffer is released to the
-    caching allocator on the stream that allocated and used it, so later reuse is stream-ordered)."""
+    caching allocator on the stream that allocated and used it, so later reuse is stream-ordered).
+    In graph mode (_Side.retain) a regrown buffer is retired instead: an earlier captured graph
+    still writes its split-K partials into it on every replay."""
     if numel <= 0:
         return None
     key = _s()
     buf = _STREAM_WS.get(key)
     if buf is None or buf.numel() < numel:
+        if buf is not None and _Side.retain:
+            _Side.retired.append(buf)
         buf = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
         _STREAM_WS[key] = buf
     return buf

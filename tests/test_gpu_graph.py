@@ -113,3 +113,22 @@ def test_graph_trainer_bit_identical_to_eager(mod):
         assert n == (2 if mod < 0 else 4), n
     finally:
         mm.kernels.bind_step_seed(None)
+
+
+def test_stream_workspace_retired_in_graph_mode():
+    """A regrown per-stream split-K workspace is retired (kept alive) in graph mode: a graph
+    captured with the smaller buffer keeps writing into it on every replay (kernels.stream_workspace)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    K = pkg().kernels
+    side = K._Side
+    saved = (side.retain, list(side.retired))
+    try:
+        side.retain = True
+        small = K.stream_workspace(1 << 20, "cuda")
+        big = K.stream_workspace(4 << 20, "cuda")
+        assert big.data_ptr() != small.data_ptr() and big.numel() >= 4 << 20
+        assert any(t.data_ptr() == small.data_ptr() for t in side.retired)
+        assert K.stream_workspace(2 << 20, "cuda").data_ptr() == big.data_ptr()   # no regrowth below the size
+    finally:
+        side.retain, side.retired[:] = saved[0], saved[1]

@@ -52,6 +52,23 @@ def test_full_base_vit_dropout_replay(mm):
         assert e < GRAD_TOL, (k, e)
 
 
+def test_full_base_audio_only_dropout_replay(mm):
+    """BASELINE configs[3]: the audio-only xm_transformer path — the base 12+6 model with the
+    fusion tail skipped (mm_s2s_transformer.py:471: no image features reach the encoder), at the
+    bench's lengths, every dropout site replayed."""
+    cfg = R.base_config(fusion=False)
+    lengths = [1000, 900, 800, 700, 640, 560, 520, 500]
+    tlens = [round(0.3 * L) + 1 for L in lengths]
+    r = run_model_pair(mm, cfg, lengths, tlens, with_images=False, seed=23)
+    print(report(r))
+    assert r.Te == 250 and r.n_masks == 1 + 12 * 4 + 6 * 6
+    check_outputs(r)
+    check_relu_replay(r)
+    _assert_grads(r)
+    for k, e in layer_dgrad_errors(r).items():
+        assert e < GRAD_TOL, (k, e)
+
+
 @pytest.mark.parametrize("modality", [None, "audio", "image"])
 def test_full_detr_modality_dropout(mm, modality):
     cfg = R.base_config(image_feat_dim=256, SA_image_dropout=0.5, modality_dropout=0.5, audio_dropout=0.5)
