@@ -89,6 +89,10 @@ int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
  * 0: never (default; env MMS2UT_GEMM_PP overrides it at first use), 128 / 192 / 256: always, with
  * that tile height.  Process-global; for A/B measurements and tests.                            */
 int mms2ut_gemm_set_pp(int mode);
+/* NT shapes of more than one round of 128x128 tiles (> 512) run on a persistent kernel whose blocks
+ * walk several tiles and finish each tile's epilogue inside the next tile's k-loop (bit-identical
+ * results).  mode 1: on, 0: off (default; env MMS2UT_GEMM_DP overrides it at first use).          */
+int mms2ut_gemm_set_dp(int mode);
 
 /* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the
  * reference layer's projections): for each of the n <= 8 problems, dW[N, K] = dy[rows, N]^T @
@@ -534,6 +538,39 @@ int mms2ut_layer_ws(const mms2ut_layer* layer, int64_t* main_floats, int64_t* si
 int mms2ut_layer_fwd(const mms2ut_layer* layer, float* main_ws, int64_t main_ws_floats, hipStream_t stream);
 int mms2ut_layer_bwd(const mms2ut_layer* layer, const mms2ut_layer_grad* grad, hipStream_t main,
                      hipStream_t side);
+
+/* ---------------------------------------------------------------- Conv1d subsampler
+ * fairseq Conv1dSubsampler — SURVEY §8b mms2ut_conv1d_glu_{fwd,bwd} (A3; S2TTransformerEncoder's
+ * front, reached at mm_s2s_transformer.py:464): nlayers x [Conv1d(C_l -> cout_l, k_l, stride 2,
+ * padding k_l / 2) -> GLU over channels], input x [B][T][C] fp16 (row b*T + t), output
+ * [B][T_out][cout_last / 2] at the arena offset conv1d_glu_arena returns.  One call enqueues the
+ * layer sequence (im2col, projection GEMM with bias, GLU); the backward the GLU backward, the
+ * weight / bias gradients on `side` (g_w[l] viewed [cout][C k], NULL = skip) and the input
+ * gradients of layers > 0 (dgrad through wt[l] = W^T image [C k][cout] when non-NULL, col2im).
+ * The first layer's input gradient is not formed (fbank features are not trained).  Buffers as for
+ * the layers: arena (forward -> backward), scratch (keep until the side stream is joined),
+ * per-stream workspaces from conv1d_glu_ws.                                                     */
+#define MMS_CONV_MAX 4
+typedef struct mms2ut_conv1d_glu {
+  int B, T, C, nlayers;
+  int k[MMS_CONV_MAX];            /* kernel sizes                                                */
+  int cout[MMS_CONV_MAX];         /* conv output channels (2 x GLU channels), multiples of 16    */
+  const mms2ut_half* w[MMS_CONV_MAX];    /* [cout][C_l][k] (nn.Conv1d weight)                   */
+  const mms2ut_half* b[MMS_CONV_MAX];
+  const mms2ut_half* wt[MMS_CONV_MAX];   /* W^T images [C_l k][cout] for the dgrads, or NULL     */
+  mms2ut_half* g_w[MMS_CONV_MAX];
+  mms2ut_half* g_b[MMS_CONV_MAX];
+  const mms2ut_half* x;
+  void* saved;
+} mms2ut_conv1d_glu;
+int mms2ut_conv1d_glu_arena(const mms2ut_conv1d_glu* c, int64_t* out_offset, int64_t* bytes);
+/* dx_offset: the gradient of layer 1's input (= layer 0's GLU output) in the scratch, -1 for one layer */
+int mms2ut_conv1d_glu_scratch(const mms2ut_conv1d_glu* c, int64_t* dx_offset, int64_t* bytes);
+int mms2ut_conv1d_glu_ws(const mms2ut_conv1d_glu* c, int64_t* main_floats, int64_t* side_floats);
+int mms2ut_conv1d_glu_fwd(const mms2ut_conv1d_glu* c, float* main_ws, int64_t main_ws_floats, hipStream_t stream);
+int mms2ut_conv1d_glu_bwd(const mms2ut_conv1d_glu* c, const mms2ut_half* dy, void* scratch, float* main_ws,
+                          int64_t main_ws_floats, float* side_ws, int64_t side_ws_floats, int side_blocks,
+                          hipStream_t main, hipStream_t side);
 
 #ifdef __cplusplus
 }

@@ -92,6 +92,15 @@ class LayerArgs(C.Structure):
         [("x", vp), ("saved", vp)]
 
 
+CONV_MAX = 4   # include/mms2ut.h MMS_CONV_MAX
+
+
+class ConvArgs(C.Structure):
+    """mms2ut_conv1d_glu (include/mms2ut.h): the Conv1d subsampler."""
+    _fields_ = [("B", i32), ("T", i32), ("C", i32), ("nlayers", i32), ("k", i32 * CONV_MAX), ("cout", i32 * CONV_MAX)] + \
+        [(n, vp * CONV_MAX) for n in ("w", "b", "wt", "g_w", "g_b")] + [("x", vp), ("saved", vp)]
+
+
 class WgradArgs(C.Structure):
     """mms2ut_wgrad (include/mms2ut.h): one problem of a grouped weight-gradient launch."""
     _fields_ = [("dy", vp), ("lddy", i64), ("x", vp), ("ldx", i64), ("dW", vp), ("db", vp), ("N", i32), ("K", i32)]
@@ -113,6 +122,7 @@ SIGNATURES = {
     "mms2ut_version": (i32, []),
     "mms2ut_gemm_f16": (i32, [vp, vp]),   # GEMM_ARGS.pack(...) bytes or C.byref(GemmArgs)
     "mms2ut_gemm_set_pp": (i32, [i32]),
+    "mms2ut_gemm_set_dp": (i32, [i32]),
     "mms2ut_wgrad_group": (i32, [vp, i32, i64, i32, vp]),
     "mms2ut_profile_begin": (i32, [i32]),
     "mms2ut_profile_end": (i32, [C.POINTER(C.c_float), C.POINTER(C.c_int), C.POINTER(C.c_double)]),
@@ -181,6 +191,11 @@ SIGNATURES = {
     "mms2ut_layer_ws": (i32, [vp, vp, vp]),
     "mms2ut_layer_fwd": (i32, [vp, vp, i64, vp]),
     "mms2ut_layer_bwd": (i32, [vp, vp, vp, vp]),
+    "mms2ut_conv1d_glu_arena": (i32, [vp, vp, vp]),
+    "mms2ut_conv1d_glu_scratch": (i32, [vp, vp, vp]),
+    "mms2ut_conv1d_glu_ws": (i32, [vp, vp, vp]),
+    "mms2ut_conv1d_glu_fwd": (i32, [vp, vp, i64, vp]),
+    "mms2ut_conv1d_glu_bwd": (i32, [vp, vp, vp, vp, i64, vp, i64, i32, vp, vp]),
     "mms2ut_log_softmax_step": (i32, [vp, i64, i64, i32, i32, i32, i32, vp, vp]),
     "mms2ut_kv_cache_gather": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "mms2ut_decode_self_attn": (i32, [vp, i64, vp, vp, i32, i32, i32, i32, vp, vp, i64, i64, vp, i64, f32, vp]),

@@ -163,25 +163,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP P, int tiles_m, int t
 // need no predication; a K-contiguous operand needs K % 64 == 0 (host routing).
 // ------------------------------------------------------------------------------------------
 
-template <bool KC>
-MMS_DEV void dma_tile(__amdgpu_buffer_rsrc_t rs, char* lds, long ld, int row0, int k0rel, int wid, int lane) {
-  // 16 wave-instructions per 16 KiB tile: wave `wid` issues 4 of them
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ins = wid * 4 + i;
-    int voff;
-    if (KC) {
-      const int row = ins * 8 + (lane >> 3), slot = lane & 7;
-      const int c = slot ^ (row & 7);
-      voff = (int)(((long)(row0 + row) * ld + k0rel + c * 8) * 2);
-    } else {
-      const int kr = ins * 4 + (lane >> 4), slot = lane & 15;
-      const int c = slot ^ swz_mn(kr);
-      voff = (int)(((long)(k0rel + kr) * ld + row0 + c * 8) * 2);
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
-  }
-}
 
 
 // One 128x128 output tile of the LDS-DMA pipeline (z = batch * splitk + split).  PRI: raise the
@@ -314,7 +295,15 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
   // the ring is idle once every wave is past its last fragment read (no DMA is in flight: the
   // last k-step waited for vmcnt(0))
   __syncthreads();
+#ifdef MMS_GEMM_NOEPI   // ablation build: no epilogue (accumulators kept live; garbage output)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
+  (void)Cz; (void)auxz;
+#else
   staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+#endif
 }
 
 template <bool A_KC, bool B_KC, int EPI, int STAGES, bool RS = false>
@@ -898,6 +887,22 @@ extern "C" int mms2ut_gemm_set_pp(int mode) {
   return 0;
 }
 
+// Persistent deferred-epilogue kernel (gemm_dp.hip) for NT grids of more than one round of the
+// 512 block slots.  1 on, 0 off (default until it measures faster; mms2ut_gemm_set_dp / MMS2UT_GEMM_DP).
+static int g_dp_mode = -1;
+static int dp_mode() {
+  if (g_dp_mode < 0) {
+    const char* e = getenv("MMS2UT_GEMM_DP");
+    g_dp_mode = e ? atoi(e) : 0;
+  }
+  return g_dp_mode;
+}
+extern "C" int mms2ut_gemm_set_dp(int mode) {
+  MMS_REQUIRE(mode == 0 || mode == 1, "gemm_set_dp: mode must be 0 or 1 (got %d)", mode);
+  g_dp_mode = mode;
+  return 0;
+}
+
 // Tile height of the ping-pong kernel for an NT shape, 0 = use the 128x128 kernel.  One block per
 // CU: a launch of t tiles takes ceil(t / 256) rounds, each as long as one BM x 256 tile, so the
 // height that fills the last round best wins (per-tile cost ~ BM + a fixed 48-row overhead for
@@ -1029,6 +1034,12 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
       P.stamps = stamp_take((long)tmp * tnp);
       return mmsg::launch_pp(a->epi, bm, P, tmp, tnp, s);
     }
+  }
+  if (dma_ok && a_kc && b_kc && nz == 1 && a->epi != MMS_EPI_F32 && P.vec16 && a->N % 4 == 0 &&
+      (long)tm * tn > 512 && dp_mode()) {
+    const int grid = 512;   // two blocks per CU, each walking its XCD's tiles
+    P.stamps = stamp_take(grid);
+    return mmsg::launch_dp(a->epi, P, tm, tn, grid, s);
   }
   if (dma_ok) {
     if (use_256(a, nz)) {

@@ -29,6 +29,8 @@ struct GemmP {
 
 // ping-pong 256-column NT kernel (gemm_pp.hip): tile height bm (128 / 192 / 256) x 256 columns
 int launch_pp(int epi, int bm, const GemmP& P, int tiles_m, int tiles_n, hipStream_t s);
+// persistent 128x128 NT kernel with the deferred epilogue (gemm_dp.hip) on `grid` blocks
+int launch_dp(int epi, const GemmP& P, int tiles_m, int tiles_n, int grid, hipStream_t s);
 }  // namespace mmsg
 
 namespace {
@@ -494,6 +496,30 @@ MMS_DEV h16x8 read_frag32(const char* lds, int sub, int lane) {
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
+
+// one 128-row x 64-k operand stage by LDS-DMA: 16 wave-instructions, wave `wid` issues 4
+template <bool KC>
+MMS_DEV void dma_tile(__amdgpu_buffer_rsrc_t rs, char* lds, long ld, int row0, int k0rel, int wid, int lane) {
+#ifdef MMS_GEMM_NODMA   // ablation build: no operand traffic (garbage output)
+  return;
+#endif
+  // 16 wave-instructions per 16 KiB tile: wave `wid` issues 4 of them
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ins = wid * 4 + i;
+    int voff;
+    if (KC) {
+      const int row = ins * 8 + (lane >> 3), slot = lane & 7;
+      const int c = slot ^ (row & 7);
+      voff = (int)(((long)(row0 + row) * ld + k0rel + c * 8) * 2);
+    } else {
+      const int kr = ins * 4 + (lane >> 4), slot = lane & 15;
+      const int c = slot ^ swz_mn(kr);
+      voff = (int)(((long)(k0rel + kr) * ld + row0 + c * 8) * 2);
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
+  }
+}
 
 template <int N>
 MMS_DEV void wait_vm() {

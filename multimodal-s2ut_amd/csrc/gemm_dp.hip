@@ -1,0 +1,302 @@
+// Persistent 128x128 NT GEMM with a deferred epilogue (gfx950): C[M, N] = epilogue(A[M, K] . B[N, K]^T),
+// both operands K-contiguous — the step's forward projections and (through the W^T images) dgrads.
+//
+// Why: in the one-tile-per-block kernel (gemm.hip gemm_dma_kernel) every tile of a round finishes
+// its k-loop at about the same time, so the whole chip alternates between an MFMA phase (HBM idle)
+// and an epilogue phase (every CU storing C, MFMAs idle).  On the short-K wide shapes (K = 768,
+// N = 2304 / 3072) the epilogue was 35-40 % of the kernel (gemm.hip -DMMS_GEMM_NOEPI ablation,
+// profiles/round4_gemm_ablation.txt).  Here each block (2 per CU, grid <= 512) walks a strided
+// sequence of tiles of its XCD's range and runs tile i's epilogue INSIDE tile i+1's k-loop: two
+// 16x16 accumulator fragments per k-step (math, dropout hash, 8-B stores), their aux / residual
+// operands loaded one k-step ahead so the k-step's vmcnt(0) (which the 2-stage LDS-DMA ring takes
+// anyway) has already retired them.  The last k-step of a tile DMAs the next tile's first stage,
+// so the tile prologue's load latency is hidden as well.
+//
+// The k-loop is gemm_dma_kernel's (128x128x64 tiles, 4 waves of 64x64, 2-stage LDS-DMA ring,
+// XOR-swizzled images, mfma_f32_16x16x32_f16 with (B, A) swapped) and the epilogue arithmetic is
+// staged_epilogue's element for element, so results are bit-identical to gemm_dma_kernel
+// (tests/test_gpu_gemm_splitk.py::test_dp_gemm_bit_identical).
+#include <utility>
+
+#include "gemm_common.h"
+
+namespace {
+
+constexpr int DP_PIECES = 2;   // accumulator fragments of the previous tile finished per k-step
+
+template <int EPI>
+constexpr bool dp_aux() {
+  return EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_GATE || EPI == MMS_EPI_RELU_DROP_BWD ||
+         EPI == MMS_EPI_F16_ACC || EPI == MMS_EPI_GELU_DROP_BWD;
+}
+
+// the deferred epilogue operands of one fragment: lane's 4 columns of row m
+struct DpAux {
+  h16x4 a, b, bias;
+};
+
+MMS_DEV h16x4 ld8b(const h16* p) { return *reinterpret_cast<const h16x4*>(p); }
+
+// fragment (i, j) of a wave's 64x64 accumulator tile: lane owns row (i*16 + (lane & 15)),
+// columns j*16 + 4*(lane >> 4) .. +3 (the (B, A)-swapped MFMA layout)
+template <int EPI>
+MMS_DEV DpAux dp_load(const GemmP& P, int m, int n) {
+  DpAux x;
+  x.a = h16x4{(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+  x.b = x.a;
+  x.bias = x.a;
+  if (m >= P.M || n >= P.N) return x;
+  if (EPI != MMS_EPI_RELU_DROP_BWD && EPI != MMS_EPI_GELU_DROP_BWD && P.bias) x.bias = ld8b(P.bias + n);
+  if (!dp_aux<EPI>()) return x;
+  if (EPI == MMS_EPI_F16_ACC) {
+    x.a = ld8b(reinterpret_cast<const h16*>(P.C) + (long)m * P.ldc + n);
+  } else {
+    x.a = ld8b(P.aux + (long)m * P.ldaux + n);
+    if (EPI == MMS_EPI_GATE) x.b = ld8b(P.aux + (long)m * P.ldaux + P.N + n);
+  }
+  return x;
+}
+
+// staged_epilogue's per-element arithmetic (fast path) on 4 consecutive columns
+template <int EPI>
+MMS_DEV void dp_store(const GemmP& P, int m, int n, const f32x4& v, const DpAux& ax, uint32_t hmix,
+                      bool same_hi, float dscale) {
+  if (m >= P.M || n >= P.N) return;
+  float bv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bv[e] = (float)ax.bias[e];
+  float x[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x[e] = v[e] * P.alpha + bv[e];
+  bool keep[4] = {true, true, true, true};
+  if (epi_drops<EPI>() && P.thresh) {
+    const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
+    if (same_hi) mms_keep4_hi(hmix, c0, P.thresh, keep);
+    else mms_keep4(P.seed, c0, P.thresh, keep);
+  }
+  h16x4 o4;
+  h16* C = reinterpret_cast<h16*>(P.C) + (long)m * P.ldc + n;
+  if (EPI == MMS_EPI_GATE) {
+    h16x4 g4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float g = sigmoidf_(x[e]), ov = (float)ax.a[e], tv = (float)ax.b[e];
+      g4[e] = (h16)g;
+      o4[e] = (h16)(tv + g * (ov - tv));
+    }
+    *reinterpret_cast<h16x4*>(P.out2 + (long)m * P.ldo2 + n) = g4;
+  } else if (EPI == MMS_EPI_GELU_DROP) {
+    h16x4 z4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      z4[e] = (h16)x[e];
+      o4[e] = (h16)(keep[e] ? gelu_((float)z4[e]) * dscale : 0.f);
+    }
+    *reinterpret_cast<h16x4*>(P.out2 + (long)m * P.ldo2 + n) = z4;
+  } else if (EPI == MMS_EPI_GELU_DROP_BWD) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o4[e] = (h16)(keep[e] ? x[e] * dscale * gelu_grad_((float)ax.a[e]) : 0.f);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float o;
+      if (EPI == MMS_EPI_RELU_DROP) o = keep[e] ? fmaxf(x[e], 0.f) * dscale : 0.f;
+      else if (EPI == MMS_EPI_DROP_RESID) o = (float)ax.a[e] + (keep[e] ? x[e] * dscale : 0.f);
+      else if (EPI == MMS_EPI_RELU_DROP_BWD) o = (float)ax.a[e] > 0.f ? x[e] * dscale : 0.f;
+      else if (EPI == MMS_EPI_F16_ACC) o = (float)ax.a[e] + x[e];
+      else o = x[e];
+      o4[e] = (h16)o;
+    }
+  }
+  *reinterpret_cast<h16x4*>(C) = o4;
+}
+
+// XCD-local tile walk: the XCD's contiguous share of the tile space (tile_coords' bijective split),
+// block j of the XCD takes local tiles j, j + gx, j + 2 gx, ...; local ids follow tile_coords'
+// grouped order (GROUP_M tile-rows, column by column)
+MMS_DEV bool dp_tile(int seq, int tiles_m, int tiles_n, int total, int group_m, int& tm, int& tn) {
+  const int x = blockIdx.x % 8, j = blockIdx.x / 8, gx = gridDim.x / 8;
+  const int q = total / 8, r = total % 8;
+  const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  const int len = q + (x < r ? 1 : 0);
+  const int loc = j + seq * gx;
+  if (loc >= len) return false;
+  const int t = start + loc;
+  const int per_group = group_m * tiles_n;
+  const int g = t / per_group, first_m = g * group_m;
+  const int gsize = min(tiles_m - first_m, group_m);
+  const int w = t % per_group;
+  tm = first_m + w % gsize;
+  tn = w / gsize;
+  (void)tiles_m;
+  return true;
+}
+
+// k-steps 0 .. NP-1 with compile-time step numbers (they carry the deferred fragments)
+template <int U, int NP, typename F>
+MMS_DEV void unroll_ksteps(int nk, F& f) {
+  if constexpr (U < NP) {
+    if (U < nk) f(U, std::integral_constant<int, U>{});
+    unroll_ksteps<U + 1, NP>(nk, f);
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
+#define SA(s) (smem + (2 * (s)) * TILE_BYTES)
+#define SB(s) (smem + (2 * (s) + 1) * TILE_BYTES)
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)P.A, (short)0, (int)(((long)(P.M - 1) * P.lda + P.K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)P.B, (short)0, (int)(((long)(P.N - 1) * P.ldb + P.K) * 2), 0x00020000);
+  const int nk = P.K / BK;   // host: K % 64 == 0, K > 0
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+
+  int tm, tn;
+  if (!dp_tile(0, tiles_m, tiles_n, total, P.group_m, tm, tn)) {
+    stamp_end(P.stamps, t_start);
+    return;
+  }
+  dma_tile<true>(ra, SA(0), P.lda, tm * BM, 0, wid, lane);
+  dma_tile<true>(rb, SB(0), P.ldb, tn * BN, 0, wid, lane);
+
+  // the previous tile's accumulators and its epilogue state
+  f32x4 prev[4][4];
+  int pm0 = 0, pn0 = 0;   // lane's first row / column of the previous tile
+  bool have_prev = false;
+  uint32_t hmix = 0;
+  bool same_hi = false;
+  // operands of the fragments finished in k-step e live in pa[e & 1]: the next k-step's are loaded
+  // while this one's are consumed
+  DpAux pa[2][DP_PIECES];
+  // fragment p = 4 i + j of the previous tile (p compile-time after unrolling)
+  auto load_pieces = [&](int p0) {
+    DpAux* dst = pa[(p0 / DP_PIECES) & 1];
+#pragma unroll
+    for (int u = 0; u < DP_PIECES; ++u)
+      if (p0 + u < 16) dst[u] = dp_load<EPI>(P, pm0 + ((p0 + u) >> 2) * 16, pn0 + ((p0 + u) & 3) * 16);
+  };
+  auto store_pieces = [&](int p0) {
+    const DpAux* src = pa[(p0 / DP_PIECES) & 1];
+#pragma unroll
+    for (int u = 0; u < DP_PIECES; ++u) {
+      const int p = p0 + u;
+      if (p < 16)
+        dp_store<EPI>(P, pm0 + (p >> 2) * 16, pn0 + (p & 3) * 16, prev[p >> 2][p & 3], src[u], hmix, same_hi, dscale);
+    }
+  };
+
+  int kbase = 0;   // k-steps run so far: the ring parity carries over from tile to tile
+  for (int seq = 0;; ++seq) {
+    const int bm = tm * BM, bn = tn * BN;
+    int ntm = 0, ntn = 0;
+    const bool more = dp_tile(seq + 1, tiles_m, tiles_n, total, P.group_m, ntm, ntn);
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (have_prev) load_pieces(0);
+    // one k-step; EP >= 0: also finish the previous tile's fragments EP*DP_PIECES.. (EP compile-time)
+    auto kstep = [&](int kt, auto ep) {
+      constexpr int EP = decltype(ep)::value;
+      // stage kt (and every aux load / store issued in the previous k-step) has landed.  The
+      // builtin form of the wait (not inline asm) tells the compiler's waitcnt pass that those
+      // loads are retired, so it adds no wait of its own in front of their use below, behind the
+      // next stage's DMA
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int cur = (kbase + kt) & 1;
+      if (kt + 1 < nk) {
+        dma_tile<true>(ra, SA(cur ^ 1), P.lda, bm, (kt + 1) * BK, wid, lane);
+        dma_tile<true>(rb, SB(cur ^ 1), P.ldb, bn, (kt + 1) * BK, wid, lane);
+      } else if (more) {   // the next tile's first stage, behind this tile's last k-step
+        dma_tile<true>(ra, SA(cur ^ 1), P.lda, ntm * BM, 0, wid, lane);
+        dma_tile<true>(rb, SB(cur ^ 1), P.ldb, ntn * BN, 0, wid, lane);
+      }
+      if (EP >= 0 && have_prev && (EP + 1) * DP_PIECES < 16 && kt + 1 < nk) load_pieces((EP + 1) * DP_PIECES);
+      h16x8 fa2[2][4], fb2[2][4];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa2[kk][i] = read_frag<true>(SA(cur), wm * 64 + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<true>(SB(cur), wn * 64 + j * 16, kk, lane);
+      }
+      if (EP >= 0 && have_prev) store_pieces(EP * DP_PIECES);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb2[kk][j], fa2[kk][i], acc[i][j], 0, 0, 0);
+    };
+    constexpr int NP = 16 / DP_PIECES;   // k-steps that carry deferred fragments
+    unroll_ksteps<0, NP>(nk, kstep);
+    for (int kt = NP; kt < nk; ++kt) kstep(kt, std::integral_constant<int, -1>{});
+    // a tile shorter than NP k-steps: finish the previous tile's remaining fragments now
+    if (have_prev && nk < NP) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+      for (int p0 = 0; p0 < 16; p0 += DP_PIECES) {
+        if (p0 < DP_PIECES * nk) continue;
+        load_pieces(p0);
+        store_pieces(p0);
+      }
+    }
+    kbase += nk;
+    // this tile becomes the deferred one
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) prev[i][j] = acc[i][j];
+    pm0 = bm + wm * 64 + (lane & 15);
+    pn0 = bn + wn * 64 + 4 * (lane >> 4);
+    have_prev = true;
+    if (epi_drops<EPI>() && P.thresh) {
+      // one hash half per lane and tile when every counter of the lane's fragments shares the
+      // high word (staged_epilogue's fast path; bit-identical to mms_keep4)
+      const uint64_t cf = P.offset + (uint64_t)pm0 * P.ld_rng + pn0;
+      const uint64_t cl = P.offset + (uint64_t)(pm0 + 48) * P.ld_rng + pn0 + 48 + 3;
+      same_hi = mms_same_hi(cf, cl) && ((cf & 1) == 0) && ((P.ld_rng & 1) == 0);
+      hmix = mms_hi_mix(P.seed, cf);
+    }
+    if (!more) break;
+    tm = ntm;
+    tn = ntn;
+  }
+  // the last tile's epilogue
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+  for (int p0 = 0; p0 < 16; p0 += DP_PIECES) {
+    load_pieces(p0);
+    store_pieces(p0);
+  }
+#undef SA
+#undef SB
+  stamp_end(P.stamps, t_start);
+}
+
+}  // namespace
+
+namespace mmsg {
+int launch_dp(int epi, const GemmP& P, int tiles_m, int tiles_n, int grid, hipStream_t s) {
+  const int total = tiles_m * tiles_n;
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dp_kernel<E>), dim3(grid), dim3(NT), 0, s, P, tiles_m, tiles_n, total); break;
+    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_GATE)
+    CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
+#undef CASE
+    default: mms::set_error("gemm_dp: bad epilogue %d", epi); return 1;
+  }
+  return mms::check_launch("gemm_dp");
+}
+}  // namespace mmsg

@@ -12,14 +12,15 @@
 // barrier one group starts its MFMA block while the other starts reading its next slot's fragments
 // and issuing DMA: on each SIMD (waves w and w + 4) one wave feeds the matrix core while the other
 // waits on LDS / memory.  Per slot s, barrier-delimited segments:
-//     group 0:  [read s, issue A(s+L)]  |  [MFMA s, wait A(s+1)]           |
-//     group 1:                          |  [read s, issue B(s+L), wait B(s+1)]  |  [MFMA s]
+//     group 0:  [read s]  |  [MFMA s, issue A(s+L), wait A(s+1)]        |
+//     group 1:            |  [read s, issue B(s+L), wait B(s+1)]  |  [MFMA s]
 // Group 0 DMAs every slot's A image (BM/16 wave-instructions over its 4 waves), group 1 its B image
 // (16).  Each wave waits only for its own DMA with a counted vmcnt (L - 1 later slots stay in
-// flight) before the barrier that precedes the first read of that slot (RAW).  Slot u + L goes
-// into the ring position of slot u + L - R, whose last reads (group 1, two segments earlier) were
-// retired by that group's lgkmcnt wait before the barrier the issuing wave has passed (WAR):
-// L = R - 2.
+// flight) before the barrier that precedes the first read of that slot (RAW).  Slot s + L goes
+// into the ring position of slot s - 1 (L = R - 1), whose reads both groups retired (lgkmcnt)
+// before the barrier the issuing wave passed last (WAR): group 1's read of slot s - 1 ended one
+// segment before group 0's MFMA segment of slot s, group 0's one segment before group 1's read
+// segment of slot s.
 //
 // Accumulation order per output element is the 128x128 kernel's (32-deep k-chunks ascending, the
 // same MFMA with the same operands), and the epilogue is its staged_epilogue: results are
@@ -38,7 +39,7 @@ struct PPGeo {
   static constexpr int SLOT = A_BYTES + B_BYTES;
   static constexpr int R0 = (160 * 1024) / SLOT;
   static constexpr int R = R0 > 6 ? 6 : R0;           // ring slots (256: 5 x 32 KiB, 192: 5 x 28, 128: 6 x 24)
-  static constexpr int L = R - 2;                     // slots in flight ahead of the one being read
+  static constexpr int L = R - 1;                     // slots issued ahead of the one being read
   static constexpr int NI_A = BM / 64;                // A wave-instructions per group-0 wave per slot
   static constexpr int NI_B = 4;                      // B: 16 per slot over the 4 group-1 waves
   static_assert(R * SLOT >= 8 * 64 * 64 * 4, "the staged epilogue needs 16 KiB per wave");
@@ -77,6 +78,10 @@ MMS_DEV void wait_parts(int c) {
 // one 16-row x 32-k wave-instruction of a slot image: lane l fills row (l >> 2), 16-B chunk l & 3,
 // with the global chunk (l & 3) ^ swz32(row) (read_frag32's swizzle)
 MMS_DEV void pp_dma(__amdgpu_buffer_rsrc_t rs, char* img, long ld, int row0, int k0, int ins, int lane) {
+#ifdef MMS_PP_L2HOT   // ablation build: every block streams the same 64 KiB (L2-resident; garbage results)
+  row0 = 0;
+  k0 &= 127;
+#endif
   const int row = ins * 16 + (lane >> 2);
   const int c = (lane & 3) ^ swz32(row);
   const int voff = (int)(((long)(row0 + row) * ld + k0 + c * 8) * 2);
@@ -158,7 +163,7 @@ __global__ void __launch_bounds__(PP_NT, 2) gemm_pp_kernel(GemmP P, int tiles_m,
 #pragma unroll
     for (int i = 0; i < G::FA; ++i) fa[i] = read_frag32<true>(slot, arow + i * 16, lane);
 #endif
-    if (s + G::L < nk) issue(s + G::L);
+    if (g1 && s + G::L < nk) issue(s + G::L);
 #ifdef MMS_PP_NOSTAGGER
     if (s + 1 < nk) wait_slot(s + 1, s + G::L);
 #else
@@ -167,7 +172,7 @@ __global__ void __launch_bounds__(PP_NT, 2) gemm_pp_kernel(GemmP P, int tiles_m,
     PP_T(0);
     pp_barrier();
     PP_T(1);
-#ifndef MMS_PP_NOPRIO
+#ifdef MMS_PP_PRIO
     __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
@@ -180,9 +185,10 @@ __global__ void __launch_bounds__(PP_NT, 2) gemm_pp_kernel(GemmP P, int tiles_m,
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
 #endif
       }
-#ifndef MMS_PP_NOPRIO
+#ifdef MMS_PP_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
+    if (!g1 && s + G::L < nk) issue(s + G::L);
 #ifndef MMS_PP_NOSTAGGER
     if (!g1 && s + 1 < nk) wait_slot(s + 1, s + G::L);
 #endif

@@ -462,3 +462,203 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
   if ((rc = fork(c))) return rc;
   return mms2ut_wgrad_group(group, ngroup, R, side == main ? 0 : G->side_blocks, side);
 }
+
+// ---------------------------------------------------------------- Conv1d subsampler (one call)
+// fairseq Conv1dSubsampler (S2TTransformerEncoder's front, reached at mm_s2s_transformer.py:464):
+// nlayers x [Conv1d(C_l -> cout_l, k_l, stride 2, padding k_l / 2) -> GLU(dim = channels)], as
+// implicit GEMMs: im2col (K = C_l k_l, padded to whole 64-wide k-tiles with zero columns and a
+// zero-padded copy of the weight when C_l k_l % 64 != 0), the projection GEMM with its bias, the
+// GLU.  The same kernels / arguments / stream order as the per-launch path (model.subsample_*_ref),
+// so results are bit-identical to it (tests/test_gpu_layers.py).
+namespace {
+
+struct ConvDims {
+  int n;
+  int64_t Tin[MMS_CONV_MAX], Tout[MMS_CONV_MAX], C[MMS_CONV_MAX], ck[MMS_CONV_MAX], kp[MMS_CONV_MAX];
+  int64_t rows[MMS_CONV_MAX];
+};
+
+ConvDims conv_dims(const mms2ut_conv1d_glu* c) {
+  ConvDims D{};
+  D.n = c->nlayers;
+  int64_t T = c->T, C = c->C;
+  for (int i = 0; i < D.n; ++i) {
+    D.Tin[i] = T;
+    D.Tout[i] = (T - 1) / 2 + 1;
+    D.C[i] = C;
+    D.ck[i] = C * c->k[i];
+    D.kp[i] = D.ck[i] % 64 ? (D.ck[i] + 63) / 64 * 64 : D.ck[i];
+    D.rows[i] = (int64_t)c->B * D.Tout[i];
+    T = D.Tout[i];
+    C = c->cout[i] / 2;
+  }
+  return D;
+}
+
+// arena: per layer col, y (pre-GLU), g (GLU output = the next layer's input / the result), Wp
+enum { CA_COL = 0, CA_Y, CA_G, CA_WP, CA_N };
+void conv_arena_sizes(const mms2ut_conv1d_glu* c, const ConvDims& D, int64_t* sz) {
+  for (int i = 0; i < MMS_CONV_MAX * CA_N; ++i) sz[i] = 0;
+  for (int i = 0; i < D.n; ++i) {
+    sz[i * CA_N + CA_COL] = D.rows[i] * D.kp[i] * 2;
+    sz[i * CA_N + CA_Y] = D.rows[i] * c->cout[i] * 2;
+    sz[i * CA_N + CA_G] = D.rows[i] * (c->cout[i] / 2) * 2;
+    sz[i * CA_N + CA_WP] = D.kp[i] != D.ck[i] ? (int64_t)c->cout[i] * D.kp[i] * 2 : 0;
+  }
+}
+// scratch: per layer dy (pre-GLU gradient), dcol, dx (the layer input's gradient; layers > 0), and
+// the colsum partials of the bias-gradient fallback
+enum { CS_DY = 0, CS_DCOL, CS_DX, CS_N };
+void conv_scratch_sizes(const mms2ut_conv1d_glu* c, const ConvDims& D, int64_t* sz) {
+  for (int i = 0; i < MMS_CONV_MAX * CS_N + 1; ++i) sz[i] = 0;
+  int64_t maxc = 0;
+  for (int i = 0; i < D.n; ++i) {
+    sz[i * CS_N + CS_DY] = D.rows[i] * c->cout[i] * 2;
+    if (i > 0) {
+      sz[i * CS_N + CS_DCOL] = D.rows[i] * D.ck[i] * 2;
+      sz[i * CS_N + CS_DX] = (int64_t)c->B * D.Tin[i] * D.C[i] * 2;
+    }
+    maxc = std::max<int64_t>(maxc, c->cout[i]);
+  }
+  sz[MMS_CONV_MAX * CS_N] = (int64_t)mms2ut_colsum_nparts(D.rows[0]) * maxc * 4;
+}
+
+bool conv_group_ok(const mms2ut_conv1d_glu* c, const ConvDims& D, int i) {
+  // kernels.linear_wgrad: >= 256 output tiles and the grouped kernel's shape rules -> unsplit grouped
+  const int64_t N = c->cout[i], Kk = D.ck[i];
+  return ((N + 127) / 128) * ((Kk + 127) / 128) >= 256 && N % 8 == 0 && Kk % 8 == 0 && D.kp[i] % 8 == 0 &&
+         D.rows[i] * std::max<int64_t>(N, D.kp[i]) * 2 < (1LL << 31);
+}
+
+int conv_check(const mms2ut_conv1d_glu* c) {
+  MMS_REQUIRE(c && c->nlayers >= 1 && c->nlayers <= MMS_CONV_MAX, "conv1d_glu: 1..%d layers", MMS_CONV_MAX);
+  MMS_REQUIRE(c->B >= 0 && c->T >= 1 && c->C >= 1, "conv1d_glu: B=%d T=%d C=%d", c->B, c->T, c->C);
+  for (int i = 0; i < c->nlayers; ++i)
+    MMS_REQUIRE(c->k[i] >= 1 && c->cout[i] > 0 && c->cout[i] % 16 == 0 && c->w[i] && c->b[i],
+                "conv1d_glu: layer %d: k=%d cout=%d (multiple of 16), weight and bias required", i, c->k[i], c->cout[i]);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int mms2ut_conv1d_glu_arena(const mms2ut_conv1d_glu* c, int64_t* out_offset, int64_t* bytes) {
+  if (int rc = conv_check(c)) return rc;
+  MMS_REQUIRE(bytes, "conv1d_glu_arena: null");
+  const ConvDims D = conv_dims(c);
+  int64_t sz[MMS_CONV_MAX * CA_N], off[MMS_CONV_MAX * CA_N];
+  conv_arena_sizes(c, D, sz);
+  *bytes = layout(sz, MMS_CONV_MAX * CA_N, off);
+  if (out_offset) *out_offset = off[(D.n - 1) * CA_N + CA_G];
+  return 0;
+}
+
+extern "C" int mms2ut_conv1d_glu_scratch(const mms2ut_conv1d_glu* c, int64_t* dx_offset, int64_t* bytes) {
+  if (int rc = conv_check(c)) return rc;
+  MMS_REQUIRE(bytes, "conv1d_glu_scratch: null");
+  const ConvDims D = conv_dims(c);
+  int64_t sz[MMS_CONV_MAX * CS_N + 1], off[MMS_CONV_MAX * CS_N + 1];
+  conv_scratch_sizes(c, D, sz);
+  *bytes = layout(sz, MMS_CONV_MAX * CS_N + 1, off);
+  if (dx_offset) *dx_offset = D.n > 1 ? off[1 * CS_N + CS_DX] : -1;   // gradient of layer 1's input
+  return 0;
+}
+
+extern "C" int mms2ut_conv1d_glu_ws(const mms2ut_conv1d_glu* c, int64_t* main_floats, int64_t* side_floats) {
+  if (int rc = conv_check(c)) return rc;
+  MMS_REQUIRE(main_floats && side_floats, "conv1d_glu_ws: null");
+  const ConvDims D = conv_dims(c);
+  int64_t mw = 0, sw = 0;
+  for (int i = 0; i < D.n; ++i) {
+    const int64_t N = c->cout[i];
+    int s = fixup_splits(D.rows[i], N, D.kp[i]);
+    if (s > 1) mw = std::max(mw, (int64_t)s * D.rows[i] * N);
+    if (i > 0 && (s = fixup_splits(D.rows[i], D.ck[i], N)) > 1) mw = std::max(mw, (int64_t)s * D.rows[i] * D.ck[i]);
+    if (!conv_group_ok(c, D, i)) {
+      s = wgrad_splits(((N + 127) / 128) * ((D.ck[i] + 127) / 128), D.rows[i]);
+      sw = std::max(sw, (int64_t)s * N * D.ck[i] + (int64_t)s * N);
+    }
+  }
+  *main_floats = mw;
+  *side_floats = sw;
+  return 0;
+}
+
+extern "C" int mms2ut_conv1d_glu_fwd(const mms2ut_conv1d_glu* c, float* main_ws, int64_t main_ws_floats,
+                                     hipStream_t s) {
+  if (int rc = conv_check(c)) return rc;
+  MMS_REQUIRE(c->x && c->saved, "conv1d_glu_fwd: null input / arena");
+  const ConvDims D = conv_dims(c);
+  int64_t sz[MMS_CONV_MAX * CA_N], off[MMS_CONV_MAX * CA_N];
+  conv_arena_sizes(c, D, sz);
+  layout(sz, MMS_CONV_MAX * CA_N, off);
+  void* A = c->saved;
+  const Ctx cx{s, s, main_ws, main_ws_floats, nullptr, 0, nullptr};
+  const mms2ut_half* x = c->x;
+  int rc;
+  for (int i = 0; i < D.n; ++i) {
+    const int k = c->k[i], N = c->cout[i];
+    mms2ut_half* col = at<mms2ut_half>(A, off, i * CA_N + CA_COL);
+    mms2ut_half* y = at<mms2ut_half>(A, off, i * CA_N + CA_Y);
+    mms2ut_half* g = at<mms2ut_half>(A, off, i * CA_N + CA_G);
+    if ((rc = mms2ut_im2col_ld(x, col, c->B, (int)D.Tin[i], (int)D.Tout[i], (int)D.C[i], k, 2, k / 2, (int)D.kp[i], s)))
+      return rc;
+    const mms2ut_half* W = c->w[i];
+    if (D.kp[i] != D.ck[i]) {   // the weight, zero-padded to the padded K
+      mms2ut_half* Wp = at<mms2ut_half>(A, off, i * CA_N + CA_WP);
+      if (hipMemsetAsync(Wp, 0, (size_t)N * D.kp[i] * 2, s) != hipSuccess) {
+        mms::set_error("conv1d_glu_fwd: hipMemsetAsync failed");
+        return 1;
+      }
+      if ((rc = mms2ut_copy2d(W, D.ck[i], Wp, D.kp[i], N, (int)D.ck[i], s))) return rc;
+      W = Wp;
+    }
+    if ((rc = linear(cx, col, W, c->b[i], y, D.rows[i], N, D.kp[i]))) return rc;
+    if ((rc = mms2ut_glu_fwd(y, g, D.rows[i], N / 2, s))) return rc;
+    x = g;
+  }
+  return 0;
+}
+
+extern "C" int mms2ut_conv1d_glu_bwd(const mms2ut_conv1d_glu* c, const mms2ut_half* dy, void* scratch,
+                                     float* main_ws, int64_t main_ws_floats, float* side_ws,
+                                     int64_t side_ws_floats, int side_blocks, hipStream_t main, hipStream_t side) {
+  if (int rc = conv_check(c)) return rc;
+  MMS_REQUIRE(dy && scratch && c->saved, "conv1d_glu_bwd: null gradient / scratch / arena");
+  if (!side) side = main;
+  const ConvDims D = conv_dims(c);
+  int64_t sz[MMS_CONV_MAX * CA_N], off[MMS_CONV_MAX * CA_N];
+  conv_arena_sizes(c, D, sz);
+  layout(sz, MMS_CONV_MAX * CA_N, off);
+  int64_t ssz[MMS_CONV_MAX * CS_N + 1], so[MMS_CONV_MAX * CS_N + 1];
+  conv_scratch_sizes(c, D, ssz);
+  layout(ssz, MMS_CONV_MAX * CS_N + 1, so);
+  void* A = c->saved;
+  void* S = scratch;
+  const Ctx cx{main, side, main_ws, main_ws_floats, side_ws, side_ws_floats, at<float>(S, so, MMS_CONV_MAX * CS_N),
+               nullptr, nullptr, false};
+  const mms2ut_half* dg = dy;   // gradient of layer i's GLU output
+  int rc;
+  for (int i = D.n - 1; i >= 0; --i) {
+    const int k = c->k[i], N = c->cout[i];
+    const mms2ut_half* col = at<mms2ut_half>(A, off, i * CA_N + CA_COL);
+    mms2ut_half* dyi = at<mms2ut_half>(S, so, i * CS_N + CS_DY);
+    if ((rc = mms2ut_glu_bwd(at<mms2ut_half>(A, off, i * CA_N + CA_Y), dg, dyi, D.rows[i], N / 2, main))) return rc;
+    // dW [N, C k] (the weight's [out][C][k] layout) and db: on the side stream
+    if (c->g_w[i]) {
+      if (conv_group_ok(c, D, i)) {
+        if ((rc = fork(cx))) return rc;
+        mms2ut_wgrad w{dyi, N, col, D.kp[i], c->g_w[i], c->g_b[i], N, (int)D.ck[i]};
+        if ((rc = mms2ut_wgrad_group(&w, 1, D.rows[i], side == main ? 0 : side_blocks, side))) return rc;
+      } else if ((rc = wgrad(cx, dyi, N, col, D.kp[i], c->g_w[i], c->g_b[i], D.rows[i], N, D.ck[i]))) {
+        return rc;
+      }
+    }
+    if (i == 0) break;
+    mms2ut_half* dcol = at<mms2ut_half>(S, so, i * CS_N + CS_DCOL);
+    mms2ut_half* dx = at<mms2ut_half>(S, so, i * CS_N + CS_DX);
+    if ((rc = dgrad(cx, dyi, N, c->w[i], c->wt[i], dcol, D.rows[i], N, D.ck[i]))) return rc;
+    if ((rc = mms2ut_col2im(dcol, dx, c->B, (int)D.Tin[i], (int)D.Tout[i], (int)D.C[i], k, 2, k / 2, main))) return rc;
+    dg = dx;
+  }
+  return 0;
+}

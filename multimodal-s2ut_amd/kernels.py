@@ -372,6 +372,91 @@ class LayerCall:
         return dx, dxd
 
 
+class ConvCall:
+    """The Conv1d subsampler enqueued by one library call each way (include/mms2ut.h
+    mms2ut_conv1d_glu_fwd / _bwd: im2col, projection GEMM, GLU per layer from C++, the weight
+    gradients on the side stream).  Weight / gradient / W^T pointers are bound once; each forward
+    sets the batch shape and the arena and snapshots the argument block for its backward."""
+
+    _sizes = {}
+
+    def __init__(self, ks, couts, weights, biases, gweights, gbiases, dgrad_weights):
+        a = _lib.ConvArgs()
+        a.nlayers = len(ks)
+        for i, k in enumerate(ks):
+            a.k[i], a.cout[i] = k, couts[i]
+            a.w[i], a.b[i] = weights[i].data_ptr(), biases[i].data_ptr()
+            a.g_w[i], a.g_b[i] = gweights[i].data_ptr(), gbiases[i].data_ptr()
+        self.a = a
+        self.dgrad_weights = dgrad_weights     # {layer: W viewed [cout, C k]} for layers >= 1
+        self.wt_of = None
+
+    def _bind_wt(self):
+        wt = TransposedWeights.active
+        if wt is self.wt_of:
+            return
+        for i, W in self.dgrad_weights.items():
+            img = wt.get(W, wait=False) if wt is not None else None
+            self.a.wt[i] = 0 if img is None else img.data_ptr()
+        self.wt_of = wt
+
+    def sizes(self):
+        a = self.a
+        key = (a.B, a.T, a.C, a.nlayers, tuple(a.k), tuple(a.cout))
+        s = ConvCall._sizes.get(key)
+        if s is None:
+            out_off, nb, sb, dxo = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            mw, sw = ctypes.c_int64(), ctypes.c_int64()
+            call("mms2ut_conv1d_glu_arena", ctypes.byref(a), ctypes.byref(out_off), ctypes.byref(nb))
+            call("mms2ut_conv1d_glu_scratch", ctypes.byref(a), ctypes.byref(dxo), ctypes.byref(sb))
+            call("mms2ut_conv1d_glu_ws", ctypes.byref(a), ctypes.byref(mw), ctypes.byref(sw))
+            s = (nb.value, out_off.value, sb.value, mw.value, sw.value)
+            ConvCall._sizes[key] = s
+        return s
+
+    def fwd(self, x, B, T, C):
+        """x [B*T, C] fp16 -> (arena, output [B*T_out, cout_last / 2] view, argument snapshot)."""
+        a = self.a
+        a.B, a.T, a.C = B, T, C
+        a.x = x.data_ptr()
+        self._bind_wt()
+        nb, out_off, _, mw, _ = self.sizes()
+        arena = torch.empty(nb, dtype=torch.uint8, device=x.device)
+        a.saved = arena.data_ptr()
+        ws = stream_workspace(mw, x.device)
+        call("mms2ut_conv1d_glu_fwd", ctypes.byref(a), None if ws is None else ws.data_ptr(), mw, _s())
+        Tout = T
+        for i in range(a.nlayers):
+            Tout = (Tout - 1) // 2 + 1
+        Cg = a.cout[a.nlayers - 1] // 2
+        out = arena[out_off:out_off + 2 * B * Tout * Cg].view(F16).view(B * Tout, Cg)
+        return arena, out, bytes(a)
+
+    def bwd(self, snap, arena, dy):
+        """Backward of the forward whose argument snapshot is ``snap`` (weight / bias gradients)."""
+        nb, _, sbytes, mw, sw = self.sizes()
+        dev = dy.device
+        scratch = torch.empty(sbytes, dtype=torch.uint8, device=dev)
+        if TransposedWeights.active is not None:
+            TransposedWeights.active.wait_ready()
+        main_ws = stream_workspace(mw, dev)
+        side = 0
+        if _Side.enabled:
+            side_stream(dev)
+            side = _Side.ptr
+            with _SIDE_REGION:
+                side_ws = _workspace("slab", sw, dev) if sw > 0 else None
+        else:
+            side_ws = _workspace("slab", sw, dev) if sw > 0 else None
+        call("mms2ut_conv1d_glu_bwd", snap, dy.data_ptr(), scratch.data_ptr(),
+             None if main_ws is None else main_ws.data_ptr(), mw, None if side_ws is None else side_ws.data_ptr(), sw,
+             SIDE_WGRAD_BLOCKS if side else 0, _s(), side)
+        if side:
+            # the side stream reads the arena (im2col images) and the scratch (GLU gradients)
+            _Side.keep.extend((arena, scratch, dy))
+            _Side.used = True
+
+
 def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None):
     """dx[M,K] = dy[M,N] @ W[N,K]  (W row-major, reduction over N).  Reads the W^T image when one
     is registered (TransposedWeights), else W itself through transposed fragment reads.

@@ -517,6 +517,7 @@ class MMS2UTModel:
         self.wt = None  # K.TransposedWeights of the dgrad weights (built at the first training forward)
         self._wpad = {}  # subsampler conv weights zero-padded to whole 64-wide k-tiles (subsample_fwd)
         self._layer_calls = {}  # layer prefix -> K.LayerCall (one-call transformer layers)
+        self._conv = None       # K.ConvCall (one-call subsampler)
 
     def dgrad_weights(self):
         """Every weight matrix the hand-written backward multiplies a gradient by (dx = dy @ W),
@@ -681,8 +682,32 @@ class MMS2UTModel:
         return tab
 
     # -------------------------------------------------------------- subsampler
+    def _conv_call(self):
+        """The K.ConvCall of the subsampler (bound to its weight / gradient / W^T slots)."""
+        if self._conv is None:
+            ks = list(self.cfg["conv_kernel_sizes"])
+            Ws = [self.P(f"encoder.subsample.conv_layers.{i}.weight") for i in range(len(ks))]
+            self._conv = K.ConvCall(
+                ks, [W.shape[0] for W in Ws], Ws, [self.P(f"encoder.subsample.conv_layers.{i}.bias") for i in range(len(ks))],
+                [self.G(f"encoder.subsample.conv_layers.{i}.weight") for i in range(len(ks))],
+                [self.G(f"encoder.subsample.conv_layers.{i}.bias") for i in range(len(ks))],
+                {i: Ws[i].view(Ws[i].shape[0], -1) for i in range(1, len(ks))})
+        return self._conv
+
     def subsample_fwd(self, src, lens):
-        """fairseq Conv1dSubsampler: conv(k, s2, p k//2) -> GLU, twice; implicit GEMM."""
+        """fairseq Conv1dSubsampler (conv(k, s2, p k//2) -> GLU per layer) in one library call
+        (mms2ut_conv1d_glu_fwd); bit-identical to subsample_fwd_ref."""
+        B, Ts, Cin = src.shape
+        cc = self._conv_call()
+        arena, out, snap = cc.fwd(src.reshape(B * Ts, Cin), B, Ts, Cin)
+        return out, out.shape[0] // B, {"arena": arena, "snap": snap}
+
+    def subsample_bwd(self, ctx, dx):
+        self._conv_call().bwd(ctx["snap"], ctx["arena"], dx.contiguous())
+
+    def subsample_fwd_ref(self, src, lens):
+        """fairseq Conv1dSubsampler: conv(k, s2, p k//2) -> GLU, twice; implicit GEMM, one launch
+        at a time from Python (the reference sequence the one-call path is checked against)."""
         cfg = self.cfg
         B, Ts, Cin = src.shape
         ctx = {"B": B, "Ts": Ts, "layers": []}
@@ -715,7 +740,7 @@ class MMS2UTModel:
             x, Tin, C = g, Tout, Cg
         return x, Tin, ctx
 
-    def subsample_bwd(self, ctx, dx):
+    def subsample_bwd_ref(self, ctx, dx):
         B = ctx["B"]
         for i in reversed(range(len(ctx["layers"]))):
             L = ctx["layers"][i]

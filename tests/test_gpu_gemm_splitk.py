@@ -142,3 +142,42 @@ def test_pp_gemm_bit_identical(M, N, K):
         assert _rel(got, ref) < 2e-3
     finally:
         K_.call("mms2ut_gemm_set_pp", -1)
+
+
+@pytest.mark.parametrize("M,N,K", [(10000, 3072, 768), (9001, 2304, 768), (12000, 768, 3072), (9000, 1000, 128),
+                                   (9000, 1000, 64), (4500, 3072, 832)])
+def test_dp_gemm_bit_identical(M, N, K):
+    """gemm_dp.hip (persistent blocks, each tile's epilogue run inside the next tile's k-loop, the
+    next tile's first stage prefetched) against the one-tile-per-block 128x128 kernel: bit-identical
+    outputs for every fused epilogue, incl. ragged M / N, tiles of 1-2 k-steps (the deferred
+    fragments finished after the loop) and odd k-step counts (ring parity carried across tiles)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mm = pkg()
+    K_ = mm.kernels
+    assert -(-M // 128) * -(-N // 128) > 512
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 1)
+    x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
+    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).half()
+    b = (torch.randn(N, device="cuda", generator=g) * 0.1).half()
+    aux = torch.randn(M, 2 * N, device="cuda", generator=g).half()
+    c0 = torch.randn(M, N, device="cuda", generator=g).half()
+    try:
+        for name in _PP_EPIS:
+            epi = getattr(K_, "EPI_" + name)
+            outs = []
+            for mode in (0, 1):
+                K_.call("mms2ut_gemm_set_dp", mode)
+                out = c0.clone()
+                out2 = torch.zeros(M, N, dtype=torch.float16, device="cuda")
+                p = 0.1 if name in ("RELU_DROP", "DROP_RESID", "GELU_DROP", "GELU_DROP_BWD", "RELU_DROP_BWD") else 0.0
+                K_.gemm(x, W, out, M, N, K, lda=K, ldb=K, ldc=N, epi=epi, bias=b,
+                        aux=aux if name in ("DROP_RESID", "RELU_DROP_BWD", "GATE", "GELU_DROP_BWD") else None,
+                        ldaux=2 * N, out2=out2 if name in ("GATE", "GELU_DROP") else None, ldo2=N,
+                        p=p, seed=78, offset=3 * N, ld_rng=N, fixup=False)
+                outs.append((out, out2))
+            torch.cuda.synchronize()
+            assert torch.equal(outs[1][0].view(torch.int16), outs[0][0].view(torch.int16)), name
+            assert torch.equal(outs[1][1].view(torch.int16), outs[0][1].view(torch.int16)), (name, "out2")
+    finally:
+        K_.call("mms2ut_gemm_set_dp", 0)

@@ -1,6 +1,7 @@
 """GPU: the one-call transformer layers (include/mms2ut.h mms2ut_layer_fwd / mms2ut_layer_bwd,
-csrc/layers.hip) match the per-launch path they replace (model.enc_layer_*_ref /
-dec_layer_*_ref, the kernel-by-kernel sequence the oracle parity tests pinned): logits, every
+csrc/layers.hip) and the one-call Conv1d subsampler (mms2ut_conv1d_glu_fwd / _bwd) match the
+per-launch path they replace (model.enc_layer_*_ref / dec_layer_*_ref / subsample_*_ref, the
+kernel-by-kernel sequence the oracle parity tests pinned): logits, every
 parameter gradient and the encoder-output gradient, dropout on at every site, on the base dims
 and on a short batch whose GEMMs take the split-K fixup path.  Also checks the layers with the
 weight-gradient side stream folded into the main stream (the bench's roofline pass)."""
@@ -33,8 +34,10 @@ def _step(mm, model, batch, cfg, ref):
         model.enc_layer_bwd = M.enc_layer_bwd_ref.__get__(model)
         model.dec_layer_fwd = M.dec_layer_fwd_ref.__get__(model)
         model.dec_layer_bwd = M.dec_layer_bwd_ref.__get__(model)
+        model.subsample_fwd = M.subsample_fwd_ref.__get__(model)
+        model.subsample_bwd = M.subsample_bwd_ref.__get__(model)
     else:
-        for n in ("enc_layer_fwd", "enc_layer_bwd", "dec_layer_fwd", "dec_layer_bwd"):
+        for n in ("enc_layer_fwd", "enc_layer_bwd", "dec_layer_fwd", "dec_layer_bwd", "subsample_fwd", "subsample_bwd"):
             model.__dict__.pop(n, None)
     model.drop.reset(4321)
     model.np_rng = _Draws()
