@@ -572,6 +572,52 @@ int mms2ut_conv1d_glu_bwd(const mms2ut_conv1d_glu* c, const mms2ut_half* dy, voi
                           int64_t main_ws_floats, float* side_ws, int64_t side_ws_floats, int side_blocks,
                           hipStream_t main, hipStream_t side);
 
+/* ---------------------------------------------------------------- gated fusion
+ * The fusion tail — SURVEY §8b mms2ut_gated_fusion_{fwd,bwd} (A6-A9: fuse_img_feat,
+ * mm_s2s_transformer.py:594-622; SelectiveAttention fuse.py:65-117, MultimodalAttention =
+ * nn.MultiheadAttention(add_bias_kv) fuse.py:145-167): image LayerNorm (image_pre_norm) +
+ * SA_image dropout into a [B][Ti + extra][Di] key layout, SA_text dropout, q = text Wq^T + bq,
+ * k|v = img Wkv^T + bkv (extra: + the bias_k|bias_v row per batch), one-head softmax attention
+ * (key padding mask [B][>= Tk] uint8, 1 = padded; SA_attention dropout), out-projection, and either
+ * the sigmoid gate (gate: merge = [attn_out | text], g = sigmoid(merge Wg^T + bg),
+ * out = text + g (attn_out - text)) or the residual out = text + attn_out.  The output lives in
+ * the arena (gated_fusion_arena's offset).  The backward writes d(text) (and with want_dimg the
+ * image-feature gradient) into the scratch (offsets from gated_fusion_scratch) and the parameter
+ * gradients (weight / bias gradients on `side`; g_ln / g_bias_kv are [gamma|beta], [k|v] spans).  */
+typedef struct mms2ut_gated_fusion {
+  int B, Te, Ti, Di, d;
+  int extra;                      /* multimodal_attention (add_bias_kv); 0: selective_attention  */
+  int gate;                       /* use_selective_gate                                          */
+  int image_pre_norm;
+  float eps;
+  float p_img, p_txt, p_attn;     /* SA_image / SA_text / SA_attention dropout                  */
+  uint64_t seed, off_img, off_txt, off_attn;
+  const uint8_t* key_mask;        /* [B][ld_mask], 1 = padded image key, or NULL                 */
+  int64_t ld_mask;
+  const mms2ut_half *ln_g, *ln_b, *wq, *bq, *wkv, *bkv, *bias_kv, *wo, *bo, *wg, *bg;
+  mms2ut_half *g_ln, *g_wq, *g_bq, *g_wkv, *g_bkv, *g_bias_kv, *g_wo, *g_bo, *g_wg, *g_bg;
+  const mms2ut_half *wt_q, *wt_kv, *wt_o, *wt_g;   /* W^T images for the dgrads, or NULL        */
+  const mms2ut_half* text;        /* [B*Te, d] encoder output                                    */
+  const mms2ut_half* img;         /* [B*Ti, Di] image features                                   */
+  void* saved;
+} mms2ut_gated_fusion;
+int mms2ut_gated_fusion_arena(const mms2ut_gated_fusion* f, int64_t* out_offset, int64_t* bytes);
+/* offsets[0] = d(text), offsets[1] = d(img) (-1 without want_dimg)                             */
+int mms2ut_gated_fusion_scratch(const mms2ut_gated_fusion* f, int want_dimg, int64_t* offsets, int64_t* bytes);
+int mms2ut_gated_fusion_ws(const mms2ut_gated_fusion* f, int64_t* main_floats, int64_t* side_floats);
+int mms2ut_gated_fusion_fwd(const mms2ut_gated_fusion* f, float* main_ws, int64_t main_ws_floats, hipStream_t stream);
+int mms2ut_gated_fusion_bwd(const mms2ut_gated_fusion* f, const mms2ut_half* dres, int want_dimg, void* scratch,
+                            float* main_ws, int64_t main_ws_floats, float* side_ws, int64_t side_ws_floats,
+                            int side_blocks, hipStream_t main, hipStream_t side);
+
+/* Buffer sizes of a coarse entry in one query: op MMS_OP_LAYER
+ * (desc = mms2ut_layer*), MMS_OP_CONV1D_GLU (mms2ut_conv1d_glu*) or MMS_OP_GATED_FUSION
+ * (mms2ut_gated_fusion*) -> sizes[0] forward arena bytes, [1] backward scratch bytes (layer: no
+ * emitted dropout; fusion: without the image gradient), [2] main-stream and [3] side-stream
+ * workspace floats.                                                                             */
+enum { MMS_OP_LAYER = 0, MMS_OP_CONV1D_GLU = 1, MMS_OP_GATED_FUSION = 2 };
+int mms2ut_workspace_size(int op, const void* desc, int64_t* sizes);
+
 #ifdef __cplusplus
 }
 #endif

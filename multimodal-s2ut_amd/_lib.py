@@ -101,6 +101,19 @@ class ConvArgs(C.Structure):
         [(n, vp * CONV_MAX) for n in ("w", "b", "wt", "g_w", "g_b")] + [("x", vp), ("saved", vp)]
 
 
+class FusionArgs(C.Structure):
+    """mms2ut_gated_fusion (include/mms2ut.h): the fusion tail."""
+    _fields_ = [(n, i32) for n in ("B", "Te", "Ti", "Di", "d", "extra", "gate", "image_pre_norm")] + \
+        [(n, f32) for n in ("eps", "p_img", "p_txt", "p_attn")] + [(n, u64) for n in ("seed", "off_img", "off_txt", "off_attn")] + \
+        [("key_mask", vp), ("ld_mask", i64)] + \
+        [(n, vp) for n in ("ln_g", "ln_b", "wq", "bq", "wkv", "bkv", "bias_kv", "wo", "bo", "wg", "bg",
+                           "g_ln", "g_wq", "g_bq", "g_wkv", "g_bkv", "g_bias_kv", "g_wo", "g_bo", "g_wg", "g_bg",
+                           "wt_q", "wt_kv", "wt_o", "wt_g", "text", "img", "saved")]
+
+
+OP_LAYER, OP_CONV1D_GLU, OP_GATED_FUSION = range(3)   # include/mms2ut.h MMS_OP_*
+
+
 class WgradArgs(C.Structure):
     """mms2ut_wgrad (include/mms2ut.h): one problem of a grouped weight-gradient launch."""
     _fields_ = [("dy", vp), ("lddy", i64), ("x", vp), ("ldx", i64), ("dW", vp), ("db", vp), ("N", i32), ("K", i32)]
@@ -191,6 +204,12 @@ SIGNATURES = {
     "mms2ut_layer_ws": (i32, [vp, vp, vp]),
     "mms2ut_layer_fwd": (i32, [vp, vp, i64, vp]),
     "mms2ut_layer_bwd": (i32, [vp, vp, vp, vp]),
+    "mms2ut_gated_fusion_arena": (i32, [vp, vp, vp]),
+    "mms2ut_gated_fusion_scratch": (i32, [vp, i32, vp, vp]),
+    "mms2ut_gated_fusion_ws": (i32, [vp, vp, vp]),
+    "mms2ut_gated_fusion_fwd": (i32, [vp, vp, i64, vp]),
+    "mms2ut_gated_fusion_bwd": (i32, [vp, vp, i32, vp, vp, i64, vp, i64, i32, vp, vp]),
+    "mms2ut_workspace_size": (i32, [i32, vp, vp]),
     "mms2ut_conv1d_glu_arena": (i32, [vp, vp, vp]),
     "mms2ut_conv1d_glu_scratch": (i32, [vp, vp, vp]),
     "mms2ut_conv1d_glu_ws": (i32, [vp, vp, vp]),

@@ -662,3 +662,389 @@ extern "C" int mms2ut_conv1d_glu_bwd(const mms2ut_conv1d_glu* c, const mms2ut_ha
   }
   return 0;
 }
+
+// ---------------------------------------------------------------- gated fusion (one call)
+// The reference fusion tail (fuse_img_feat, mm_s2s_transformer.py:594-622; fuse.py:65-117
+// SelectiveAttention / fuse.py:145-167 MultimodalAttention = nn.MultiheadAttention with
+// add_bias_kv) behind SURVEY §8b mms2ut_gated_fusion_{fwd,bwd}: image LayerNorm (+ SA_image
+// dropout, laid out as [B][Ti (+1 bias_kv row)][Di] keys), text dropout, q / k|v projections, one-head
+// attention over the image keys (scores materialised: hd = d is past the flash kernel's head
+// sizes), out-projection, and the sigmoid gate merge (or the plain residual without the gate).
+// The launch sequence, arguments and stream order are model.fusion_fwd_ref / fusion_bwd_ref's, so
+// results are bit-identical to that per-launch path (tests/test_gpu_layers.py).
+namespace {
+
+// kernels.linear_wgrad's choice: the grouped unsplit kernel for >= 256 output tiles whose shapes
+// it takes, else fp32 split-K slabs (wgrad above); both on the side stream
+bool wgrad_group_ok(const mms2ut_half* dy, int64_t lddy, const mms2ut_half* x, int64_t ldx, const mms2ut_half* dW,
+                    int64_t M, int64_t N, int64_t K) {
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return ((N + 127) / 128) * ((K + 127) / 128) >= 256 && N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0 &&
+         al16(dy) && al16(x) && al16(dW) && M * std::max(lddy, ldx) * 2 < (1LL << 31);
+}
+
+int wgrad_auto(const Ctx& c, const mms2ut_half* dy, int64_t lddy, const mms2ut_half* x, int64_t ldx, mms2ut_half* dW,
+               mms2ut_half* db, int64_t M, int64_t N, int64_t K, int side_blocks) {
+  if (wgrad_group_ok(dy, lddy, x, ldx, dW, M, N, K)) {
+    int rc = fork(c);
+    if (rc) return rc;
+    mms2ut_wgrad w{dy, lddy, x, ldx, dW, db, (int)N, (int)K};
+    return mms2ut_wgrad_group(&w, 1, M, c.side == c.main ? 0 : side_blocks, c.side);
+  }
+  return wgrad(c, dy, lddy, x, ldx, dW, db, M, N, K);
+}
+
+struct FusDims {
+  int64_t B, Te, Ti, Tk, Di, d, Rt, Ri, Rk, ldS;
+  bool extra, gate, pre, ln_fused;
+};
+
+FusDims fus_dims(const mms2ut_gated_fusion* f) {
+  FusDims D;
+  D.B = f->B; D.Te = f->Te; D.Ti = f->Ti; D.Di = f->Di; D.d = f->d;
+  D.extra = f->extra != 0; D.gate = f->gate != 0; D.pre = f->image_pre_norm != 0;
+  D.Tk = D.Ti + (D.extra ? 1 : 0);
+  D.Rt = D.B * D.Te; D.Ri = D.B * D.Ti; D.Rk = D.B * D.Tk;
+  D.ldS = (D.Tk + 7) / 8 * 8;
+  D.ln_fused = D.pre && D.Di % 256 == 0 && D.Di <= 1024;
+  return D;
+}
+
+enum { FA_IM = 0, FA_IR, FA_IMGN, FA_IMGD, FA_TEXTD, FA_Q, FA_KV, FA_S, FA_P, FA_PD, FA_O, FA_MERGE, FA_G, FA_OUT, FA_N };
+void fus_arena_sizes(const mms2ut_gated_fusion* f, const FusDims& D, int64_t* sz) {
+  for (int i = 0; i < FA_N; ++i) sz[i] = 0;
+  const int64_t h = 2;
+  if (D.pre) sz[FA_IM] = sz[FA_IR] = D.Ri * 4;
+  if (!D.ln_fused && (D.pre || f->p_img > 0.f)) sz[FA_IMGN] = D.Ri * D.Di * h;
+  if (D.ln_fused || D.extra) sz[FA_IMGD] = D.Rk * D.Di * h;
+  if (f->p_txt > 0.f) sz[FA_TEXTD] = D.Rt * D.d * h;
+  sz[FA_Q] = D.Rt * D.d * h;
+  sz[FA_KV] = D.Rk * 2 * D.d * h;
+  sz[FA_S] = sz[FA_P] = D.Rt * D.ldS * h;
+  if (f->p_attn > 0.f) sz[FA_PD] = sz[FA_P];
+  sz[FA_O] = D.Rt * D.d * h;
+  if (D.gate) { sz[FA_MERGE] = D.Rt * 2 * D.d * h; sz[FA_G] = D.Rt * D.d * h; }
+  sz[FA_OUT] = D.Rt * D.d * h;
+}
+
+enum { FS_DPRE = 0, FS_DMERGE, FS_DO, FS_DQ, FS_DKV, FS_DPD, FS_DIMGD, FS_DIMG, FS_DIMGIN, FS_DTEXT, FS_LNP, FS_KVP,
+       FS_BPART, FS_N };
+void fus_scratch_sizes(const mms2ut_gated_fusion* f, const FusDims& D, int want_dimg, int64_t* sz) {
+  for (int i = 0; i < FS_N; ++i) sz[i] = 0;
+  const int64_t h = 2;
+  if (D.gate) { sz[FS_DPRE] = D.Rt * D.d * h; sz[FS_DMERGE] = D.Rt * 2 * D.d * h; }
+  sz[FS_DO] = sz[FS_DQ] = D.Rt * D.d * h;
+  sz[FS_DKV] = D.Rk * 2 * D.d * h;
+  sz[FS_DPD] = D.Rt * D.ldS * h;
+  if (D.pre || want_dimg) {
+    sz[FS_DIMGD] = D.Rk * D.Di * h;
+    sz[FS_DIMG] = D.Ri * D.Di * h;
+    sz[FS_DIMGIN] = D.Ri * D.Di * h;
+    if (D.pre) sz[FS_LNP] = (int64_t)mms2ut_layernorm_bwd_nparts(D.Ri, (int)D.Di) * 2 * D.Di * 4;
+  }
+  sz[FS_DTEXT] = D.Rt * D.d * h;
+  if (D.extra) sz[FS_KVP] = (int64_t)mms2ut_colsum_nparts(D.B) * 2 * D.d * 4;
+  sz[FS_BPART] = (int64_t)mms2ut_colsum_nparts(std::max(D.Rt, D.Rk)) * 2 * D.d * 4;
+}
+
+int fus_check(const mms2ut_gated_fusion* f) {
+  MMS_REQUIRE(f && f->B >= 1 && f->Te >= 1 && f->Ti >= 1, "gated_fusion: B, Te, Ti must be >= 1");
+  MMS_REQUIRE(f->d % 8 == 0 && f->Di % 8 == 0 && f->d > 0 && f->Di > 0, "gated_fusion: d=%d Di=%d (multiples of 8)", f->d, f->Di);
+  MMS_REQUIRE(f->wq && f->bq && f->wkv && f->bkv && f->wo && f->bo, "gated_fusion: projection weights / biases required");
+  MMS_REQUIRE(!f->extra || f->bias_kv, "gated_fusion: multimodal attention needs bias_kv");
+  MMS_REQUIRE(!f->gate || (f->wg && f->bg), "gated_fusion: the gate needs its weight and bias");
+  MMS_REQUIRE(!f->image_pre_norm || (f->ln_g && f->ln_b), "gated_fusion: image_pre_norm needs the LayerNorm");
+  return 0;
+}
+
+mms2ut_gemm_args batched(const mms2ut_half* A, const mms2ut_half* B_, void* C, int M, int N, int K, int a_kc, int b_kc,
+                         int64_t lda, int64_t ldb, int64_t ldc, int batch, int64_t sA, int64_t sB, int64_t sC,
+                         float alpha) {
+  // model.attn_fwd / attn_bwd's batched products (H = 1: bdiv 1, the head strides unused)
+  mms2ut_gemm_args a = gemm_args();
+  a.A = A; a.B = B_; a.C = C;
+  a.M = M; a.N = N; a.K = K;
+  a.a_kcontig = a_kc; a.b_kcontig = b_kc;
+  a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.batch = batch; a.bdiv = 1;
+  a.sA1 = sA; a.sB1 = sB; a.sC1 = sC;
+  a.sA2 = a.sB2 = a.sC2 = 0;
+  a.alpha = alpha;
+  return a;
+}
+
+int zero_rows(mms2ut_half* p, int64_t pitch_elems, int64_t width_elems, int64_t rows, hipStream_t s) {
+  if (hipMemset2DAsync(p, (size_t)pitch_elems * 2, 0, (size_t)width_elems * 2, (size_t)rows, s) != hipSuccess) {
+    mms::set_error("gated_fusion: hipMemset2DAsync failed");
+    return 1;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int mms2ut_gated_fusion_arena(const mms2ut_gated_fusion* f, int64_t* out_offset, int64_t* bytes) {
+  if (int rc = fus_check(f)) return rc;
+  MMS_REQUIRE(bytes, "gated_fusion_arena: null");
+  const FusDims D = fus_dims(f);
+  int64_t sz[FA_N], off[FA_N];
+  fus_arena_sizes(f, D, sz);
+  *bytes = layout(sz, FA_N, off);
+  if (out_offset) *out_offset = off[FA_OUT];
+  return 0;
+}
+
+extern "C" int mms2ut_gated_fusion_scratch(const mms2ut_gated_fusion* f, int want_dimg, int64_t* offsets, int64_t* bytes) {
+  if (int rc = fus_check(f)) return rc;
+  MMS_REQUIRE(bytes, "gated_fusion_scratch: null");
+  const FusDims D = fus_dims(f);
+  int64_t sz[FS_N], off[FS_N];
+  fus_scratch_sizes(f, D, want_dimg, sz);
+  *bytes = layout(sz, FS_N, off);
+  if (offsets) {
+    offsets[0] = off[FS_DTEXT];
+    // the image gradient: LN backward's dx, or the (un-padded, dropout-applied) key gradient
+    offsets[1] = want_dimg ? (D.pre ? off[FS_DIMGIN] : (D.extra ? off[FS_DIMG] : off[FS_DIMGD])) : -1;
+  }
+  return 0;
+}
+
+extern "C" int mms2ut_gated_fusion_ws(const mms2ut_gated_fusion* f, int64_t* main_floats, int64_t* side_floats) {
+  if (int rc = fus_check(f)) return rc;
+  MMS_REQUIRE(main_floats && side_floats, "gated_fusion_ws: null");
+  const FusDims D = fus_dims(f);
+  int64_t mw = 0, sw = 0;
+  auto fw = [&](int64_t M, int64_t N, int64_t K) {
+    const int s = fixup_splits(M, N, K);
+    if (s > 1) mw = std::max(mw, (int64_t)s * M * N);
+  };
+  auto ww = [&](int64_t M, int64_t N, int64_t K) {
+    const int s = wgrad_splits(((N + 127) / 128) * ((K + 127) / 128), M);
+    sw = std::max(sw, (int64_t)s * N * K + (int64_t)s * N);
+  };
+  const int64_t d = D.d;
+  fw(D.Rt, d, d); fw(D.Rk, 2 * d, D.Di); fw(D.Rt, d, d); fw(D.Rt, d, 2 * d);      // forward
+  fw(D.Rt, 2 * d, d); fw(D.Rt, d, d); fw(D.Rk, D.Di, 2 * d); fw(D.Rt, d, d);      // dgrads
+  ww(D.Rt, d, 2 * d); ww(D.Rt, d, d); ww(D.Rk, 2 * d, D.Di); ww(D.Rt, d, d);      // weight gradients
+  *main_floats = mw;
+  *side_floats = sw;
+  return 0;
+}
+
+extern "C" int mms2ut_gated_fusion_fwd(const mms2ut_gated_fusion* f, float* main_ws, int64_t main_ws_floats,
+                                       hipStream_t s) {
+  if (int rc = fus_check(f)) return rc;
+  MMS_REQUIRE(f->text && f->img && f->saved, "gated_fusion_fwd: null text / image / arena");
+  const FusDims D = fus_dims(f);
+  int64_t sz[FA_N], off[FA_N];
+  fus_arena_sizes(f, D, sz);
+  layout(sz, FA_N, off);
+  void* A = f->saved;
+  auto H_ = [&](int slot) { return at<mms2ut_half>(A, off, slot); };
+  const Ctx c{s, s, main_ws, main_ws_floats, nullptr, 0, nullptr};
+  const int64_t d = D.d, Di = D.Di;
+  int rc;
+  // image: LayerNorm (+ dropout) into the [B][Tk][Di] key layout (bias_kv row zero)
+  const mms2ut_half* imgd;
+  if (D.ln_fused) {
+    if (D.extra && (rc = zero_rows(H_(FA_IMGD) + D.Ti * Di, D.Tk * Di, Di, D.B, s))) return rc;
+    if ((rc = mms2ut_layernorm_fwd_ex(f->img, f->ln_g, f->ln_b, H_(FA_IMGD), at<float>(A, off, FA_IM),
+                                      at<float>(A, off, FA_IR), D.Ri, (int)Di, f->eps, D.extra ? D.Ti : 0,
+                                      D.extra ? D.Tk : 0, f->p_img, f->seed, f->off_img, s))) return rc;
+    imgd = H_(FA_IMGD);
+  } else {
+    const mms2ut_half* imgn = f->img;
+    if (D.pre) {
+      if ((rc = mms2ut_layernorm_fwd(f->img, f->ln_g, f->ln_b, H_(FA_IMGN), at<float>(A, off, FA_IM),
+                                     at<float>(A, off, FA_IR), D.Ri, (int)Di, f->eps, s))) return rc;
+      imgn = H_(FA_IMGN);
+    }
+    if (f->p_img > 0.f) {
+      if ((rc = mms2ut_dropout_fwd(imgn, H_(FA_IMGN), D.Ri * Di, f->p_img, f->seed, f->off_img, s))) return rc;
+      imgn = H_(FA_IMGN);
+    }
+    if (D.extra) {
+      if (hipMemsetAsync(H_(FA_IMGD), 0, (size_t)D.Rk * Di * 2, s) != hipSuccess) {
+        mms::set_error("gated_fusion_fwd: hipMemsetAsync failed");
+        return 1;
+      }
+      if ((rc = mms2ut_copy2d(imgn, D.Ti * Di, H_(FA_IMGD), D.Tk * Di, D.B, (int)(D.Ti * Di), s))) return rc;
+      imgd = H_(FA_IMGD);
+    } else {
+      imgd = imgn;
+    }
+  }
+  const mms2ut_half* textd = f->text;
+  if (f->p_txt > 0.f) {
+    if ((rc = mms2ut_dropout_fwd(f->text, H_(FA_TEXTD), D.Rt * d, f->p_txt, f->seed, f->off_txt, s))) return rc;
+    textd = H_(FA_TEXTD);
+  }
+  mms2ut_half *q = H_(FA_Q), *kv = H_(FA_KV), *O = H_(FA_O);
+  if ((rc = linear(c, textd, f->wq, f->bq, q, D.Rt, d, d))) return rc;
+  if ((rc = linear(c, imgd, f->wkv, f->bkv, kv, D.Rk, 2 * d, Di))) return rc;
+  if (D.extra && (rc = mms2ut_copy2d(f->bias_kv, 0, kv + D.Ti * 2 * d, D.Tk * 2 * d, D.B, (int)(2 * d), s))) return rc;
+  // one-head attention, scores materialised (model.attn_fwd)
+  const float scale = (float)pow((double)d, -0.5);
+  mms2ut_half *S = H_(FA_S), *P = H_(FA_P), *Pd = f->p_attn > 0.f ? H_(FA_PD) : P;
+  {
+    mms2ut_gemm_args a = batched(q, kv, S, (int)D.Te, (int)D.Tk, (int)d, 1, 1, d, 2 * d, D.ldS, (int)D.B, D.Te * d,
+                                 D.Tk * 2 * d, D.Te * D.ldS, scale);
+    if ((rc = mms2ut_gemm_f16(&a, s))) return rc;
+  }
+  if ((rc = mms2ut_attn_softmax_fwd(S, P, Pd, (int)D.B, 1, (int)D.Te, (int)D.Tk, D.ldS, nullptr, f->key_mask,
+                                    f->key_mask ? f->ld_mask : 0, 0, D.extra ? 1 : 0, f->p_attn,
+                                    f->p_attn > 0.f ? f->seed : 0, f->p_attn > 0.f ? f->off_attn : 0, s))) return rc;
+  {
+    mms2ut_gemm_args a = batched(Pd, kv + d, O, (int)D.Te, (int)d, (int)D.Tk, 1, 0, D.ldS, 2 * d, d, (int)D.B,
+                                 D.Te * D.ldS, D.Tk * 2 * d, D.Te * d, 1.f);
+    if ((rc = mms2ut_gemm_f16(&a, s))) return rc;
+  }
+  mms2ut_half* out = H_(FA_OUT);
+  if (D.gate) {
+    mms2ut_half* merge = H_(FA_MERGE);
+    if ((rc = gemm_nt(c, O, d, f->wo, d, 1, merge, 2 * d, D.Rt, d, d, MMS_EPI_F16, f->bo, nullptr, 0, 0.f, 0, 0, d)))
+      return rc;
+    if ((rc = mms2ut_copy2d(textd, d, merge + d, 2 * d, D.Rt, (int)d, s))) return rc;
+    mms2ut_gemm_args a = gemm_args();
+    a.A = merge; a.B = f->wg; a.C = out;
+    a.M = (int)D.Rt; a.N = (int)d; a.K = (int)(2 * d);
+    a.a_kcontig = 1; a.b_kcontig = 1;
+    a.lda = 2 * d; a.ldb = 2 * d; a.ldc = d;
+    a.epi = MMS_EPI_GATE; a.bias = f->bg; a.aux = merge; a.ldaux = 2 * d; a.out2 = H_(FA_G); a.ldo2 = d;
+    a.ld_rng = d;
+    const int sp = fixup_splits(D.Rt, d, 2 * d);
+    if (sp > 1) {
+      MMS_REQUIRE(main_ws && main_ws_floats >= (int64_t)sp * D.Rt * d, "gated_fusion_fwd: main workspace too small");
+      a.splitk = sp; a.splitk_ws = main_ws; a.splitk_ws_floats = main_ws_floats;
+    }
+    return mms2ut_gemm_f16(&a, s);
+  }
+  return linear(c, O, f->wo, f->bo, out, D.Rt, d, d, MMS_EPI_DROP_RESID, textd);
+}
+
+extern "C" int mms2ut_gated_fusion_bwd(const mms2ut_gated_fusion* f, const mms2ut_half* dres, int want_dimg,
+                                       void* scratch, float* main_ws, int64_t main_ws_floats, float* side_ws,
+                                       int64_t side_ws_floats, int side_blocks, hipStream_t main, hipStream_t side) {
+  if (int rc = fus_check(f)) return rc;
+  MMS_REQUIRE(dres && scratch && f->saved, "gated_fusion_bwd: null gradient / scratch / arena");
+  if (!side) side = main;
+  const FusDims D = fus_dims(f);
+  int64_t sz[FA_N], off[FA_N], ssz[FS_N], so[FS_N];
+  fus_arena_sizes(f, D, sz);
+  layout(sz, FA_N, off);
+  fus_scratch_sizes(f, D, want_dimg, ssz);
+  layout(ssz, FS_N, so);
+  void* A = f->saved;
+  void* S = scratch;
+  auto H_ = [&](int slot) { return at<mms2ut_half>(A, off, slot); };
+  auto SH = [&](int slot) { return at<mms2ut_half>(S, so, slot); };
+  auto SF = [&](int slot) { return at<float>(S, so, slot); };
+  const Ctx c{main, side, main_ws, main_ws_floats, side_ws, side_ws_floats, SF(FS_BPART), nullptr, nullptr, false};
+  const int64_t d = D.d, Di = D.Di;
+  const mms2ut_half* textd = f->p_txt > 0.f ? H_(FA_TEXTD) : f->text;
+  const mms2ut_half* imgd = (D.ln_fused || D.extra) ? H_(FA_IMGD) : (!D.ln_fused && (D.pre || f->p_img > 0.f) ? H_(FA_IMGN) : f->img);
+  int rc;
+  const mms2ut_half *dOp = dres, *dtext = dres;
+  int64_t lddop = d, lddtext = d;
+  if (D.gate) {
+    mms2ut_half *dpre = SH(FS_DPRE), *dmerge = SH(FS_DMERGE);
+    if ((rc = mms2ut_gate_bwd(dres, H_(FA_MERGE), H_(FA_G), dpre, dmerge, D.Rt, (int)d, main))) return rc;
+    if ((rc = wgrad_auto(c, dpre, d, H_(FA_MERGE), 2 * d, f->g_wg, f->g_bg, D.Rt, d, 2 * d, side_blocks))) return rc;
+    if ((rc = dgrad(c, dpre, d, f->wg, f->wt_g, dmerge, D.Rt, d, 2 * d, MMS_EPI_F16_ACC))) return rc;
+    dOp = dmerge; lddop = 2 * d;
+    dtext = dmerge + d; lddtext = 2 * d;
+  }
+  if ((rc = wgrad_auto(c, dOp, lddop, H_(FA_O), d, f->g_wo, f->g_bo, D.Rt, d, d, side_blocks))) return rc;
+  mms2ut_half* dO = SH(FS_DO);
+  if ((rc = dgrad(c, dOp, lddop, f->wo, f->wt_o, dO, D.Rt, d, d))) return rc;
+  // attention backward (model.attn_bwd)
+  const float scale = (float)pow((double)d, -0.5);
+  const mms2ut_half *q = H_(FA_Q), *kv = H_(FA_KV), *P = H_(FA_P), *Pd = f->p_attn > 0.f ? H_(FA_PD) : P;
+  mms2ut_half *dq = SH(FS_DQ), *dkv = SH(FS_DKV), *dPd = SH(FS_DPD);
+  const int B = (int)D.B, Te = (int)D.Te, Tk = (int)D.Tk;
+  const int64_t sS = D.Te * D.ldS;
+  {
+    mms2ut_gemm_args a = batched(dO, kv + d, dPd, Te, Tk, (int)d, 1, 1, d, 2 * d, D.ldS, B, D.Te * d, D.Tk * 2 * d, sS, 1.f);
+    if ((rc = mms2ut_gemm_f16(&a, main))) return rc;
+    a = batched(Pd, dO, dkv + d, Tk, (int)d, Te, 0, 0, D.ldS, d, 2 * d, B, sS, D.Te * d, D.Tk * 2 * d, 1.f);
+    if ((rc = mms2ut_gemm_f16(&a, main))) return rc;
+  }
+  if ((rc = mms2ut_attn_softmax_bwd(P, dPd, dPd, B, 1, Te, Tk, D.ldS, nullptr, 0, 0, f->p_attn,
+                                    f->p_attn > 0.f ? f->seed : 0, f->p_attn > 0.f ? f->off_attn : 0, main))) return rc;
+  {
+    mms2ut_gemm_args a = batched(dPd, kv, dq, Te, (int)d, Tk, 1, 0, D.ldS, 2 * d, d, B, sS, D.Tk * 2 * d, D.Te * d, scale);
+    if ((rc = mms2ut_gemm_f16(&a, main))) return rc;
+    a = batched(dPd, q, dkv, Tk, (int)d, Te, 0, 0, D.ldS, d, 2 * d, B, sS, D.Te * d, D.Tk * 2 * d, scale);
+    if ((rc = mms2ut_gemm_f16(&a, main))) return rc;
+  }
+  if (D.extra) {
+    // bias_k / bias_v gradients: the batch sum of the extra key row's gradient (main stream), then
+    // that row is zeroed for the k|v weight gradient
+    mms2ut_half* rows = dkv + D.Ti * 2 * d;
+    const int np = mms2ut_colsum_nparts(D.B);
+    if ((rc = mms2ut_colsum_f16(rows, D.B, (int)(2 * d), D.Tk * 2 * d, SF(FS_KVP), np, main))) return rc;
+    if ((rc = mms2ut_colsum_parts(SF(FS_KVP), np, (int)(2 * d), f->g_bias_kv, 0, main))) return rc;
+    if ((rc = zero_rows(rows, D.Tk * 2 * d, 2 * d, D.B, main))) return rc;
+  }
+  if ((rc = wgrad_auto(c, dkv, 2 * d, imgd, Di, f->g_wkv, f->g_bkv, D.Rk, 2 * d, Di, side_blocks))) return rc;
+  if (D.ln_fused) {
+    mms2ut_half* dimgd = SH(FS_DIMGD);
+    if ((rc = dgrad(c, dkv, 2 * d, f->wkv, f->wt_kv, dimgd, D.Rk, 2 * d, Di))) return rc;
+    if ((rc = mms2ut_layernorm_bwd_ex(dimgd, f->img, f->ln_g, at<float>(A, off, FA_IM), at<float>(A, off, FA_IR), nullptr,
+                                      want_dimg ? SH(FS_DIMGIN) : nullptr, SF(FS_LNP), D.Ri, (int)Di, nullptr, 0.f, 0, 0,
+                                      D.extra ? D.Ti : 0, D.extra ? D.Tk : 0, f->p_img, f->p_img > 0.f ? f->seed : 0,
+                                      f->p_img > 0.f ? f->off_img : 0, main))) return rc;
+    if ((rc = fork(c)) ||
+        (rc = mms2ut_colsum_parts(SF(FS_LNP), mms2ut_layernorm_bwd_nparts(D.Ri, (int)Di), (int)(2 * Di), f->g_ln, 0, side)))
+      return rc;
+  } else if (D.pre || want_dimg) {
+    mms2ut_half* dimgd = SH(FS_DIMGD);
+    if ((rc = dgrad(c, dkv, 2 * d, f->wkv, f->wt_kv, dimgd, D.Rk, 2 * d, Di))) return rc;
+    mms2ut_half* dimg = dimgd;
+    if (D.extra) {
+      dimg = SH(FS_DIMG);
+      if ((rc = mms2ut_copy2d(dimgd, D.Tk * Di, dimg, D.Ti * Di, D.B, (int)(D.Ti * Di), main))) return rc;
+    }
+    if (f->p_img > 0.f && (rc = mms2ut_dropout_fwd(dimg, dimg, D.Ri * Di, f->p_img, f->seed, f->off_img, main))) return rc;
+    if (D.pre) {
+      if ((rc = ln_bwd(c, dimg, f->img, f->ln_g, at<float>(A, off, FA_IM), at<float>(A, off, FA_IR), nullptr,
+                       want_dimg ? SH(FS_DIMGIN) : nullptr, nullptr, 0.f, 0, 0, SF(FS_LNP), f->g_ln, D.Ri, (int)Di)))
+        return rc;
+    }
+  }
+  if ((rc = wgrad_auto(c, dq, d, textd, d, f->g_wq, f->g_bq, D.Rt, d, d, side_blocks))) return rc;
+  mms2ut_half* dtt = SH(FS_DTEXT);
+  if ((rc = mms2ut_copy2d(dtext, lddtext, dtt, d, D.Rt, (int)d, main))) return rc;
+  if ((rc = dgrad(c, dq, d, f->wq, f->wt_q, dtt, D.Rt, d, d, MMS_EPI_F16_ACC))) return rc;
+  if (f->p_txt > 0.f && (rc = mms2ut_dropout_fwd(dtt, dtt, D.Rt * d, f->p_txt, f->seed, f->off_txt, main))) return rc;
+  return 0;
+}
+
+extern "C" int mms2ut_workspace_size(int op, const void* desc, int64_t* sizes) {
+  MMS_REQUIRE(desc && sizes, "workspace_size: null");
+  int rc;
+  switch (op) {
+    case MMS_OP_LAYER: {
+      const mms2ut_layer* L = static_cast<const mms2ut_layer*>(desc);
+      if ((rc = mms2ut_layer_arena(L, nullptr, &sizes[0])) || (rc = mms2ut_layer_scratch(L, 0.f, nullptr, &sizes[1])))
+        return rc;
+      return mms2ut_layer_ws(L, &sizes[2], &sizes[3]);
+    }
+    case MMS_OP_CONV1D_GLU: {
+      const mms2ut_conv1d_glu* c = static_cast<const mms2ut_conv1d_glu*>(desc);
+      if ((rc = mms2ut_conv1d_glu_arena(c, nullptr, &sizes[0])) || (rc = mms2ut_conv1d_glu_scratch(c, nullptr, &sizes[1])))
+        return rc;
+      return mms2ut_conv1d_glu_ws(c, &sizes[2], &sizes[3]);
+    }
+    case MMS_OP_GATED_FUSION: {
+      const mms2ut_gated_fusion* f = static_cast<const mms2ut_gated_fusion*>(desc);
+      if ((rc = mms2ut_gated_fusion_arena(f, nullptr, &sizes[0])) ||
+          (rc = mms2ut_gated_fusion_scratch(f, 0, nullptr, &sizes[1])))
+        return rc;
+      return mms2ut_gated_fusion_ws(f, &sizes[2], &sizes[3]);
+    }
+    default:
+      mms::set_error("workspace_size: unknown op %d", op);
+      return 1;
+  }
+}

@@ -457,6 +457,102 @@ class ConvCall:
             _Side.used = True
 
 
+class FusionCall:
+    """The fusion tail (image LN, q / k|v projections, one-head attention, out-projection, sigmoid
+    gate) enqueued by one library call each way (include/mms2ut.h mms2ut_gated_fusion_fwd / _bwd).
+    Parameter / gradient / W^T pointers are bound once; each forward sets shapes, dropout sites and
+    the arena and snapshots the argument block for its backward."""
+
+    _sizes = {}
+
+    def __init__(self, flags, params, grads, dgrad_weights):
+        a = _lib.FusionArgs()
+        for f, v in flags.items():
+            setattr(a, f, v)
+        for f, t in params.items():
+            setattr(a, f, 0 if t is None else t.data_ptr())
+        for f, t in grads.items():
+            setattr(a, f, 0 if t is None else t.data_ptr())
+        self.a = a
+        self.dgrad_weights = dgrad_weights      # {"wt_q": W, ...}
+        self.wt_of = None
+
+    def _bind_wt(self):
+        wt = TransposedWeights.active
+        if wt is self.wt_of:
+            return
+        for f, W in self.dgrad_weights.items():
+            img = wt.get(W, wait=False) if wt is not None else None
+            setattr(self.a, f, 0 if img is None else img.data_ptr())
+        self.wt_of = wt
+
+    def sizes(self, want_dimg):
+        a = self.a
+        key = (a.B, a.Te, a.Ti, a.Di, a.d, a.extra, a.gate, a.image_pre_norm, a.p_img > 0, a.p_txt > 0, a.p_attn > 0,
+               bool(want_dimg))
+        s = FusionCall._sizes.get(key)
+        if s is None:
+            oo, nb, sb, mw, sw = (ctypes.c_int64() for _ in range(5))
+            so = (ctypes.c_int64 * 2)()
+            call("mms2ut_gated_fusion_arena", ctypes.byref(a), ctypes.byref(oo), ctypes.byref(nb))
+            call("mms2ut_gated_fusion_scratch", ctypes.byref(a), int(want_dimg), so, ctypes.byref(sb))
+            call("mms2ut_gated_fusion_ws", ctypes.byref(a), ctypes.byref(mw), ctypes.byref(sw))
+            s = (nb.value, oo.value, sb.value, list(so), mw.value, sw.value)
+            FusionCall._sizes[key] = s
+        return s
+
+    def fwd(self, text, img, key_mask, B, Te, Ti, p, drops):
+        """p = (p_img, p_txt, p_attn); drops = their (seed, offset) pairs or None.
+        Returns (arena, output [B*Te, d] view, argument snapshot)."""
+        a = self.a
+        a.B, a.Te, a.Ti = B, Te, Ti
+        a.p_img, a.p_txt, a.p_attn = p
+        seeds = [dr[0] for dr in drops if dr is not None]
+        a.seed = seeds[0] if seeds else 0
+        assert all(sd == a.seed for sd in seeds), "one dropout seed per step"
+        a.off_img, a.off_txt, a.off_attn = (dr[1] if dr is not None else 0 for dr in drops)
+        a.key_mask, a.ld_mask = (key_mask.data_ptr(), key_mask.stride(0)) if key_mask is not None else (0, 0)
+        a.text, a.img = text.data_ptr(), img.data_ptr()
+        self._bind_wt()
+        nb, oo, _, _, mw, _ = self.sizes(False)
+        arena = torch.empty(nb, dtype=torch.uint8, device=text.device)
+        a.saved = arena.data_ptr()
+        ws = stream_workspace(mw, text.device)
+        call("mms2ut_gated_fusion_fwd", ctypes.byref(a), None if ws is None else ws.data_ptr(), mw, _s())
+        out = arena[oo:oo + 2 * B * Te * a.d].view(F16).view(B * Te, a.d)
+        return arena, out, bytes(a)
+
+    def bwd(self, snap, arena, keep, dres, want_dimg=False):
+        """-> d(text) [B*Te, d] (and d(img) [B*Ti, Di] with want_dimg)."""
+        a = _lib.FusionArgs.from_buffer_copy(snap)
+        _, _, sbytes, so, mw, sw = self.sizes(want_dimg)
+        dev = dres.device
+        scratch = torch.empty(sbytes, dtype=torch.uint8, device=dev)
+        if TransposedWeights.active is not None:
+            TransposedWeights.active.wait_ready()
+        main_ws = stream_workspace(mw, dev)
+        side = 0
+        if _Side.enabled:
+            side_stream(dev)
+            side = _Side.ptr
+            with _SIDE_REGION:
+                side_ws = _workspace("slab", sw, dev) if sw > 0 else None
+        else:
+            side_ws = _workspace("slab", sw, dev) if sw > 0 else None
+        call("mms2ut_gated_fusion_bwd", snap, dres.data_ptr(), int(want_dimg), scratch.data_ptr(),
+             None if main_ws is None else main_ws.data_ptr(), mw, None if side_ws is None else side_ws.data_ptr(), sw,
+             SIDE_WGRAD_BLOCKS if side else 0, _s(), side)
+        if side:
+            _Side.keep.extend((arena, scratch, dres) + tuple(keep))
+            _Side.used = True
+        R, d = a.B * a.Te, a.d
+        dtext = scratch[so[0]:so[0] + 2 * R * d].view(F16).view(R, d)
+        if not want_dimg:
+            return dtext
+        Ri = a.B * a.Ti
+        return dtext, scratch[so[1]:so[1] + 2 * Ri * a.Di].view(F16).view(Ri, a.Di)
+
+
 def linear_dgrad(dy, W, out=None, *, epi=EPI_F16, aux=None, p=0.0, accumulate=False, drop=None):
     """dx[M,K] = dy[M,N] @ W[N,K]  (W row-major, reduction over N).  Reads the W^T image when one
     is registered (TransposedWeights), else W itself through transposed fragment reads.

@@ -518,6 +518,7 @@ class MMS2UTModel:
         self._wpad = {}  # subsampler conv weights zero-padded to whole 64-wide k-tiles (subsample_fwd)
         self._layer_calls = {}  # layer prefix -> K.LayerCall (one-call transformer layers)
         self._conv = None       # K.ConvCall (one-call subsampler)
+        self._fusion = {}       # image feature width -> K.FusionCall (one-call fusion tail)
 
     def dgrad_weights(self):
         """Every weight matrix the hand-written backward multiplies a gradient by (dx = dy @ W),
@@ -940,8 +941,81 @@ class MMS2UTModel:
                                dres=dx2, emit=emit)
 
     # -------------------------------------------------------------- fusion (fuse_img_feat)
+    def _fusion_call(self, Di):
+        """The K.FusionCall of the fusion tail (bound to its parameter / gradient / W^T slots)."""
+        fc = self._fusion.get(Di)
+        if fc is not None:
+            return fc
+        cfg, P, G, span = self.cfg, self.P, self.G, self.params.span
+        d = cfg["encoder_embed_dim"]
+        extra = cfg["multimodal_attention_type"] == "multimodal_attention"
+        if extra:
+            pre = "encoder.multimodal_attns.0"
+            if Di == d:
+                W, gW = P(pre + ".in_proj_weight"), G(pre + ".in_proj_weight")
+                Wq, Wkv, gWq, gWkv = W[:d], W[d:], gW[:d], gW[d:]
+            else:
+                Wq, gWq = P(pre + ".q_proj_weight"), G(pre + ".q_proj_weight")
+                Wkv = span(pre + ".k_proj_weight", pre + ".v_proj_weight").view(2 * d, Di)
+                gWkv = span(pre + ".k_proj_weight", pre + ".v_proj_weight", grad=True).view(2 * d, Di)
+            b, gb = P(pre + ".in_proj_bias"), G(pre + ".in_proj_bias")
+            bq, bkv, gbq, gbkv = b[:d], b[d:], gb[:d], gb[d:]
+            Wo, bo, gWo, gbo = (P(pre + ".out_proj.weight"), P(pre + ".out_proj.bias"), G(pre + ".out_proj.weight"),
+                                G(pre + ".out_proj.bias"))
+            bias_kv, g_bias_kv = span(pre + ".bias_k", pre + ".bias_v"), span(pre + ".bias_k", pre + ".bias_v", grad=True)
+        else:
+            pre = "encoder.selective_attns.0"
+            Wq, bq, gWq, gbq = (P(pre + ".q_proj.weight"), P(pre + ".q_proj.bias"), G(pre + ".q_proj.weight"),
+                                G(pre + ".q_proj.bias"))
+            Wkv = span(pre + ".k_proj.weight", pre + ".v_proj.weight").view(2 * d, Di)
+            gWkv = span(pre + ".k_proj.weight", pre + ".v_proj.weight", grad=True).view(2 * d, Di)
+            bkv, gbkv = span(pre + ".k_proj.bias", pre + ".v_proj.bias"), span(pre + ".k_proj.bias", pre + ".v_proj.bias", grad=True)
+            Wo, bo, gWo, gbo = P(pre + ".proj.weight"), P(pre + ".proj.bias"), G(pre + ".proj.weight"), G(pre + ".proj.bias")
+            bias_kv = g_bias_kv = None
+        gate, pre_norm = bool(cfg["use_selective_gate"]), bool(cfg["image_pre_norm"])
+        ln = "encoder.image_pre_norm_module"
+        params = {"ln_g": P(ln + ".weight") if pre_norm else None, "ln_b": P(ln + ".bias") if pre_norm else None,
+                  "wq": Wq, "bq": bq, "wkv": Wkv, "bkv": bkv, "bias_kv": bias_kv, "wo": Wo, "bo": bo,
+                  "wg": P("encoder.gate_denses.0.weight") if gate else None,
+                  "bg": P("encoder.gate_denses.0.bias") if gate else None}
+        grads = {"g_ln": span(ln + ".weight", ln + ".bias", grad=True) if pre_norm else None,
+                 "g_wq": gWq, "g_bq": gbq, "g_wkv": gWkv, "g_bkv": gbkv, "g_bias_kv": g_bias_kv, "g_wo": gWo, "g_bo": gbo,
+                 "g_wg": G("encoder.gate_denses.0.weight") if gate else None,
+                 "g_bg": G("encoder.gate_denses.0.bias") if gate else None}
+        wts = {"wt_q": Wq, "wt_kv": Wkv, "wt_o": Wo}
+        if gate:
+            wts["wt_g"] = P("encoder.gate_denses.0.weight")
+        flags = {"d": d, "Di": Di, "extra": int(extra), "gate": int(gate), "image_pre_norm": int(pre_norm), "eps": 1e-5}
+        fc = K.FusionCall(flags, params, grads, wts)
+        self._fusion[Di] = fc
+        return fc
+
     def fusion_fwd(self, text, img, img_mask, B, Te):
-        """mm_s2s_transformer.py:594-622. text [B*Te, d] (encoder out), img [B, Ti, Di] fp16."""
+        """mm_s2s_transformer.py:594-622 in one library call (mms2ut_gated_fusion_fwd); the same
+        dropout draws and bit-identical results as fusion_fwd_ref.  text [B*Te, d] (encoder out),
+        img [B, Ti, Di] fp16."""
+        cfg = self.cfg
+        d = cfg["encoder_embed_dim"]
+        _, Ti, Di = img.shape
+        extra = cfg["multimodal_attention_type"] == "multimodal_attention"
+        Tk = Ti + 1 if extra else Ti
+        pimg, ptxt, pat = self._p("SA_image_dropout"), self._p("SA_text_dropout"), self._p("SA_attention_dropout")
+        drops = (self._drop(pimg, B * Ti * Di), self._drop(ptxt, B * Te * d), self._drop(pat, B * Te * Tk))
+        img2 = img.reshape(B * Ti, Di).contiguous()
+        text = text.contiguous()
+        arena, out, snap = self._fusion_call(Di).fwd(text, img2, img_mask, B, Te, Ti, (pimg, ptxt, pat), drops)
+        c = {"B": B, "Te": Te, "Ti": Ti, "Di": Di, "Tk": Tk, "extra": extra, "pimg": pimg, "ptxt": ptxt, "pat": pat,
+             "drop_img": drops[0], "drop_txt": drops[1], "drop_attn": drops[2], "arena": arena, "snap": snap,
+             "keep": tuple(t for t in (text, img2, img_mask) if t is not None)}
+        return out, c
+
+    def fusion_bwd(self, c, dres, want_dimg=False):
+        """-> d(text) [B*Te, d]; with want_dimg also d(img) [B*Ti, Di] (mms2ut_gated_fusion_bwd)."""
+        return self._fusion_call(c["Di"]).bwd(c["snap"], c["arena"], c["keep"], dres.contiguous(), want_dimg)
+
+    def fusion_fwd_ref(self, text, img, img_mask, B, Te):
+        """mm_s2s_transformer.py:594-622, one launch at a time from Python (the reference sequence
+        the one-call path is checked against). text [B*Te, d] (encoder out), img [B, Ti, Di] fp16."""
         cfg = self.cfg
         d = cfg["encoder_embed_dim"]
         _, Ti, Di = img.shape
@@ -1031,7 +1105,7 @@ class MMS2UTModel:
             res = K.linear(O, Wo, bo, epi=K.EPI_DROP_RESID, aux=textd)
         return res, c
 
-    def fusion_bwd(self, c, dres, want_dimg=False):
+    def fusion_bwd_ref(self, c, dres, want_dimg=False):
         """-> d(text) [B*Te, d]; with want_dimg also d(img) [B*Ti, Di] (the image features are not
         leaves behind a QFormer)."""
         cfg = self.cfg
