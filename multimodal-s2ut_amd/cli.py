@@ -158,6 +158,9 @@ def _save(args, tr, rank):
     import os
     if not args.save_dir:
         return
+    # a run that went FATAL (sticky) since the last log boundary raises here, on every rank, instead
+    # of writing a checkpoint that could never apply another update (fairseq raises at the step)
+    tr.opt.check_fatal()
     state = tr.state_dict()          # every rank syncs; only rank 0 writes
     if rank != 0:
         return
@@ -190,6 +193,8 @@ def _restore(args, tr, dev):
     ti = es.get("train_iterator") or {}
     pos.update(num_updates=tr.completed_updates(), epoch=int(ti.get("epoch", 1)),
                iterations_in_epoch=int(ti.get("iterations_in_epoch", 0)))
+    # a resume that is already at --max-update saves this position again, not the default one
+    tr.position = {"epoch": pos["epoch"], "iterations_in_epoch": pos["iterations_in_epoch"]}
     return pos
 
 
