@@ -22,6 +22,7 @@ constexpr int WIN = 400, SHIFT = 160, NFFT = 512, NBIN = 257;
 constexpr int NC = 256;                        // complex FFT points (the real 512-point FFT's half)
 constexpr int FB_WAVES = 4;
 constexpr int MELW_MAX = 1024;                 // nonzero mel weights staged per block (80 bins: ~510)
+constexpr int FB_MAXB = 512;                   // utterances whose frame / sample offsets are staged in LDS
 
 struct FbankConst {
   float window[WIN];
@@ -39,6 +40,8 @@ struct FbankSmem {
   float win[WIN];
   float melw[MELW_MAX];
   int mlo[256], mlen[256], moff[256], ntot;
+  int foff[FB_MAXB + 1];                       // frame_off (B <= FB_MAXB)
+  long woff[FB_MAXB];                          // wave_off
   float x[FB_WAVES][WIN];
   float zr[FB_WAVES][NC], zi[FB_WAVES][NC];
   float pw[FB_WAVES][NBIN + 3];
@@ -75,6 +78,13 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
     const int lo = mel_range[2 * m], hi = mel_range[2 * m + 1];
     S.mlo[m] = lo;
     S.mlen[m] = hi - lo;
+  }
+  // utterance offsets in LDS: a frame's utterance is then found without a chain of dependent
+  // global loads (the binary search used to stall every frame on ~log2(B) L2 round trips)
+  const bool lds_off = B <= FB_MAXB;
+  if (lds_off) {
+    for (int i = tid; i <= B; i += blockDim.x) S.foff[i] = frame_off[i];
+    for (int i = tid; i < B; i += blockDim.x) S.woff[i] = wave_off[i];
   }
   __syncthreads();
   if (w == 0) {
@@ -121,7 +131,13 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
   // persistent: wave (block, w) takes frames w + FB_WAVES * block, + FB_WAVES * gridDim.x, ...;
   // the next frame's 400 samples are loaded into registers while the current one is transformed
   const int fstep = gridDim.x * FB_WAVES;
+  int utt = 0;   // utterance of the wave's last frame: frames only move forward, so the LDS walk
+                 // from it is a step or two per frame
   auto frame_src = [&](int f) {
+    if (lds_off) {
+      while (utt + 1 < B && S.foff[utt + 1] <= f) ++utt;
+      return wave + S.woff[utt] + (long)(f - S.foff[utt]) * SHIFT;
+    }
     int lo = 0, hi = B;   // utterance of frame f (binary search over frame_off)
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;

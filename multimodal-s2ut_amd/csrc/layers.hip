@@ -21,6 +21,7 @@
 // launch (mms2ut_wgrad_group) on the side stream at the end of the layer's backward — no fp32
 // split-K slabs, no reduction launches; it overlaps the next layer's dgrad chain.
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -206,6 +207,16 @@ int dgrad(const Ctx& c, const mms2ut_half* dy, int64_t lddy, const mms2ut_half* 
 }
 
 int fork(const Ctx& c) { return c.side == c.main ? 0 : mms2ut_stream_wait(c.side, c.main); }
+
+// MMS2UT_WGRAD_SPLIT (A/B): issue a layer's FFN weight gradients as a separate grouped launch
+int wgrad_split_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("MMS2UT_WGRAD_SPLIT");
+    m = e ? atoi(e) : 0;
+  }
+  return m;
+}
 
 // dW[N, K] = dy[M, N]^T @ x[M, K] and db[N] = colsum(dy), on the side stream (kernels.linear_wgrad):
 // fp32 split-K slabs with the bias partials as A-row sums, one reduction launch
@@ -418,6 +429,13 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
   if ((rc = wgrad(c, dyd, d, H_(MMS_SLOT_F1), F, L->g_w_fc2, L->g_b_fc2, R, d, F))) return rc;
   if ((rc = dgrad(c, SH(S_DF1), F, L->w_fc1, L->wt_fc1, SH(S_DH3), R, F, d))) return rc;
   if ((rc = wgrad(c, SH(S_DF1), F, H_(MMS_SLOT_H3), d, L->g_w_fc1, L->g_b_fc1, R, F, d))) return rc;
+  if (c.grouped && wgrad_split_mode()) {
+    // A/B (MMS2UT_WGRAD_SPLIT=1): the FFN weight gradients as their own grouped launch right here,
+    // beside the rest of this layer's (attention / LayerNorm) backward instead of the next layer's
+    // FFN dgrads; the attention projections' group follows at the end as usual
+    if ((rc = fork(c)) || (rc = mms2ut_wgrad_group(group, ngroup, R, side == main ? 0 : G->side_blocks, side))) return rc;
+    ngroup = 0;
+  }
   // LN3 backward: dx of the FFN input (+ the residual dy) and its dropout with the mask of the
   // block below's residual branch (cross-attention for the decoder, self-attention for the encoder)
   mms2ut_half* dxf = D.dec ? SH(S_DX3) : SH(S_DX2);
@@ -456,7 +474,7 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
   // LN1 backward: the layer input's gradient (+ dropout for the layer below when asked)
   if ((rc = ln_bwd(c, SH(S_DH1), L->x, L->ln1_g, F_(MMS_SLOT_M1), F_(MMS_SLOT_R1), dxa, SH(S_DX), SH(S_DXD), G->emit_p,
                    G->emit_seed, G->emit_offset, SF(S_P1), L->g_ln1, R, Dm))) return rc;
-  if (!c.grouped) return 0;
+  if (!c.grouped || ngroup == 0) return 0;
   // the layer's weight gradients: one grouped launch on the side stream, behind everything the
   // main stream enqueued for this layer (it overlaps the next layer's dgrad chain)
   if ((rc = fork(c))) return rc;
