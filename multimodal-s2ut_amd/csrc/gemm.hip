@@ -16,6 +16,8 @@
 // vector stores and 4-wide epilogue math.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "gemm_common.h"
 
 namespace {
@@ -1035,8 +1037,10 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
       return mmsg::launch_pp(a->epi, bm, P, tmp, tnp, s);
     }
   }
+  // (the deferred epilogue addresses C / aux / out2 through buffer descriptors: 31-bit extents)
+  const long ep_ext = 2 * ((long)(a->M - 1) * std::max<long>({(long)a->ldc, (long)a->ldaux, (long)a->ldo2}) + 2L * a->N);
   if (dma_ok && a_kc && b_kc && nz == 1 && a->epi != MMS_EPI_F32 && P.vec16 && a->N % 4 == 0 &&
-      (long)tm * tn > 512 && dp_mode()) {
+      (long)tm * tn > 512 && ep_ext < (1L << 31) && dp_mode()) {
     const int grid = 512;   // two blocks per CU, each walking its XCD's tiles
     P.stamps = stamp_take(grid);
     return mmsg::launch_dp(a->epi, P, tm, tn, grid, s);

@@ -23,6 +23,7 @@
 namespace {
 
 constexpr int DP_PIECES = 2;   // accumulator fragments of the previous tile finished per k-step
+constexpr int NP_ = 16 / DP_PIECES;   // k-steps of a tile that carry the previous tile's fragments
 
 template <int EPI>
 constexpr bool dp_aux() {
@@ -35,33 +36,61 @@ struct DpAux {
   h16x4 a, b, bias;
 };
 
-MMS_DEV h16x4 ld8b(const h16* p) { return *reinterpret_cast<const h16x4*>(p); }
+typedef unsigned int u32x2_dp __attribute__((ext_vector_type(2)));
+constexpr int kOut = (int)0x80000000;   // an offset past any extent (the host keeps extents < 2^31 bytes)
+
+// the epilogue's operands as buffer descriptors over their exact extents: a load past the extent
+// returns zero and a store past it is dropped, so every wave issues the same loads / stores
+// whatever its rows and columns
+struct DpRes {
+  __amdgpu_buffer_rsrc_t c, o2, aux, bias;
+};
+MMS_DEV __amdgpu_buffer_rsrc_t dp_rsrc(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, p ? (int)bytes : 0, 0x00020000);
+}
+MMS_DEV h16x4 dp_ld8(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(h16x4, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+MMS_DEV void dp_st8(__amdgpu_buffer_rsrc_t r, int off, h16x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_dp, v), r, off, 0, 0);
+}
 
 // fragment (i, j) of a wave's 64x64 accumulator tile: lane owns row (i*16 + (lane & 15)),
 // columns j*16 + 4*(lane >> 4) .. +3 (the (B, A)-swapped MFMA layout)
 template <int EPI>
-MMS_DEV DpAux dp_load(const GemmP& P, int m, int n) {
+MMS_DEV DpAux dp_load(const GemmP& P, const DpRes& R, int m, int n) {
   DpAux x;
-  x.a = h16x4{(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
-  x.b = x.a;
-  x.bias = x.a;
-  if (m >= P.M || n >= P.N) return x;
-  if (EPI != MMS_EPI_RELU_DROP_BWD && EPI != MMS_EPI_GELU_DROP_BWD && P.bias) x.bias = ld8b(P.bias + n);
+  const h16x4 z = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+  x.a = z;
+  x.b = z;
+  x.bias = z;
+  const bool ok = m < P.M && n < P.N;
+  if (EPI != MMS_EPI_RELU_DROP_BWD && EPI != MMS_EPI_GELU_DROP_BWD) x.bias = dp_ld8(R.bias, ok ? n * 2 : kOut);
   if (!dp_aux<EPI>()) return x;
   if (EPI == MMS_EPI_F16_ACC) {
-    x.a = ld8b(reinterpret_cast<const h16*>(P.C) + (long)m * P.ldc + n);
+    x.a = dp_ld8(R.c, ok ? (int)(((long)m * P.ldc + n) * 2) : kOut);
   } else {
-    x.a = ld8b(P.aux + (long)m * P.ldaux + n);
-    if (EPI == MMS_EPI_GATE) x.b = ld8b(P.aux + (long)m * P.ldaux + P.N + n);
+    x.a = dp_ld8(R.aux, ok ? (int)(((long)m * P.ldaux + n) * 2) : kOut);
+    if (EPI == MMS_EPI_GATE) x.b = dp_ld8(R.aux, ok ? (int)(((long)m * P.ldaux + P.N + n) * 2) : kOut);
   }
   return x;
 }
 
 // staged_epilogue's per-element arithmetic (fast path) on 4 consecutive columns
+// The stores are raw buffer stores issued by every wave unconditionally -- an out-of-range element
+// gets an offset past the descriptor's extent and is dropped by the range check -- so each k-step
+// issues exactly dp_nstores<EPI>() of them per wave, the youngest vector-memory operations of the
+// k-step.  vmcnt retires in issue order, so the next k-step's wait for its DMA stage and aux loads
+// is vmcnt(dp_nstores) and leaves these stores in flight (a vmcnt(0) there would put the C-store
+// latency in front of every deferred-epilogue k-step).
 template <int EPI>
-MMS_DEV void dp_store(const GemmP& P, int m, int n, const f32x4& v, const DpAux& ax, uint32_t hmix,
-                      bool same_hi, float dscale) {
-  if (m >= P.M || n >= P.N) return;
+constexpr int dp_nstores() {
+  return DP_PIECES * ((EPI == MMS_EPI_GATE || EPI == MMS_EPI_GELU_DROP) ? 2 : 1);
+}
+template <int EPI>
+MMS_DEV void dp_store(const GemmP& P, const DpRes& R, bool live, int m, int n, const f32x4& v, const DpAux& ax,
+                      uint32_t hmix, bool same_hi, float dscale) {
+  const bool ok = live && m < P.M && n < P.N;
   float bv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) bv[e] = (float)ax.bias[e];
@@ -75,7 +104,6 @@ MMS_DEV void dp_store(const GemmP& P, int m, int n, const f32x4& v, const DpAux&
     else mms_keep4(P.seed, c0, P.thresh, keep);
   }
   h16x4 o4;
-  h16* C = reinterpret_cast<h16*>(P.C) + (long)m * P.ldc + n;
   if (EPI == MMS_EPI_GATE) {
     h16x4 g4;
 #pragma unroll
@@ -84,7 +112,7 @@ MMS_DEV void dp_store(const GemmP& P, int m, int n, const f32x4& v, const DpAux&
       g4[e] = (h16)g;
       o4[e] = (h16)(tv + g * (ov - tv));
     }
-    *reinterpret_cast<h16x4*>(P.out2 + (long)m * P.ldo2 + n) = g4;
+    dp_st8(R.o2, ok ? (int)(((long)m * P.ldo2 + n) * 2) : kOut, g4);
   } else if (EPI == MMS_EPI_GELU_DROP) {
     h16x4 z4;
 #pragma unroll
@@ -92,7 +120,7 @@ MMS_DEV void dp_store(const GemmP& P, int m, int n, const f32x4& v, const DpAux&
       z4[e] = (h16)x[e];
       o4[e] = (h16)(keep[e] ? gelu_((float)z4[e]) * dscale : 0.f);
     }
-    *reinterpret_cast<h16x4*>(P.out2 + (long)m * P.ldo2 + n) = z4;
+    dp_st8(R.o2, ok ? (int)(((long)m * P.ldo2 + n) * 2) : kOut, z4);
   } else if (EPI == MMS_EPI_GELU_DROP_BWD) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) o4[e] = (h16)(keep[e] ? x[e] * dscale * gelu_grad_((float)ax.a[e]) : 0.f);
@@ -108,7 +136,7 @@ MMS_DEV void dp_store(const GemmP& P, int m, int n, const f32x4& v, const DpAux&
       o4[e] = (h16)o;
     }
   }
-  *reinterpret_cast<h16x4*>(C) = o4;
+  dp_st8(R.c, ok ? (int)(((long)m * P.ldc + n) * 2) : kOut, o4);
 }
 
 // XCD-local tile walk: the XCD's contiguous share of the tile space (tile_coords' bijective split),
@@ -154,6 +182,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
       (void*)P.A, (short)0, (int)(((long)(P.M - 1) * P.lda + P.K) * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)P.B, (short)0, (int)(((long)(P.N - 1) * P.ldb + P.K) * 2), 0x00020000);
+  DpRes R;
+  R.c = dp_rsrc(P.C, ((long)(P.M - 1) * P.ldc + P.N) * 2);
+  R.o2 = dp_rsrc(P.out2, ((long)(P.M - 1) * P.ldo2 + P.N) * 2);
+  R.aux = dp_rsrc(P.aux, ((long)(P.M - 1) * P.ldaux + (EPI == MMS_EPI_GATE ? 2 : 1) * P.N) * 2);
+  R.bias = dp_rsrc(P.bias, (long)P.N * 2);
   const int nk = P.K / BK;   // host: K % 64 == 0, K > 0
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
@@ -168,6 +201,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 
   // the previous tile's accumulators and its epilogue state
   f32x4 prev[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) prev[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int pm0 = 0, pn0 = 0;   // lane's first row / column of the previous tile
   bool have_prev = false;
   uint32_t hmix = 0;
@@ -175,20 +212,29 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
   // operands of the fragments finished in k-step e live in pa[e & 1]: the next k-step's are loaded
   // while this one's are consumed
   DpAux pa[2][DP_PIECES];
+  {
+    const h16x4 z = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int u = 0; u < DP_PIECES; ++u) pa[b][u] = DpAux{z, z, z};
+  }
   // fragment p = 4 i + j of the previous tile (p compile-time after unrolling)
   auto load_pieces = [&](int p0) {
     DpAux* dst = pa[(p0 / DP_PIECES) & 1];
 #pragma unroll
     for (int u = 0; u < DP_PIECES; ++u)
-      if (p0 + u < 16) dst[u] = dp_load<EPI>(P, pm0 + ((p0 + u) >> 2) * 16, pn0 + ((p0 + u) & 3) * 16);
+      if (p0 + u < 16) dst[u] = dp_load<EPI>(P, R, pm0 + ((p0 + u) >> 2) * 16, pn0 + ((p0 + u) & 3) * 16);
   };
+  // (issued whether or not there is a previous tile: exactly dp_nstores stores per call)
   auto store_pieces = [&](int p0) {
     const DpAux* src = pa[(p0 / DP_PIECES) & 1];
 #pragma unroll
     for (int u = 0; u < DP_PIECES; ++u) {
       const int p = p0 + u;
       if (p < 16)
-        dp_store<EPI>(P, pm0 + (p >> 2) * 16, pn0 + (p & 3) * 16, prev[p >> 2][p & 3], src[u], hmix, same_hi, dscale);
+        dp_store<EPI>(P, R, have_prev, pm0 + (p >> 2) * 16, pn0 + (p & 3) * 16, prev[p >> 2][p & 3], src[u],
+                      hmix, same_hi, dscale);
     }
   };
 
@@ -203,14 +249,16 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (have_prev) load_pieces(0);
-    // one k-step; EP >= 0: also finish the previous tile's fragments EP*DP_PIECES.. (EP compile-time)
+    // one k-step; EP >= 0: also finish the previous tile's fragments EP*DP_PIECES.. (EP compile-time).
+    // The previous k-step issued, in order, stage kt's DMA, the aux loads of this step's fragments
+    // and (EP >= 1) its own fragments' stores: waiting for all but those stores retires the first
+    // two.  The builtin form of the wait (not inline asm) tells the compiler's waitcnt pass what is
+    // retired, so it adds no wait of its own in front of the aux operands' use below.
     auto kstep = [&](int kt, auto ep) {
       constexpr int EP = decltype(ep)::value;
-      // stage kt (and every aux load / store issued in the previous k-step) has landed.  The
-      // builtin form of the wait (not inline asm) tells the compiler's waitcnt pass that those
-      // loads are retired, so it adds no wait of its own in front of their use below, behind the
-      // next stage's DMA
-      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      constexpr int WS = EP >= 1 ? dp_nstores<EPI>() : 0;
+      static_assert(WS < 16, "vmcnt field");
+      __builtin_amdgcn_s_waitcnt(0x0F70 | WS);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const int cur = (kbase + kt) & 1;
@@ -221,7 +269,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
         dma_tile<true>(ra, SA(cur ^ 1), P.lda, ntm * BM, 0, wid, lane);
         dma_tile<true>(rb, SB(cur ^ 1), P.ldb, ntn * BN, 0, wid, lane);
       }
-      if (EP >= 0 && have_prev && (EP + 1) * DP_PIECES < 16 && kt + 1 < nk) load_pieces((EP + 1) * DP_PIECES);
+      if (EP >= 0 && EP < NP_ && have_prev && (EP + 1) * DP_PIECES < 16 && kt + 1 < nk) load_pieces((EP + 1) * DP_PIECES);
       h16x8 fa2[2][4], fb2[2][4];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -230,7 +278,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<true>(SB(cur), wn * 64 + j * 16, kk, lane);
       }
-      if (EP >= 0 && have_prev) store_pieces(EP * DP_PIECES);
+      if (EP >= 0 && EP < NP_) store_pieces(EP * DP_PIECES);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -239,11 +287,12 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb2[kk][j], fa2[kk][i], acc[i][j], 0, 0, 0);
     };
-    constexpr int NP = 16 / DP_PIECES;   // k-steps that carry deferred fragments
-    unroll_ksteps<0, NP>(nk, kstep);
-    for (int kt = NP; kt < nk; ++kt) kstep(kt, std::integral_constant<int, -1>{});
+    // k-steps 0 .. NP_-1 carry deferred fragments; step NP_ (no fragments) still waits behind the
+    // previous step's stores; the rest wait for everything (EP = -1)
+    unroll_ksteps<0, NP_ + 1>(nk, kstep);
+    for (int kt = NP_ + 1; kt < nk; ++kt) kstep(kt, std::integral_constant<int, -1>{});
     // a tile shorter than NP k-steps: finish the previous tile's remaining fragments now
-    if (have_prev && nk < NP) {
+    if (have_prev && nk < NP_) {
       __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
       for (int p0 = 0; p0 < 16; p0 += DP_PIECES) {

@@ -283,7 +283,6 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
                                                        uint32_t thresh, uint64_t seed, uint64_t offset,
                                                        long dgrp, long dgrp_out, float pin, uint32_t thin,
                                                        uint64_t sin, uint64_t oin, int iters) {
-  constexpr int NR = 1;   // rows in flight per wave
   if (thresh) seed = mms_step_seed(seed);
   if (thin) sin = mms_step_seed(sin);
   __shared__ __attribute__((aligned(16))) float red[4][2][C * 256];
@@ -298,104 +297,106 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
     for (int e = 0; e < 4; ++e) { gam[c][e] = (float)gg[e]; dg[c][e] = 0.f; db[c][e] = 0.f; }
   }
   const h16x4 z4 = {(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
-#pragma unroll 1
-  for (int it = 0; it < iters * (2 / NR); ++it) {
-    const long rb = ((long)blockIdx.x * iters + it / (2 / NR)) * 8 + (it % (2 / NR));
-    if (rb >= rows) break;
-    h16x4 xv[NR][C], dv[NR][C], rv[NR][C];
-    float mu[NR], rs[NR];
-    long row[NR];
+  // one row's operands (x, dy, dres quads, mean, rstd); iteration `it` of this wave is row
+  // (block * iters + it / 2) * 8 + 2 w + it % 2
+  struct RowIn {
+    h16x4 xv[C], dv[C], rv[C];
+    float mu, rs;
+  };
+  auto row_of = [&](int it) { return ((long)blockIdx.x * iters + it / 2) * 8 + (it % 2) + 2 * w; };
+  auto load_row = [&](int it, RowIn& r) {
+    const long row = row_of(it);
+    const bool ok = it < 2 * iters && row < rows;
+    r.mu = ok ? mean[row] : 0.f;
+    r.rs = ok ? rstd[row] : 0.f;
+    // (32-bit row arithmetic: the host guarantees rows * D < 2^31)
+    const int r32 = (int)row, g32 = (int)dgrp;
+    const int drow = g32 ? (r32 / g32) * (int)dgrp_out + r32 % g32 : r32;
+    const h16* xr = x + (long)(r32 * D + lane * 4);
+    const h16* dr = dy + (long)(drow * D + lane * 4);
+    const h16* rr = dres + (long)(r32 * D + lane * 4);
 #pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      row[k] = rb + 2 * w + k;   // NR = 1: rb carries the row's parity
-      const bool ok = row[k] < rows;
-      mu[k] = ok ? mean[row[k]] : 0.f;
-      rs[k] = ok ? rstd[row[k]] : 0.f;
-      // (32-bit row arithmetic: the host guarantees rows * D < 2^31)
-      const int r32 = (int)row[k], g32 = (int)dgrp;
-      const int drow = g32 ? (r32 / g32) * (int)dgrp_out + r32 % g32 : r32;
-      const h16* xr = x + (long)(r32 * D + lane * 4);
-      const h16* dr = dy + (long)(drow * D + lane * 4);
-      const h16* rr = dres + (long)(r32 * D + lane * 4);
-#pragma unroll
-      for (int c = 0; c < C; ++c) {
-        xv[k][c] = ok ? ld4(xr + 256 * c) : z4;
-        dv[k][c] = ok ? ld4(dr + 256 * c) : z4;
-        rv[k][c] = (ok && dres && dx) ? ld4(rr + 256 * c) : z4;
-      }
+    for (int c = 0; c < C; ++c) {
+      r.xv[c] = ok ? ld4(xr + 256 * c) : z4;
+      r.dv[c] = ok ? ld4(dr + 256 * c) : z4;
+      r.rv[c] = (ok && dres && dx) ? ld4(rr + 256 * c) : z4;
     }
+  };
+  // MMS_LN_BWD_PREFETCH: the next row's loads are issued before this row's arithmetic (two rows of
+  // operands in flight per wave)
+#ifndef MMS_LN_BWD_PREFETCH
+#define MMS_LN_BWD_PREFETCH 0
+#endif
+  RowIn cur;
+  if (MMS_LN_BWD_PREFETCH) load_row(0, cur);
+#pragma unroll 1
+  for (int it = 0; it < iters * 2; ++it) {
+    const long row = row_of(it);
+    if (row - 2 * w >= rows) break;   // (the group's first row: every wave leaves together)
+    if (!MMS_LN_BWD_PREFETCH) load_row(it, cur);
+    RowIn nxt;
+    if (MMS_LN_BWD_PREFETCH) load_row(it + 1, nxt);
+    const float mu = cur.mu, rs = cur.rs;
     if (thin) {
       // dy = dropout(dy_in) with the counters of the unpadded element index, rounded to fp16 as a
       // separate dropout pass would store it
       const float dsi = 1.f / (1.f - pin);
 #pragma unroll
-      for (int k = 0; k < NR; ++k)
+      for (int c = 0; c < C; ++c) {
+        bool kp[4];
+        mms_keep4(sin, oin + (uint64_t)((int)row * D + (lane + 64 * c) * 4), thin, kp);
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-          bool kp[4];
-          mms_keep4(sin, oin + (uint64_t)((int)row[k] * D + (lane + 64 * c) * 4), thin, kp);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dv[k][c][e] = (h16)(kp[e] ? (float)dv[k][c][e] * dsi : 0.f);
-        }
+        for (int e = 0; e < 4; ++e) cur.dv[c][e] = (h16)(kp[e] ? (float)cur.dv[c][e] * dsi : 0.f);
+      }
     }
-    float s1[NR], s2[NR];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      s1[k] = 0.f;
-      s2[k] = 0.f;
+    for (int c = 0; c < C; ++c)
 #pragma unroll
-      for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
-          const float d = (float)dv[k][c][e];
-          const float gd = d * gam[c][e];
-          s1[k] += gd * xh;
-          s2[k] += gd;
-          dg[c][e] += d * xh;
-          db[c][e] += d;
-        }
-    }
-    if (!dx) continue;
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      s1[k] = wave_sum(s1[k]) * invD;
-      s2[k] = wave_sum(s2[k]) * invD;
-    }
-    // re-derive x-hat and dy from the fp16 quads below instead of keeping the first pass's fp32
-    // copies alive across the reductions (they would double the per-row registers)
-#pragma unroll
-    for (int k = 0; k < NR; ++k)
+      for (int e = 0; e < 4; ++e) {
+        const float xh = ((float)cur.xv[c][e] - mu) * rs;
+        const float d = (float)cur.dv[c][e];
+        const float gd = d * gam[c][e];
+        s1 += gd * xh;
+        s2 += gd;
+        dg[c][e] += d * xh;
+        db[c][e] += d;
+      }
+    if (dx) {
+      s1 = wave_sum(s1) * invD;
+      s2 = wave_sum(s2) * invD;
+      // re-derive x-hat and dy from the fp16 quads below instead of keeping the first pass's fp32
+      // copies alive across the reductions (they would double the per-row registers)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         typedef unsigned int u32x2_ __attribute__((ext_vector_type(2)));
-        u32x2_ a = __builtin_bit_cast(u32x2_, xv[k][c]), b = __builtin_bit_cast(u32x2_, dv[k][c]);
+        u32x2_ a = __builtin_bit_cast(u32x2_, cur.xv[c]), b = __builtin_bit_cast(u32x2_, cur.dv[c]);
         asm volatile("" : "+v"(a), "+v"(b));
-        xv[k][c] = __builtin_bit_cast(h16x4, a);
-        dv[k][c] = __builtin_bit_cast(h16x4, b);
+        cur.xv[c] = __builtin_bit_cast(h16x4, a);
+        cur.dv[c] = __builtin_bit_cast(h16x4, b);
       }
+      if (row < rows) {
+        const int off0 = (int)row * D + lane * 4;
 #pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      if (row[k] >= rows) continue;
-      const int off0 = (int)row[k] * D + lane * 4;
+        for (int c = 0; c < C; ++c) {
+          const int off = off0 + 256 * c;
+          float o[4];
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        const int off = off0 + 256 * c;
-        float o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xh = ((float)xv[k][c][e] - mu[k]) * rs[k];
-          o[e] = rs[k] * ((float)dv[k][c][e] * gam[c][e] - xh * s1[k] - s2[k]) + (float)rv[k][c][e];
-        }
-        st4(dx + (long)off0 + 256 * c, o[0], o[1], o[2], o[3]);
-        if (dxd) {
-          bool kp[4] = {true, true, true, true};
-          if (thresh) mms_keep4(seed, offset + (uint64_t)off, thresh, kp);
-          st4(dxd + (long)off0 + 256 * c, kp[0] ? o[0] * dscale : 0.f, kp[1] ? o[1] * dscale : 0.f, kp[2] ? o[2] * dscale : 0.f,
-              kp[3] ? o[3] * dscale : 0.f);
+          for (int e = 0; e < 4; ++e) {
+            const float xh = ((float)cur.xv[c][e] - mu) * rs;
+            o[e] = rs * ((float)cur.dv[c][e] * gam[c][e] - xh * s1 - s2) + (float)cur.rv[c][e];
+          }
+          st4(dx + (long)off, o[0], o[1], o[2], o[3]);
+          if (dxd) {
+            bool kp[4] = {true, true, true, true};
+            if (thresh) mms_keep4(seed, offset + (uint64_t)off, thresh, kp);
+            st4(dxd + (long)off, kp[0] ? o[0] * dscale : 0.f, kp[1] ? o[1] * dscale : 0.f, kp[2] ? o[2] * dscale : 0.f,
+                kp[3] ? o[3] * dscale : 0.f);
+          }
         }
       }
     }
+    if (MMS_LN_BWD_PREFETCH) cur = nxt;
   }
 #pragma unroll
   for (int c = 0; c < C; ++c)
@@ -984,8 +985,11 @@ extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
 // groups of 8 rows per ln_bwd_w block: enough blocks to fill the chip (1024), each folding its
 // groups' dgamma / dbeta into one partial row — the partials (rows / 8 x 6 KB at D = 768 before
 // the folding) are what colsum_parts reads back on the side stream
+#ifndef MMS_LN_BWD_GROUPS
+#define MMS_LN_BWD_GROUPS 1024
+#endif
 static int ln16_iters(int64_t rows) {
-  constexpr long target = 1024;
+  constexpr long target = MMS_LN_BWD_GROUPS;
   const long groups = (rows + 7) / 8;
   const long it = (groups + target - 1) / target;
   return (int)(it > 1 ? it : 1);

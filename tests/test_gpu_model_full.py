@@ -61,7 +61,8 @@ def test_full_base_audio_only_dropout_replay(mm):
     tlens = [round(0.3 * L) + 1 for L in lengths]
     r = run_model_pair(mm, cfg, lengths, tlens, with_images=False, seed=23)
     print(report(r))
-    assert r.Te == 250 and r.n_masks == 1 + 12 * 4 + 6 * 6
+    # encoder embed + 12 x (attn probs, drop1, act, drop2) + decoder embed + 6 x 6 (no fusion sites)
+    assert r.Te == 250 and r.n_masks == 1 + 12 * 4 + 1 + 6 * 6
     check_outputs(r)
     check_relu_replay(r)
     _assert_grads(r)
