@@ -890,17 +890,29 @@ extern "C" int mms2ut_gemm_set_pp(int mode) {
 }
 
 // Persistent deferred-epilogue kernel (gemm_dp.hip) for NT grids of more than one round of the
-// 512 block slots.  1 on, 0 off (default until it measures faster; mms2ut_gemm_set_dp / MMS2UT_GEMM_DP).
+// 512 block slots (mms2ut_gemm_set_dp / MMS2UT_GEMM_DP).  Default 3 = the short-K (K < 1536) wide
+// shapes only: step 17.29-17.32 ms against 17.43-17.48 for the one-tile-per-block kernel, and
+// 17.25-17.32 with every qualifying shape (the long-K N = 768 shapes alone: 17.55-17.57) --
+// round-4 A/B, gpurun_out r4o, three interleaved reps (profiles/round4_dp_ab.txt).
 static int g_dp_mode = -1;
 static int dp_mode() {
   if (g_dp_mode < 0) {
     const char* e = getenv("MMS2UT_GEMM_DP");
-    g_dp_mode = e ? atoi(e) : 0;
+    g_dp_mode = e ? atoi(e) : 3;
   }
   return g_dp_mode;
 }
+// mode 2: only K >= 1536 (the long-K, N = 768 projections); mode 3: only K < 1536
+static bool dp_route(const mms2ut_gemm_args* a) {
+  switch (dp_mode()) {
+    case 1: return true;
+    case 2: return a->K >= 1536;
+    case 3: return a->K < 1536;
+    default: return false;
+  }
+}
 extern "C" int mms2ut_gemm_set_dp(int mode) {
-  MMS_REQUIRE(mode == 0 || mode == 1, "gemm_set_dp: mode must be 0 or 1 (got %d)", mode);
+  MMS_REQUIRE(mode >= 0 && mode <= 3, "gemm_set_dp: mode must be 0..3 (got %d)", mode);
   g_dp_mode = mode;
   return 0;
 }
@@ -1040,7 +1052,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   // (the deferred epilogue addresses C / aux / out2 through buffer descriptors: 31-bit extents)
   const long ep_ext = 2 * ((long)(a->M - 1) * std::max<long>({(long)a->ldc, (long)a->ldaux, (long)a->ldo2}) + 2L * a->N);
   if (dma_ok && a_kc && b_kc && nz == 1 && a->epi != MMS_EPI_F32 && P.vec16 && a->N % 4 == 0 &&
-      (long)tm * tn > 512 && ep_ext < (1L << 31) && dp_mode()) {
+      (long)tm * tn > 512 && ep_ext < (1L << 31) && dp_route(a)) {
     const int grid = 512;   // two blocks per CU, each walking its XCD's tiles
     P.stamps = stamp_take(grid);
     return mmsg::launch_dp(a->epi, P, tm, tn, grid, s);

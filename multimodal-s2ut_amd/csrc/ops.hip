@@ -322,20 +322,15 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
       r.rv[c] = (ok && dres && dx) ? ld4(rr + 256 * c) : z4;
     }
   };
-  // MMS_LN_BWD_PREFETCH: the next row's loads are issued before this row's arithmetic (two rows of
-  // operands in flight per wave)
-#ifndef MMS_LN_BWD_PREFETCH
-#define MMS_LN_BWD_PREFETCH 0
-#endif
+  // (loading the next row before this row's arithmetic -- two rows in flight, 140 VGPRs, 3 waves per
+  // SIMD -- and twice the blocks (2048 row groups) both measured no faster: round-4 A/B,
+  // gpurun_out r4n ln_ab, 26.2 vs 26.9 / 28.6 us isolated, step 17.24 vs 17.28 / 17.20 ms)
   RowIn cur;
-  if (MMS_LN_BWD_PREFETCH) load_row(0, cur);
 #pragma unroll 1
   for (int it = 0; it < iters * 2; ++it) {
     const long row = row_of(it);
     if (row - 2 * w >= rows) break;   // (the group's first row: every wave leaves together)
-    if (!MMS_LN_BWD_PREFETCH) load_row(it, cur);
-    RowIn nxt;
-    if (MMS_LN_BWD_PREFETCH) load_row(it + 1, nxt);
+    load_row(it, cur);
     const float mu = cur.mu, rs = cur.rs;
     if (thin) {
       // dy = dropout(dy_in) with the counters of the unpadded element index, rounded to fp16 as a
@@ -396,7 +391,6 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
         }
       }
     }
-    if (MMS_LN_BWD_PREFETCH) cur = nxt;
   }
 #pragma unroll
   for (int c = 0; c < C; ++c)
@@ -985,11 +979,8 @@ extern "C" int mms2ut_layernorm_bwd_parts(int64_t rows) {
 // groups of 8 rows per ln_bwd_w block: enough blocks to fill the chip (1024), each folding its
 // groups' dgamma / dbeta into one partial row — the partials (rows / 8 x 6 KB at D = 768 before
 // the folding) are what colsum_parts reads back on the side stream
-#ifndef MMS_LN_BWD_GROUPS
-#define MMS_LN_BWD_GROUPS 1024
-#endif
 static int ln16_iters(int64_t rows) {
-  constexpr long target = MMS_LN_BWD_GROUPS;
+  constexpr long target = 1024;
   const long groups = (rows + 7) / 8;
   const long it = (groups + target - 1) / target;
   return (int)(it > 1 ? it : 1);
