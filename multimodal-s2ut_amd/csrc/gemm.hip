@@ -784,7 +784,15 @@ static int wgrad_group_dispatch(const mms2ut_wgrad* w, int n, int64_t rows, int 
   int grid = total;
   if (max_blocks > 0 && max_blocks < total) grid = std::max(8, max_blocks / 8 * 8);
   G.stamps = stamp_take(grid);
-  hipLaunchKernelGGL(gemm_group_wgrad_kernel, dim3(grid), dim3(NT), 0, stream, G, total);
+  // A/B switch MMS2UT_WGRAD_LDS: extra dynamic LDS per block of the grouped launch (bytes), e.g.
+  // 32768 -> 96 KiB per block: at most one weight-gradient block per CU, the other slot left to
+  // the critical path's 64 KiB GEMM blocks
+  static int extra_lds = -1;
+  if (extra_lds < 0) {
+    const char* e = getenv("MMS2UT_WGRAD_LDS");
+    extra_lds = e ? std::max(0, std::min(atoi(e), 160 * 1024 - 4 * TILE_BYTES)) : 0;
+  }
+  hipLaunchKernelGGL(gemm_group_wgrad_kernel, dim3(grid), dim3(NT), extra_lds, stream, G, total);
   return mms::check_launch("gemm_group_wgrad");
 }
 
