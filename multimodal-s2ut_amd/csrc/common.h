@@ -35,21 +35,11 @@ int check_launch(const char* what);
 // ------------------------------------------------------------------------------------------
 // 32-bit integer mixer (lowbias32: two 32-bit multiplies) — cheap enough for GEMM epilogues.
 MMS_DEV uint32_t mms_mix32(uint32_t x) {
-#ifdef MMS_MIX24
-  // full-rate form: the two multiplies on the low 24 bits (v_mul_u32_u24); every input bit still
-  // reaches the product through the preceding xor-shift (avalanche 0.50 +- 0.004 per input bit)
-  x ^= x >> 16;
-  x = __umul24(x, 0x9e3779U);
-  x ^= x >> 15;
-  x = __umul24(x, 0x85ebcbU);
-  x ^= x >> 16;
-#else
   x ^= x >> 16;
   x *= 0x7feb352dU;
   x ^= x >> 15;
   x *= 0x846ca68bU;
   x ^= x >> 16;
-#endif
   return x;
 }
 // one 32-bit draw per PAIR of counters (ctr>>1); element ctr takes the low/high 16 bits.

@@ -784,15 +784,7 @@ static int wgrad_group_dispatch(const mms2ut_wgrad* w, int n, int64_t rows, int 
   int grid = total;
   if (max_blocks > 0 && max_blocks < total) grid = std::max(8, max_blocks / 8 * 8);
   G.stamps = stamp_take(grid);
-  // A/B switch MMS2UT_WGRAD_LDS: extra dynamic LDS per block of the grouped launch (bytes), e.g.
-  // 32768 -> 96 KiB per block: at most one weight-gradient block per CU, the other slot left to
-  // the critical path's 64 KiB GEMM blocks
-  static int extra_lds = -1;
-  if (extra_lds < 0) {
-    const char* e = getenv("MMS2UT_WGRAD_LDS");
-    extra_lds = e ? std::max(0, std::min(atoi(e), 160 * 1024 - 4 * TILE_BYTES)) : 0;
-  }
-  hipLaunchKernelGGL(gemm_group_wgrad_kernel, dim3(grid), dim3(NT), extra_lds, stream, G, total);
+  hipLaunchKernelGGL(gemm_group_wgrad_kernel, dim3(grid), dim3(NT), 0, stream, G, total);
   return mms::check_launch("gemm_group_wgrad");
 }
 
@@ -1060,7 +1052,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   // (the deferred epilogue addresses C / aux / out2 through buffer descriptors: 31-bit extents)
   const long ep_ext = 2 * ((long)(a->M - 1) * std::max<long>({(long)a->ldc, (long)a->ldaux, (long)a->ldo2}) + 2L * a->N);
   if (dma_ok && a_kc && b_kc && nz == 1 && a->epi != MMS_EPI_F32 && P.vec16 && a->N % 4 == 0 &&
-      (long)tm * tn > 512 && ep_ext < (1L << 31) && dp_route(a)) {
+      (long)tm * tn > 512 && a->K >= 10 * BK && ep_ext < (1L << 31) && dp_route(a)) {
     const int grid = 512;   // two blocks per CU, each walking its XCD's tiles
     P.stamps = stamp_take(grid);
     return mmsg::launch_dp(a->epi, P, tm, tn, grid, s);

@@ -16,6 +16,7 @@
 // XOR-swizzled images, mfma_f32_16x16x32_f16 with (B, A) swapped) and the epilogue arithmetic is
 // staged_epilogue's element for element, so results are bit-identical to gemm_dma_kernel
 // (tests/test_gpu_gemm_splitk.py::test_dp_gemm_bit_identical).
+#include <atomic>
 #include <utility>
 
 #include "gemm_common.h"
@@ -139,40 +140,83 @@ MMS_DEV void dp_store(const GemmP& P, const DpRes& R, bool live, int m, int n, c
   dp_st8(R.c, ok ? (int)(((long)m * P.ldc + n) * 2) : kOut, o4);
 }
 
-// XCD-local tile walk: the XCD's contiguous share of the tile space (tile_coords' bijective split),
-// block j of the XCD takes local tiles j, j + gx, j + 2 gx, ...; local ids follow tile_coords'
-// grouped order (GROUP_M tile-rows, column by column)
-MMS_DEV bool dp_tile(int seq, int tiles_m, int tiles_n, int total, int group_m, int& tm, int& tn) {
-  const int x = blockIdx.x % 8, j = blockIdx.x / 8, gx = gridDim.x / 8;
-  const int q = total / 8, r = total % 8;
-  const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  const int len = q + (x < r ? 1 : 0);
-  const int loc = j + seq * gx;
-  if (loc >= len) return false;
-  const int t = start + loc;
+// XCD-local tile queue: the XCD's contiguous share of the tile space (tile_coords' bijective split)
+// is handed out by an atomic ticket counter, one per XCD and launch slot, so a block that starts
+// late (its CU held by the side stream's weight gradients) takes fewer tiles instead of delaying
+// the launch by a fixed share.  Local ids follow tile_coords' grouped order (GROUP_M tile-rows,
+// column by column).  Every block draws exactly one ticket past the end; the block drawing the
+// last of those (len + blocks of the XCD - 1) resets the counter for the slot's next launch.
+constexpr int DP_SLOTS = 64;
+__device__ int g_dp_tickets[DP_SLOTS * 8 * 32];   // one counter per 128-B line
+
+struct DpQueue {
+  int* ctr;
+  int start, len, gx;
+};
+MMS_DEV DpQueue dp_queue(int total, int slot) {
+  const int x = blockIdx.x % 8, q = total / 8, r = total % 8;
+  DpQueue Q;
+  Q.ctr = g_dp_tickets + (slot * 8 + x) * 32;
+  Q.start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  Q.len = q + (x < r ? 1 : 0);
+  Q.gx = gridDim.x / 8 + ((int)(gridDim.x % 8) > x ? 1 : 0);   // blocks on this XCD's queue
+  return Q;
+}
+// The ticket traffic is inline asm, invisible to the compiler's waitcnt pass: as builtins, the
+// atomic optimizer turned the one-lane draw into a wave-aggregated atomic whose result it consumed
+// at once (vmcnt(0) in front of the k-step's DMA), and the ticket's LDS word made every fragment
+// read wait for the in-flight DMA stage.  The draw is issued before a k-step's DMA and retired by
+// the next k-step's counted wait (it is older than every operation that wait leaves in flight);
+// dp_sync re-defines its result after that wait so no use can be scheduled above it.
+MMS_DEV int dp_draw(const DpQueue& Q) {
+  int t;
+  const int one = 1;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(t) : "v"(Q.ctr), "v"(one) : "memory");
+  return t;
+}
+MMS_DEV void dp_sync(int& t) { asm volatile("" : "+v"(t)); }
+MMS_DEV void dp_retire(const DpQueue& Q, int t) {   // after every draw, once its value is back
+  if (t == Q.len + Q.gx - 1) {
+    const int zero = 0;
+    asm volatile("global_atomic_swap %0, %1, off" :: "v"(Q.ctr), "v"(zero) : "memory");
+  }
+}
+MMS_DEV void dp_put(char* lds, int t) {
+  asm volatile("ds_write_b32 %0, %1" :: "v"((unsigned)(uintptr_t)lds), "v"(t) : "memory");
+}
+MMS_DEV int dp_get(const char* lds) {
+  int t;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"((unsigned)(uintptr_t)lds) : "memory");
+  return t;
+}
+MMS_DEV bool dp_tile(const DpQueue& Q, int ticket, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  if (ticket >= Q.len) return false;
+  const int t = Q.start + ticket;
   const int per_group = group_m * tiles_n;
   const int g = t / per_group, first_m = g * group_m;
   const int gsize = min(tiles_m - first_m, group_m);
   const int w = t % per_group;
   tm = first_m + w % gsize;
   tn = w / gsize;
-  (void)tiles_m;
   return true;
 }
 
-// k-steps 0 .. NP-1 with compile-time step numbers (they carry the deferred fragments)
+// k-steps 0 .. NP-1 with compile-time step numbers (they carry the deferred fragments), straight-
+// line: the host routes only K >= (NP_ + 2) * 64 here, so every one of them runs and DMAs the same
+// tile's next stage (a conditional step would merge wait states and cost vmcnt waits on the DMA)
 template <int U, int NP, typename F>
-MMS_DEV void unroll_ksteps(int nk, F& f) {
+MMS_DEV void unroll_ksteps(F& f) {
   if constexpr (U < NP) {
-    if (U < nk) f(U, std::integral_constant<int, U>{});
-    unroll_ksteps<U + 1, NP>(nk, f);
+    f(U, std::integral_constant<int, U>{});
+    unroll_ksteps<U + 1, NP>(f);
   }
 }
 
 template <int EPI>
-__global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+__global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, int tiles_n, int total, int slot) {
   const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES + 16];   // + the next tile's ticket
+  char* const s_ticket = smem + 2 * 2 * TILE_BYTES;
 #define SA(s) (smem + (2 * (s)) * TILE_BYTES)
 #define SB(s) (smem + (2 * (s) + 1) * TILE_BYTES)
   const int lane = threadIdx.x & 63;
@@ -187,15 +231,28 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
   R.o2 = dp_rsrc(P.out2, ((long)(P.M - 1) * P.ldo2 + P.N) * 2);
   R.aux = dp_rsrc(P.aux, ((long)(P.M - 1) * P.ldaux + (EPI == MMS_EPI_GATE ? 2 : 1) * P.N) * 2);
   R.bias = dp_rsrc(P.bias, (long)P.N * 2);
-  const int nk = P.K / BK;   // host: K % 64 == 0, K > 0
+  const int nk = P.K / BK;   // host: K % 64 == 0, nk >= NP_ + 2
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
 
+  const DpQueue Q = dp_queue(total, slot);
+  if (threadIdx.x == 0) {
+    int t = dp_draw(Q);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    dp_sync(t);
+    dp_retire(Q, t);
+    dp_put(s_ticket, t);
+  }
+  __syncthreads();
   int tm, tn;
-  if (!dp_tile(0, tiles_m, tiles_n, total, P.group_m, tm, tn)) {
+  if (!dp_tile(Q, dp_get(s_ticket), tiles_m, tiles_n, P.group_m, tm, tn)) {
     stamp_end(P.stamps, t_start);
     return;
   }
+  // the next tile's ticket: drawn by thread 0 in a tile's k-step 0 (ahead of its DMA, so the
+  // k-step-1 wait retires it with the stage), parked in LDS in k-step 1, read by every thread in
+  // the last k-step
+  int ticket_req = 0;
   dma_tile<true>(ra, SA(0), P.lda, tm * BM, 0, wid, lane);
   dma_tile<true>(rb, SB(0), P.ldb, tn * BN, 0, wid, lane);
 
@@ -239,16 +296,16 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
   };
 
   int kbase = 0;   // k-steps run so far: the ring parity carries over from tile to tile
-  for (int seq = 0;; ++seq) {
+  for (;;) {
     const int bm = tm * BM, bn = tn * BN;
     int ntm = 0, ntn = 0;
-    const bool more = dp_tile(seq + 1, tiles_m, tiles_n, total, P.group_m, ntm, ntn);
+    bool more = false;
     f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (have_prev) load_pieces(0);
+    load_pieces(0);
     // one k-step; EP >= 0: also finish the previous tile's fragments EP*DP_PIECES.. (EP compile-time).
     // The previous k-step issued, in order, stage kt's DMA, the aux loads of this step's fragments
     // and (EP >= 1) its own fragments' stores: waiting for all but those stores retires the first
@@ -262,14 +319,22 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const int cur = (kbase + kt) & 1;
-      if (kt + 1 < nk) {
+      if (EP == 0 && threadIdx.x == 0) ticket_req = dp_draw(Q);
+      if (EP == 1 && threadIdx.x == 0) {
+        dp_sync(ticket_req);
+        dp_retire(Q, ticket_req);
+        dp_put(s_ticket, ticket_req);
+      }
+      if (EP < 0 && kt == nk - 1) more = dp_tile(Q, dp_get(s_ticket), tiles_m, tiles_n, P.group_m, ntm, ntn);
+      if (EP >= 0 || kt + 1 < nk) {
         dma_tile<true>(ra, SA(cur ^ 1), P.lda, bm, (kt + 1) * BK, wid, lane);
         dma_tile<true>(rb, SB(cur ^ 1), P.ldb, bn, (kt + 1) * BK, wid, lane);
       } else if (more) {   // the next tile's first stage, behind this tile's last k-step
         dma_tile<true>(ra, SA(cur ^ 1), P.lda, ntm * BM, 0, wid, lane);
         dma_tile<true>(rb, SB(cur ^ 1), P.ldb, ntn * BN, 0, wid, lane);
       }
-      if (EP >= 0 && EP < NP_ && have_prev && (EP + 1) * DP_PIECES < 16 && kt + 1 < nk) load_pieces((EP + 1) * DP_PIECES);
+      // (issued on the first tile as well, over row / column 0: the loads stay unconditional)
+      if (EP >= 0 && EP < NP_ && (EP + 1) * DP_PIECES < 16) load_pieces((EP + 1) * DP_PIECES);
       h16x8 fa2[2][4], fb2[2][4];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -289,18 +354,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
     };
     // k-steps 0 .. NP_-1 carry deferred fragments; step NP_ (no fragments) still waits behind the
     // previous step's stores; the rest wait for everything (EP = -1)
-    unroll_ksteps<0, NP_ + 1>(nk, kstep);
+    unroll_ksteps<0, NP_ + 1>(kstep);
     for (int kt = NP_ + 1; kt < nk; ++kt) kstep(kt, std::integral_constant<int, -1>{});
-    // a tile shorter than NP k-steps: finish the previous tile's remaining fragments now
-    if (have_prev && nk < NP_) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-#pragma unroll
-      for (int p0 = 0; p0 < 16; p0 += DP_PIECES) {
-        if (p0 < DP_PIECES * nk) continue;
-        load_pieces(p0);
-        store_pieces(p0);
-      }
-    }
     kbase += nk;
     // this tile becomes the deferred one
 #pragma unroll
@@ -339,8 +394,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 namespace mmsg {
 int launch_dp(int epi, const GemmP& P, int tiles_m, int tiles_n, int grid, hipStream_t s) {
   const int total = tiles_m * tiles_n;
+  // ticket-counter slot: launches in flight at once (main and side stream) never share one
+  static std::atomic<unsigned> next_slot{0};
+  const int slot = (int)(next_slot.fetch_add(1, std::memory_order_relaxed) % DP_SLOTS);
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_dp_kernel<E>), dim3(grid), dim3(NT), 0, s, P, tiles_m, tiles_n, total); break;
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_dp_kernel<E>), dim3(grid), dim3(NT), 0, s, P, tiles_m, tiles_n, total, slot); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID) CASE(MMS_EPI_GATE)
     CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
