@@ -77,21 +77,20 @@ MMS_DEV DpAux dp_load(const GemmP& P, const DpRes& R, int m, int n) {
   return x;
 }
 
-// staged_epilogue's per-element arithmetic (fast path) on 4 consecutive columns
-// The stores are raw buffer stores issued by every wave unconditionally -- an out-of-range element
-// gets an offset past the descriptor's extent and is dropped by the range check -- so each k-step
-// issues exactly dp_nstores<EPI>() of them per wave, the youngest vector-memory operations of the
-// k-step.  vmcnt retires in issue order, so the next k-step's wait for its DMA stage and aux loads
-// is vmcnt(dp_nstores) and leaves these stores in flight (a vmcnt(0) there would put the C-store
-// latency in front of every deferred-epilogue k-step).
+// staged_epilogue's per-element arithmetic (fast path) on 4 consecutive columns; the fp16 results
+// and their byte offsets (past the extent for an element outside C: the store is dropped) wait in
+// registers for dp_commit at the top of the next k-step.
+struct DpOut {
+  h16x4 o, o2;
+  int off, off2;
+};
 template <int EPI>
-constexpr int dp_nstores() {
-  return DP_PIECES * ((EPI == MMS_EPI_GATE || EPI == MMS_EPI_GELU_DROP) ? 2 : 1);
-}
-template <int EPI>
-MMS_DEV void dp_store(const GemmP& P, const DpRes& R, bool live, int m, int n, const f32x4& v, const DpAux& ax,
-                      uint32_t hmix, bool same_hi, float dscale) {
+MMS_DEV DpOut dp_compute(const GemmP& P, bool live, int m, int n, const f32x4& v, const DpAux& ax, uint32_t hmix,
+                         bool same_hi, float dscale) {
   const bool ok = live && m < P.M && n < P.N;
+  DpOut d;
+  d.off = ok ? (int)(((long)m * P.ldc + n) * 2) : kOut;
+  d.off2 = ok ? (int)(((long)m * P.ldo2 + n) * 2) : kOut;
   float bv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) bv[e] = (float)ax.bias[e];
@@ -113,7 +112,7 @@ MMS_DEV void dp_store(const GemmP& P, const DpRes& R, bool live, int m, int n, c
       g4[e] = (h16)g;
       o4[e] = (h16)(tv + g * (ov - tv));
     }
-    dp_st8(R.o2, ok ? (int)(((long)m * P.ldo2 + n) * 2) : kOut, g4);
+    d.o2 = g4;
   } else if (EPI == MMS_EPI_GELU_DROP) {
     h16x4 z4;
 #pragma unroll
@@ -121,7 +120,7 @@ MMS_DEV void dp_store(const GemmP& P, const DpRes& R, bool live, int m, int n, c
       z4[e] = (h16)x[e];
       o4[e] = (h16)(keep[e] ? gelu_((float)z4[e]) * dscale : 0.f);
     }
-    dp_st8(R.o2, ok ? (int)(((long)m * P.ldo2 + n) * 2) : kOut, z4);
+    d.o2 = z4;
   } else if (EPI == MMS_EPI_GELU_DROP_BWD) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) o4[e] = (h16)(keep[e] ? x[e] * dscale * gelu_grad_((float)ax.a[e]) : 0.f);
@@ -137,7 +136,13 @@ MMS_DEV void dp_store(const GemmP& P, const DpRes& R, bool live, int m, int n, c
       o4[e] = (h16)o;
     }
   }
-  dp_st8(R.c, ok ? (int)(((long)m * P.ldc + n) * 2) : kOut, o4);
+  d.o = o4;
+  return d;
+}
+template <int EPI>
+MMS_DEV void dp_commit(const DpRes& R, const DpOut& d) {
+  if (EPI == MMS_EPI_GATE || EPI == MMS_EPI_GELU_DROP) dp_st8(R.o2, d.off2, d.o2);
+  dp_st8(R.c, d.off, d.o);
 }
 
 // XCD-local tile queue: the XCD's contiguous share of the tile space (tile_coords' bijective split)
@@ -249,9 +254,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
     stamp_end(P.stamps, t_start);
     return;
   }
-  // the next tile's ticket: drawn by thread 0 in a tile's k-step 0 (ahead of its DMA, so the
-  // k-step-1 wait retires it with the stage), parked in LDS in k-step 1, read by every thread in
-  // the last k-step
+  // the next tile's ticket: drawn by thread 0 in a tile's k-step 0, parked in LDS in k-step 1
+  // (behind that step's vmcnt(0)), read by every thread in the last k-step
   int ticket_req = 0;
   dma_tile<true>(ra, SA(0), P.lda, tm * BM, 0, wid, lane);
   dma_tile<true>(rb, SB(0), P.ldb, tn * BN, 0, wid, lane);
@@ -283,16 +287,21 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
     for (int u = 0; u < DP_PIECES; ++u)
       if (p0 + u < 16) dst[u] = dp_load<EPI>(P, R, pm0 + ((p0 + u) >> 2) * 16, pn0 + ((p0 + u) & 3) * 16);
   };
-  // (issued whether or not there is a previous tile: exactly dp_nstores stores per call)
-  auto store_pieces = [&](int p0) {
+  // the previous tile's fragments p0 .. p0 + DP_PIECES - 1 (also on the first tile, dropped there)
+  DpOut po[DP_PIECES];
+  auto compute_pieces = [&](int p0) {
     const DpAux* src = pa[(p0 / DP_PIECES) & 1];
 #pragma unroll
     for (int u = 0; u < DP_PIECES; ++u) {
       const int p = p0 + u;
       if (p < 16)
-        dp_store<EPI>(P, R, have_prev, pm0 + (p >> 2) * 16, pn0 + (p & 3) * 16, prev[p >> 2][p & 3], src[u],
-                      hmix, same_hi, dscale);
+        po[u] = dp_compute<EPI>(P, have_prev, pm0 + (p >> 2) * 16, pn0 + (p & 3) * 16, prev[p >> 2][p & 3], src[u],
+                                hmix, same_hi, dscale);
     }
+  };
+  auto commit_pieces = [&]() {
+#pragma unroll
+    for (int u = 0; u < DP_PIECES; ++u) dp_commit<EPI>(R, po[u]);
   };
 
   int kbase = 0;   // k-steps run so far: the ring parity carries over from tile to tile
@@ -306,19 +315,18 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     load_pieces(0);
-    // one k-step; EP >= 0: also finish the previous tile's fragments EP*DP_PIECES.. (EP compile-time).
-    // The previous k-step issued, in order, stage kt's DMA, the aux loads of this step's fragments
-    // and (EP >= 1) its own fragments' stores: waiting for all but those stores retires the first
-    // two.  The builtin form of the wait (not inline asm) tells the compiler's waitcnt pass what is
-    // retired, so it adds no wait of its own in front of the aux operands' use below.
+    // one k-step; EP >= 0: also finish the previous tile's fragments EP*DP_PIECES.. (EP compile-time):
+    // their arithmetic runs after the k-step's MFMAs are issued (beside the matrix core), their
+    // stores at the top of the next k-step together with the DMA, so both have a whole k-step to
+    // land before its vmcnt(0) (the wait makes no assumption about the order in which loads,
+    // stores and atomics retire).  Aux operands are loaded one k-step ahead of their arithmetic.
     auto kstep = [&](int kt, auto ep) {
       constexpr int EP = decltype(ep)::value;
-      constexpr int WS = EP >= 1 ? dp_nstores<EPI>() : 0;
-      static_assert(WS < 16, "vmcnt field");
-      __builtin_amdgcn_s_waitcnt(0x0F70 | WS);
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const int cur = (kbase + kt) & 1;
+      if (EP >= 1 && EP <= NP_) commit_pieces();
       if (EP == 0 && threadIdx.x == 0) ticket_req = dp_draw(Q);
       if (EP == 1 && threadIdx.x == 0) {
         dp_sync(ticket_req);
@@ -335,6 +343,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
       }
       // (issued on the first tile as well, over row / column 0: the loads stay unconditional)
       if (EP >= 0 && EP < NP_ && (EP + 1) * DP_PIECES < 16) load_pieces((EP + 1) * DP_PIECES);
+      // keep the stores / DMA / aux loads at the top: the scheduler would otherwise sink the stores
+      // behind the MFMAs and shorten the time they have before the next k-step's vmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
       h16x8 fa2[2][4], fb2[2][4];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -343,7 +354,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 #pragma unroll
         for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<true>(SB(cur), wn * 64 + j * 16, kk, lane);
       }
-      if (EP >= 0 && EP < NP_) store_pieces(EP * DP_PIECES);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -351,6 +361,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb2[kk][j], fa2[kk][i], acc[i][j], 0, 0, 0);
+      if (EP >= 0 && EP < NP_) compute_pieces(EP * DP_PIECES);
     };
     // k-steps 0 .. NP_-1 carry deferred fragments; step NP_ (no fragments) still waits behind the
     // previous step's stores; the rest wait for everything (EP = -1)
@@ -382,7 +393,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
 #pragma unroll
   for (int p0 = 0; p0 < 16; p0 += DP_PIECES) {
     load_pieces(p0);
-    store_pieces(p0);
+    compute_pieces(p0);
+    commit_pieces();
   }
 #undef SA
 #undef SB
