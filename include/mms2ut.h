@@ -24,6 +24,10 @@ typedef _Float16 mms2ut_half;
 
 /* ---------------------------------------------------------------- errors / introspection */
 const char* mms2ut_last_error(void);
+/* A non-blocking HIP stream (hipStreamNonBlocking) at a priority clamped to the device's range
+ * (lower = more urgent): the trainer's critical-path and weight-gradient side streams, so that no
+ * work a caller leaves on the legacy NULL stream implicitly orders itself behind them.           */
+int mms2ut_stream_create(int priority, hipStream_t* out);
 int mms2ut_version(void);
 
 /* ---------------------------------------------------------------- GEMM (MFMA fp16, fp32 acc)

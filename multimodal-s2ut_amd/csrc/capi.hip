@@ -28,6 +28,25 @@ int check_launch(const char* what) {
 extern "C" const char* mms2ut_last_error(void) { return mms::g_err; }
 extern "C" int mms2ut_version(void) { return 1; }
 
+// A non-blocking stream at a clamped priority (lower = more urgent).  The step's own streams are
+// created here so that no work on the legacy default stream implicitly waits for them (a stream
+// created without hipStreamNonBlocking synchronises with the NULL stream in both directions).
+extern "C" int mms2ut_stream_create(int priority, hipStream_t* out) {
+  if (!out) {
+    mms::set_error("stream_create: null out");
+    return 1;
+  }
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+  const int p = priority < greatest ? greatest : (priority > least ? least : priority);
+  const hipError_t e = hipStreamCreateWithPriority(out, hipStreamNonBlocking, p);
+  if (e != hipSuccess) {
+    mms::set_error("stream_create: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}
+
 namespace {
 __global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int nsplit, long slab,
                                      int rows, int cols, void* out, long ldo, int out_f16,

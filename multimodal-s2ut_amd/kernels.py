@@ -5,6 +5,7 @@ Tensors are fp16 (``torch.float16``) unless stated; shapes are checked before th
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -625,10 +626,20 @@ class _SideRegion:
 _SIDE_REGION = _SideRegion()
 
 
+def make_stream(device, priority):
+    """A non-blocking stream (include/mms2ut.h mms2ut_stream_create) wrapped for torch: work a
+    caller leaves on the legacy NULL stream does not implicitly wait for it (measured equal to
+    torch's pool streams in the bench, 17.05 vs 17.01-17.08 ms, round 4)."""
+    with torch.cuda.device(device):
+        h = ctypes.c_void_p()
+        call("mms2ut_stream_create", int(priority), ctypes.addressof(h))
+        return torch.cuda.ExternalStream(h.value, device=device)
+
+
 def make_side_stream(device):
     """The weight-gradient side stream: lowest priority, so the hardware dispatcher prefers the
     critical path's workgroups (a CU-masked variant measured 5 % slower, round 1)."""
-    return torch.cuda.Stream(device=device, priority=100)
+    return make_stream(device, 100)
 
 
 def side_stream(device):

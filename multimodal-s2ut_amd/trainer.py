@@ -78,7 +78,7 @@ class Trainer:
         # (lowest priority), which only fills the CUs the critical path leaves idle.
         self.stream = None
         if model.params.flat.is_cuda:
-            self.stream = torch.cuda.Stream(device=model.params.flat.device, priority=-100)
+            self.stream = K.make_stream(model.params.flat.device, -100)
             if K._Side.stream is None:
                 K._Side.stream = K.make_side_stream(model.params.flat.device)
                 K._Side.ptr = K._Side.stream.cuda_stream
