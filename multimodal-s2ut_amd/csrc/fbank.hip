@@ -20,7 +20,10 @@ namespace {
 
 constexpr int WIN = 400, SHIFT = 160, NFFT = 512, NBIN = 257;
 constexpr int NC = 256;                        // complex FFT points (the real 512-point FFT's half)
-constexpr int FB_WAVES = 4;
+#ifndef MMS_FB_WAVES
+#define MMS_FB_WAVES 4
+#endif
+constexpr int FB_WAVES = MMS_FB_WAVES;
 constexpr int MELW_MAX = 1024;                 // nonzero mel weights staged per block (80 bins: ~510)
 constexpr int FB_MAXB = 512;                   // utterances whose frame / sample offsets are staged in LDS
 
@@ -225,11 +228,31 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
       P[k] = xr * xr + xi * xi;
     }
     wave_sync();
+#ifndef MMS_FB_MEL4
+#define MMS_FB_MEL4 0
+#endif
     for (int m = lane; m < nbins; m += 64) {
       const float* wm = S.melw + S.moff[m];
       const float* pm = P + S.mlo[m];
       float acc = 0.f;
-      for (int j = 0; j < S.mlen[m]; ++j) acc += wm[j] * pm[j];
+      if (MMS_FB_MEL4) {
+        // four weights per trip, the reads of a trip issued together (a one-weight trip waited on
+        // its two LDS reads before the next); zero-padded past the filter, the same summation order
+        const int len = S.mlen[m];
+        for (int j = 0; j < len; j += 4) {
+          float w4[4], p4[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool in = j + e < len;
+            w4[e] = in ? wm[j + e] : 0.f;
+            p4[e] = in ? pm[j + e] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc += w4[e] * p4[e];
+        }
+      } else {
+        for (int j = 0; j < S.mlen[m]; ++j) acc += wm[j] * pm[j];
+      }
       feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
     }
     wave_sync();
@@ -414,14 +437,18 @@ extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, cons
   MMS_REQUIRE(mel_range != nullptr, "fbank: mel_range required");
   if (init_consts(s)) return 1;
   if (total_frames == 0) return 0;
-  // persistent: 4 blocks (16 waves) per CU at most, each building its LDS tables once
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  const int grid = std::min((total_frames + FB_WAVES - 1) / FB_WAVES, 4 * ncu);
+  // persistent: as many blocks as fit on a CU at once (LDS / VGPR bound), each building its tables once
+  static int per_cu = 0;
+  if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fbank_kernel, 64 * FB_WAVES, 0) != hipSuccess ||
+                      per_cu <= 0))
+    per_cu = 4;
+  const int grid = std::min((total_frames + FB_WAVES - 1) / FB_WAVES, per_cu * ncu);
   hipLaunchKernelGGL(fbank_kernel, dim3(grid), dim3(64 * FB_WAVES), 0, s, wave, wave_off,
                      frame_off, B, total_frames, mel_banks, mel_range, nbins, feats);
   return mms::check_launch("fbank");
