@@ -20,10 +20,9 @@ namespace {
 
 constexpr int WIN = 400, SHIFT = 160, NFFT = 512, NBIN = 257;
 constexpr int NC = 256;                        // complex FFT points (the real 512-point FFT's half)
-#ifndef MMS_FB_WAVES
-#define MMS_FB_WAVES 4
-#endif
-constexpr int FB_WAVES = MMS_FB_WAVES;
+// 4 waves per block: 8 (6 waves per SIMD instead of 4) and 2 both measured slower, and four-weight
+// mel trips made no difference (round 4, profiles/round4_fbank_ab.txt)
+constexpr int FB_WAVES = 4;
 constexpr int MELW_MAX = 1024;                 // nonzero mel weights staged per block (80 bins: ~510)
 constexpr int FB_MAXB = 512;                   // utterances whose frame / sample offsets are staged in LDS
 
@@ -228,31 +227,11 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
       P[k] = xr * xr + xi * xi;
     }
     wave_sync();
-#ifndef MMS_FB_MEL4
-#define MMS_FB_MEL4 0
-#endif
     for (int m = lane; m < nbins; m += 64) {
       const float* wm = S.melw + S.moff[m];
       const float* pm = P + S.mlo[m];
       float acc = 0.f;
-      if (MMS_FB_MEL4) {
-        // four weights per trip, the reads of a trip issued together (a one-weight trip waited on
-        // its two LDS reads before the next); zero-padded past the filter, the same summation order
-        const int len = S.mlen[m];
-        for (int j = 0; j < len; j += 4) {
-          float w4[4], p4[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bool in = j + e < len;
-            w4[e] = in ? wm[j + e] : 0.f;
-            p4[e] = in ? pm[j + e] : 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc += w4[e] * p4[e];
-        }
-      } else {
-        for (int j = 0; j < S.mlen[m]; ++j) acc += wm[j] * pm[j];
-      }
+      for (int j = 0; j < S.mlen[m]; ++j) acc += wm[j] * pm[j];
       feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
     }
     wave_sync();
