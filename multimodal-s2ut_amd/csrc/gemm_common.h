@@ -402,13 +402,17 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][
   // the seed / high-counter half of the dropout hash is one constant for all 64 of this lane's
   // counters whenever they share the high word (always, unless the run straddles a 2^33
   // boundary): one mixer per pair of elements instead of two (bit-identical to mms_keep4)
-  uint32_t hmix = 0;
-  bool same_hi = false;
+  uint32_t hmix = 0, pbase = 0;
+  bool same_hi = false, fast = false;
   if (DROPS && P.thresh) {
     const uint64_t cf = P.offset + (uint64_t)m0 * P.ld_rng + n;
     const uint64_t cl = P.offset + (uint64_t)(m0 + 8 * (PASSES - 1)) * P.ld_rng + n + 7;
     same_hi = mms_same_hi(cf, cl) && ((cf & 1) == 0) && ((P.ld_rng & 1) == 0);
     hmix = mms_hi_mix(P.seed, cf);
+    // wave-uniform fast path (the compiler versions the pass loop on it): pass p's first pair index
+    // is pbase + 4 p ld_rng, in 32-bit arithmetic, no 64-bit counter per pass
+    pbase = (uint32_t)(cf >> 1);
+    fast = __all(same_hi);
   }
 #pragma unroll
   for (int pass = 0; pass < PASSES; ++pass) {
@@ -419,7 +423,15 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] = x[e] * P.alpha + bv[e];
     bool keep[8] = {true, true, true, true, true, true, true, true};
-    if (DROPS && P.thresh) {
+    if (DROPS && P.thresh && fast) {
+      const uint32_t p0 = pbase + (uint32_t)(4 * pass) * (uint32_t)P.ld_rng;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const uint32_t hv = mms_mix32((p0 + h) ^ hmix);
+        keep[2 * h] = (hv & 0xffffU) >= P.thresh;
+        keep[2 * h + 1] = (hv >> 16) >= P.thresh;
+      }
+    } else if (DROPS && P.thresh) {
       const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
       bool k0[4], k1[4];
       if (same_hi) {

@@ -86,7 +86,7 @@ struct DpOut {
 };
 template <int EPI>
 MMS_DEV DpOut dp_compute(const GemmP& P, bool live, int m, int n, const f32x4& v, const DpAux& ax, uint32_t hmix,
-                         bool same_hi, float dscale) {
+                         bool same_hi, bool fast, uint32_t pfrag, float dscale) {
   const bool ok = live && m < P.M && n < P.N;
   DpOut d;
   d.off = ok ? (int)(((long)m * P.ldc + n) * 2) : kOut;
@@ -99,9 +99,19 @@ MMS_DEV DpOut dp_compute(const GemmP& P, bool live, int m, int n, const f32x4& v
   for (int e = 0; e < 4; ++e) x[e] = v[e] * P.alpha + bv[e];
   bool keep[4] = {true, true, true, true};
   if (epi_drops<EPI>() && P.thresh) {
-    const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
-    if (same_hi) mms_keep4_hi(hmix, c0, P.thresh, keep);
-    else mms_keep4(P.seed, c0, P.thresh, keep);
+    if (fast) {
+      // wave-uniform fast path: the fragment's first pair index comes precomputed (32-bit, no
+      // 64-bit counter math); bit-identical to mms_keep4_hi on an even counter
+      const uint32_t h0 = mms_mix32(pfrag ^ hmix), h1 = mms_mix32((pfrag + 1) ^ hmix);
+      keep[0] = (h0 & 0xffffU) >= P.thresh;
+      keep[1] = (h0 >> 16) >= P.thresh;
+      keep[2] = (h1 & 0xffffU) >= P.thresh;
+      keep[3] = (h1 >> 16) >= P.thresh;
+    } else {
+      const uint64_t c0 = P.offset + (uint64_t)m * P.ld_rng + n;
+      if (same_hi) mms_keep4_hi(hmix, c0, P.thresh, keep);
+      else mms_keep4(P.seed, c0, P.thresh, keep);
+    }
   }
   h16x4 o4;
   if (EPI == MMS_EPI_GATE) {
@@ -268,8 +278,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
     for (int j = 0; j < 4; ++j) prev[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   int pm0 = 0, pn0 = 0;   // lane's first row / column of the previous tile
   bool have_prev = false;
-  uint32_t hmix = 0;
-  bool same_hi = false;
+  uint32_t hmix = 0, pbase = 0;   // pbase: the lane's first dropout pair index (fast path)
+  bool same_hi = false, fast = false;
   // operands of the fragments finished in k-step e live in pa[e & 1]: the next k-step's are loaded
   // while this one's are consumed
   DpAux pa[2][DP_PIECES];
@@ -281,7 +291,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
       for (int u = 0; u < DP_PIECES; ++u) pa[b][u] = DpAux{z, z, z};
   }
   // fragment p = 4 i + j of the previous tile (p compile-time after unrolling)
-  auto load_pieces = [&](int p0) {
+  auto load_pieces = [&](int p0) __attribute__((always_inline)) {
     DpAux* dst = pa[(p0 / DP_PIECES) & 1];
 #pragma unroll
     for (int u = 0; u < DP_PIECES; ++u)
@@ -289,17 +299,19 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
   };
   // the previous tile's fragments p0 .. p0 + DP_PIECES - 1 (also on the first tile, dropped there)
   DpOut po[DP_PIECES];
-  auto compute_pieces = [&](int p0) {
+  auto compute_pieces = [&](int p0) __attribute__((always_inline)) {
     const DpAux* src = pa[(p0 / DP_PIECES) & 1];
 #pragma unroll
     for (int u = 0; u < DP_PIECES; ++u) {
       const int p = p0 + u;
-      if (p < 16)
+      if (p < 16) {
+        const uint32_t pfrag = pbase + (uint32_t)((p >> 2) * 8) * (uint32_t)P.ld_rng + (uint32_t)((p & 3) * 8);
         po[u] = dp_compute<EPI>(P, have_prev, pm0 + (p >> 2) * 16, pn0 + (p & 3) * 16, prev[p >> 2][p & 3], src[u],
-                                hmix, same_hi, dscale);
+                                hmix, same_hi, fast, pfrag, dscale);
+      }
     }
   };
-  auto commit_pieces = [&]() {
+  auto commit_pieces = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < DP_PIECES; ++u) dp_commit<EPI>(R, po[u]);
   };
@@ -320,7 +332,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
     // stores at the top of the next k-step together with the DMA, so both have a whole k-step to
     // land before its vmcnt(0) (the wait makes no assumption about the order in which loads,
     // stores and atomics retire).  Aux operands are loaded one k-step ahead of their arithmetic.
-    auto kstep = [&](int kt, auto ep) {
+    auto kstep = [&](int kt, auto ep) __attribute__((always_inline)) {
       constexpr int EP = decltype(ep)::value;
       __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
       __builtin_amdgcn_s_barrier();
@@ -383,6 +395,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_dp_kernel(GemmP P, int tiles_m, in
       const uint64_t cl = P.offset + (uint64_t)(pm0 + 48) * P.ld_rng + pn0 + 48 + 3;
       same_hi = mms_same_hi(cf, cl) && ((cf & 1) == 0) && ((P.ld_rng & 1) == 0);
       hmix = mms_hi_mix(P.seed, cf);
+      pbase = (uint32_t)(cf >> 1);
+      fast = __all(same_hi);
     }
     if (!more) break;
     tm = ntm;
