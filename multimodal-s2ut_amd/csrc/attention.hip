@@ -217,6 +217,10 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   const uint64_t row_ctr = P.offset + ((uint64_t)z * P.Tq + q_own) * (uint64_t)P.Tk;
   const uint64_t zctr = P.offset + (uint64_t)z * P.Tq * P.Tk;
   const bool hi_fast = mms_same_hi(zctr, zctr + (uint64_t)P.Tq * P.Tk - 1);  // uniform per head
+  // every row's counters start even (even base, even key length): a key quad's two hash pairs are
+  // pair indices prow + (key >> 1) + {0, 1}, in 32-bit arithmetic (bit-identical to mms_keep4_hi)
+  const bool hi_pairs = hi_fast && (zctr & 1) == 0 && (P.Tk & 1) == 0;
+  const uint32_t prow = (uint32_t)(row_ctr >> 1);
   const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
   Pair64<HD, 64 * NW> pf;
   if constexpr (SHORT) {
@@ -302,8 +306,18 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
     for (int t = 0; t < 4; ++t) {
       bool keep[4] = {true, true, true, true};
       if (P.thresh) {
-        if (hi_fast) mms_keep4_hi(hi_mix, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
-        else mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+        if (hi_pairs) {
+          const uint32_t p0 = prow + (uint32_t)((kb + 16 * t + 4 * g) >> 1);
+          const uint32_t h0 = mms_mix32(p0 ^ hi_mix), h1 = mms_mix32((p0 + 1) ^ hi_mix);
+          keep[0] = (h0 & 0xffffU) >= P.thresh;
+          keep[1] = (h0 >> 16) >= P.thresh;
+          keep[2] = (h1 & 0xffffU) >= P.thresh;
+          keep[3] = (h1 >> 16) >= P.thresh;
+        } else if (hi_fast) {
+          mms_keep4_hi(hi_mix, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+        } else {
+          mms_keep4(P.seed, row_ctr + kb + 16 * t + 4 * g, P.thresh, keep);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {

@@ -2,13 +2,13 @@
 // path the reference's get_fbank takes: mm_s2ut/data/audio_utils.py:326-349) + utterance CMVN +
 // zero-padded fp16 collation.
 //
-// fbank_kernel: one wave per 25 ms frame, 4 waves per block, a persistent grid (frames dealt to the
-// waves round-robin), so the per-block LDS tables are built once per block, not per 16 frames.  DC
-// removal and pre-emphasis, povey window, then the 512-point real FFT as a 256-point complex FFT
-// of the even/odd sample pairs (z[n] = x[2n] + i x[2n+1]; radix-4, four in-place LDS stages, one
-// butterfly of 4 points per lane) and the standard split X[k] = E[k] + W^k O[k]; power spectrum,
-// triangular mel filters from a compact per-block LDS copy of their nonzero weights,
-// log(max(x, FLT_EPSILON)).  Twiddles, window and mel weights are staged in LDS once per block.
+// fbank_kernel: four frames per wave (16 lanes each), 4 waves per block, a persistent grid (frame
+// quads dealt to the waves round-robin), so the per-block LDS tables are built once per block.  DC
+// removal, pre-emphasis and the povey window in registers, then the 512-point real FFT as a
+// 256-point complex FFT of the even/odd sample pairs (z[n] = x[2n] + i x[2n+1]) done four-step
+// (16 x 16: register DFTs, one LDS transpose) and the standard split X[k] = E[k] + W^k O[k]; power
+// spectrum, triangular mel filters from a compact per-block LDS copy of their nonzero weights,
+// log(max(x, FLT_EPSILON)).
 // HBM-bound: 640 B of wave read (400 samples, hop 160 -> 4 B/sample amortised) + 4 * nbins B of
 // features written per frame.
 #include <algorithm>
@@ -20,11 +20,9 @@ namespace {
 
 constexpr int WIN = 400, SHIFT = 160, NFFT = 512, NBIN = 257;
 constexpr int NC = 256;                        // complex FFT points (the real 512-point FFT's half)
-// 4 waves per block: 8 (6 waves per SIMD instead of 4) and 2 both measured slower, and four-weight
-// mel trips made no difference (round 4, profiles/round4_fbank_ab.txt)
-constexpr int FB_WAVES = 4;
+constexpr int FB_WAVES = 4;                    // waves per block
 constexpr int MELW_MAX = 1024;                 // nonzero mel weights staged per block (80 bins: ~510)
-constexpr int FB_MAXB = 512;                   // utterances whose frame / sample offsets are staged in LDS
+constexpr int FB_MAXB = 256;                   // utterances whose frame / sample offsets are staged in LDS
 
 struct FbankConst {
   float window[WIN];
@@ -37,34 +35,82 @@ static bool g_fb_init = false;
 // base-4 digit reversal of an 8-bit index (256 = 4^4)
 MMS_DEV int rev4(int x) { return ((x & 3) << 6) | ((x & 12) << 2) | ((x & 48) >> 2) | ((x & 192) >> 6); }
 
+// Four frames per wave, 16 lanes per frame.  The 256-point complex FFT runs as 16 x 16 (four-step):
+// n = 16 n1 + n2, k = k1 + 16 k2.  Lane n2 holds z[16 n1 + n2] for all n1 in registers and does a
+// 16-point DFT over n1 (radix 4 x 4, constant twiddles), multiplies by W256^(n2 k1), and the frame's
+// 16 lanes swap rows and columns once through a padded LDS tile; lane k1 then does the 16-point DFT
+// over n2 and holds Z[k1 + 16 k2].  One more LDS round trip pairs Z[k] with Z[256 - k] for the real
+// split, a third hands the power spectrum to the mel sums (lane c: filters c, c + 16, ...).  Three
+// LDS hand-offs per four frames instead of eight per frame, and no per-stage index arithmetic.
+constexpr int FR_W = 4;                        // frames per wave
+constexpr int TSTR = 17;                       // row stride (float2) of the transpose tile: conflict-free
+
 struct FbankSmem {
-  float tw_re[NFFT / 2], tw_im[NFFT / 2];
-  float win[WIN];
+  float2 tw[NFFT / 2];                         // exp(-2 pi i j / 512), j < 256
+  float2 win2[NC];                             // (window[2m], window[2m + 1]); 0 past the 400 samples
   float melw[MELW_MAX];
   int mlo[256], mlen[256], moff[256], ntot;
-  int foff[FB_MAXB + 1];                       // frame_off (B <= FB_MAXB)
-  long woff[FB_MAXB];                          // wave_off
-  float x[FB_WAVES][WIN];
-  float zr[FB_WAVES][NC], zi[FB_WAVES][NC];
-  float pw[FB_WAVES][NBIN + 3];
+  int foff[FB_MAXB + 1];
+  long woff[FB_MAXB];
+  float2 buf[FB_WAVES][FR_W][16 * TSTR];       // transpose tile, then Z, then the power spectrum
 };
 
-// exp(-2 pi i j / 512) for 0 <= j < 512 from the half table (W^(j+256) = -W^j)
-MMS_DEV void tw512(const FbankSmem& S, int j, float& c, float& s) {
-  const int jj = j & 255;
-  const float sg = (j & 256) ? -1.f : 1.f;
-  c = sg * S.tw_re[jj];
-  s = sg * S.tw_im[jj];
+// exp(-2 pi i j / 512) for 0 <= j < 512 (W^(j+256) = -W^j)
+MMS_DEV float2 tw512(const FbankSmem& S, int j) {
+  const float2 t = S.tw[j & 255];
+  return (j & 256) ? make_float2(-t.x, -t.y) : t;
+}
+
+// in-register 16-point forward DFT, A[k] = sum_n a[n] exp(-2 pi i nk / 16), as 4 x 4: n = 4p + q,
+// k = r + 4s: four 4-point DFTs over p, twiddles W16^(qr), four 4-point DFTs over q
+MMS_DEV void dft4(float& r0, float& i0, float& r1, float& i1, float& r2, float& i2, float& r3, float& i3) {
+  const float s0r = r0 + r2, s0i = i0 + i2, d0r = r0 - r2, d0i = i0 - i2;
+  const float s1r = r1 + r3, s1i = i1 + i3, d1r = r1 - r3, d1i = i1 - i3;
+  r0 = s0r + s1r; i0 = s0i + s1i;            // y0 = a0 + a1 + a2 + a3
+  r1 = d0r + d1i; i1 = d0i - d1r;            // y1 = a0 - i a1 - a2 + i a3
+  r2 = s0r - s1r; i2 = s0i - s1i;            // y2 = a0 - a1 + a2 - a3
+  r3 = d0r - d1i; i3 = d0i + d1r;            // y3 = a0 + i a1 - a2 - i a3
+}
+
+MMS_DEV void dft16(float (&re)[16], float (&im)[16]) {
+  // W16^e = (cos(pi e / 8), -sin(pi e / 8)), e = q r <= 9
+  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508977f, R2 = 0.70710678118654752f;
+  constexpr float WC[10] = {1.f, C1, R2, S1, 0.f, -S1, -R2, -C1, -1.f, -C1};
+  constexpr float WS[10] = {0.f, -S1, -R2, -C1, -1.f, -C1, -R2, -S1, 0.f, S1};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dft4(re[q], im[q], re[4 + q], im[4 + q], re[8 + q], im[8 + q], re[12 + q], im[12 + q]);
+  // now element (p = r, q) holds B[q][r] at index 4r + q
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+#pragma unroll
+    for (int r = 1; r < 4; ++r) {
+      const int e = q * r, i = 4 * r + q;
+      const float xr = re[i] * WC[e] - im[i] * WS[e], xi = re[i] * WS[e] + im[i] * WC[e];
+      re[i] = xr;
+      im[i] = xi;
+    }
+  float orr[16], oi[16];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float a[8] = {re[4 * r], im[4 * r], re[4 * r + 1], im[4 * r + 1], re[4 * r + 2], im[4 * r + 2], re[4 * r + 3], im[4 * r + 3]};
+    dft4(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { orr[r + 4 * s] = a[2 * s]; oi[r + 4 * s] = a[2 * s + 1]; }
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { re[k] = orr[k]; im[k] = oi[k]; }
 }
 
 // intra-wave LDS hand-off: this wave's LDS writes are complete (no wait on its global stores, so
-// a frame's feature stores stay in flight under the next frame's work)
+// a frame's feature stores stay in flight under the next frames' work)
 MMS_DEV void wave_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 }
 
-__global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __restrict__ wave,
+// 3 waves per SIMD (168 VGPRs, a few spilled; the LDS allows 3 blocks per CU): 60 us against 70 us
+// at the compiler's own 186 VGPRs / 2 waves (profiles/round4_fbank_v2_ab.txt)
+__global__ void __launch_bounds__(64 * FB_WAVES, 3) fbank_kernel(const float* __restrict__ wave,
                                                               const int64_t* __restrict__ wave_off,
                                                               const int* __restrict__ frame_off, int B, int total,
                                                               const float* __restrict__ banks,
@@ -72,17 +118,16 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
                                                               float* __restrict__ feats) {
   __shared__ FbankSmem S;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // per-block tables, built once per (persistent) block, every step parallel over the threads:
-  // twiddles, window, and the mel filters' nonzero weights (compact, prefix offsets)
-  for (int i = tid; i < NFFT / 2; i += blockDim.x) { S.tw_re[i] = c_fb.tw_re[i]; S.tw_im[i] = c_fb.tw_im[i]; }
-  for (int i = tid; i < WIN; i += blockDim.x) S.win[i] = c_fb.window[i];
+  for (int i = tid; i < NFFT / 2; i += blockDim.x) S.tw[i] = make_float2(c_fb.tw_re[i], c_fb.tw_im[i]);
+  for (int m = tid; m < NC; m += blockDim.x)
+    S.win2[m] = 2 * m + 1 < WIN ? make_float2(c_fb.window[2 * m], c_fb.window[2 * m + 1]) : make_float2(0.f, 0.f);
   for (int m = tid; m < nbins; m += blockDim.x) {
     const int lo = mel_range[2 * m], hi = mel_range[2 * m + 1];
     S.mlo[m] = lo;
     S.mlen[m] = hi - lo;
   }
   // utterance offsets in LDS: a frame's utterance is then found without a chain of dependent
-  // global loads (the binary search used to stall every frame on ~log2(B) L2 round trips)
+  // global loads
   const bool lds_off = B <= FB_MAXB;
   if (lds_off) {
     for (int i = tid; i <= B; i += blockDim.x) S.foff[i] = frame_off[i];
@@ -115,7 +160,6 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
   }
   __syncthreads();
   const int nw = S.ntot;   // <= 2 * 257: each FFT bin lies in at most two triangular filters
-  // every weight by a flat index: its filter by binary search over the prefix offsets
   for (int i = tid; i < nw && i < MELW_MAX; i += blockDim.x) {
     int a = 0, b = nbins;
     while (b - a > 1) {
@@ -125,114 +169,122 @@ __global__ void __launch_bounds__(64 * FB_WAVES) fbank_kernel(const float* __res
     S.melw[i] = banks[(long)a * NBIN + S.mlo[a] + (i - S.moff[a])];
   }
   __syncthreads();
-  float* X = S.x[w];
-  float* zr = S.zr[w];
-  float* zi = S.zi[w];
-  float* P = S.pw[w];
+  const int g = lane >> 4, c = lane & 15;
+  float2* T = S.buf[w][g];
+  float* P = reinterpret_cast<float*>(T);
   const float flt_eps = 1.1920928955078125e-07f;
-  // persistent: wave (block, w) takes frames w + FB_WAVES * block, + FB_WAVES * gridDim.x, ...;
-  // the next frame's 400 samples are loaded into registers while the current one is transformed
-  const int fstep = gridDim.x * FB_WAVES;
-  int utt = 0;   // utterance of the wave's last frame: frames only move forward, so the LDS walk
-                 // from it is a step or two per frame
+  int utt = 0;   // utterance of the lane's last frame (frames only move forward)
   auto frame_src = [&](int f) {
     if (lds_off) {
       while (utt + 1 < B && S.foff[utt + 1] <= f) ++utt;
       return wave + S.woff[utt] + (long)(f - S.foff[utt]) * SHIFT;
     }
-    int lo = 0, hi = B;   // utterance of frame f (binary search over frame_off)
+    int lo = 0, hi = B;
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
       if (frame_off[mid] <= f) lo = mid; else hi = mid;
     }
     return wave + wave_off[lo] + (long)(f - frame_off[lo]) * SHIFT;
   };
-  float xs[7];
+  // lane c of a frame holds samples 2m, 2m + 1 of m = 16 n1 + c, n1 < 13 (m < 200: the 400 samples)
+  constexpr int NR = (WIN / 2 + 15) / 16;
+  float xe[NR], xo[NR];
   auto load_frame = [&](int f) {
-    if (f >= total) return;
-    const float* src = frame_src(f);
+    if (f < total) {
+      const float* src = frame_src(f);
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int j = lane + 64 * q;
-      xs[q] = j < WIN ? src[j] : 0.f;
+      for (int n1 = 0; n1 < NR; ++n1) {
+        const int m = 16 * n1 + c;
+        const bool in = m < WIN / 2;
+        xe[n1] = in ? src[2 * m] : 0.f;
+        xo[n1] = in ? src[2 * m + 1] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int n1 = 0; n1 < NR; ++n1) xe[n1] = xo[n1] = 0.f;
     }
   };
-  load_frame(blockIdx.x * FB_WAVES + w);
-  for (int f = blockIdx.x * FB_WAVES + w; f < total; f += fstep) {
+  // persistent: wave (block, w) takes frames 4 (w + FB_WAVES block) + g, then + 4 FB_WAVES gridDim.x
+  const int fstep = FR_W * FB_WAVES * gridDim.x;
+  int f = FR_W * (blockIdx.x * FB_WAVES + w) + g;
+  load_frame(f);
+  for (int f0 = FR_W * (blockIdx.x * FB_WAVES + w); f0 < total; f0 += fstep, f += fstep) {
     float sum = 0.f;
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
-      const int j = lane + 64 * q;
-      if (j < WIN) { X[j] = xs[q]; sum += xs[q]; }
+    for (int n1 = 0; n1 < NR; ++n1) sum += xe[n1] + xo[n1];
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 16);
+    const float mean = sum * (1.f / WIN);
+    // DC removal, pre-emphasis (x[-1] = x[0]), window; x[2m - 1] is lane c - 1's odd sample (lane
+    // 15's of the previous row for c = 0)
+    float zr[16], zi[16];
+#pragma unroll
+    for (int n1 = 0; n1 < NR; ++n1) {
+      const float r = __shfl(xo[n1], (c + 15) & 15, 16);
+      const float prev_row = n1 ? __shfl(xo[n1 - 1], 15, 16) : xe[0];
+      const float pe = c ? r : prev_row;
+      const float2 wv = S.win2[16 * n1 + c];
+      const float e = xe[n1] - mean, o = xo[n1] - mean;
+      zr[n1] = (e - 0.97f * (pe - mean)) * wv.x;
+      zi[n1] = (o - 0.97f * e) * wv.y;
     }
-    load_frame(f + fstep);
-    const float mean = wave_sum(sum) * (1.f / WIN);
-    wave_sync();
-    // pre-emphasis (replicate-pad at j = 0), window, zero pad to 512; pairs -> digit-reversed slots
 #pragma unroll
-    for (int q = 0; q < NC / 64; ++q) {
-      const int n = lane + 64 * q;
-      float v[2];
+    for (int n1 = NR; n1 < 16; ++n1) zr[n1] = zi[n1] = 0.f;
+    load_frame(f + fstep);   // the next frames' samples stream in under this one's transform
+    // 16-point DFTs over n1, twiddle W256^(c k1) = W512^(2 c k1), transpose through LDS
+    dft16(zr, zi);
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int j = 2 * n + e;
-        v[e] = 0.f;
-        if (j < WIN) {
-          const float xj = X[j] - mean;
-          const float xp = (j > 0 ? X[j - 1] : X[0]) - mean;
-          v[e] = (xj - 0.97f * xp) * S.win[j];
-        }
+    for (int k1 = 0; k1 < 16; ++k1) {
+      float2 y = make_float2(zr[k1], zi[k1]);
+      if (k1) {
+        const float2 t = tw512(S, 2 * c * k1);
+        y = make_float2(zr[k1] * t.x - zi[k1] * t.y, zr[k1] * t.y + zi[k1] * t.x);
       }
-      const int r = rev4(n);
-      zr[r] = v[0];
-      zi[r] = v[1];
-    }
-    wave_sync();
-    // radix-4 DIT: stage L combines four length-L DFTs into one of length 4L; lane = butterfly
-#pragma unroll
-    for (int L = 1; L < NC; L <<= 2) {
-      const int k = lane & (L - 1), base = (lane - k) * 4 + k;
-      float ar[4], ai[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ar[q] = zr[base + q * L];
-        ai[q] = zi[base + q * L];
-      }
-      // b_q = W_{4L}^{qk} a_q, W_{4L} = W_512^(128 / L)
-#pragma unroll
-      for (int q = 1; q < 4; ++q) {
-        float c, s;
-        tw512(S, (q * k * (128 / L)) & 511, c, s);
-        const float r = ar[q] * c - ai[q] * s, im = ar[q] * s + ai[q] * c;
-        ar[q] = r;
-        ai[q] = im;
-      }
-      const float s0r = ar[0] + ar[2], s0i = ai[0] + ai[2], d0r = ar[0] - ar[2], d0i = ai[0] - ai[2];
-      const float s1r = ar[1] + ar[3], s1i = ai[1] + ai[3], d1r = ar[1] - ar[3], d1i = ai[1] - ai[3];
-      zr[base] = s0r + s1r;            zi[base] = s0i + s1i;            // y0 = b0 + b1 + b2 + b3
-      zr[base + L] = d0r + d1i;        zi[base + L] = d0i - d1r;        // y1 = b0 - i b1 - b2 + i b3
-      zr[base + 2 * L] = s0r - s1r;    zi[base + 2 * L] = s0i - s1i;    // y2 = b0 - b1 + b2 - b3
-      zr[base + 3 * L] = d0r - d1i;    zi[base + 3 * L] = d0i + d1r;    // y3 = b0 + i b1 - b2 - i b3
-      wave_sync();
-    }
-    // real-FFT split: X[k] = E + W_512^k O, E = (Z[k] + conj Z[256-k]) / 2, O = -i (Z[k] - conj Z[256-k]) / 2
-    for (int k = lane; k < NBIN; k += 64) {
-      const int a = k & (NC - 1), b = (NC - k) & (NC - 1);
-      const float zkr = zr[a], zki = zi[a], znr = zr[b], zni = zi[b];
-      const float er = 0.5f * (zkr + znr), ei = 0.5f * (zki - zni);
-      const float orr = 0.5f * (zki + zni), oi = -0.5f * (zkr - znr);
-      float c, s;
-      tw512(S, k, c, s);
-      const float xr = er + (orr * c - oi * s), xi = ei + (orr * s + oi * c);
-      P[k] = xr * xr + xi * xi;
+      T[k1 * TSTR + c] = y;
     }
     wave_sync();
-    for (int m = lane; m < nbins; m += 64) {
-      const float* wm = S.melw + S.moff[m];
-      const float* pm = P + S.mlo[m];
-      float acc = 0.f;
-      for (int j = 0; j < S.mlen[m]; ++j) acc += wm[j] * pm[j];
-      feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) {
+      const float2 y = T[c * TSTR + n2];
+      zr[n2] = y.x;
+      zi[n2] = y.y;
+    }
+    dft16(zr, zi);   // lane c: Z[c + 16 k2] at k2
+    float2* Z = T;
+    // (the buffer is rewritten in place: compiler fences keep every read of one phase ahead of the
+    // next phase's writes; the LDS itself serves one wave's accesses in order)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) Z[c + 16 * k2] = make_float2(zr[k2], zi[k2]);
+    wave_sync();
+    // real-FFT split: X[k] = E + W512^k O, E = (Z[k] + conj Z[256-k]) / 2, O = -i (Z[k] - conj Z[256-k]) / 2
+    float pw[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) {
+      const int k = c + 16 * k2;
+      const float2 zn = Z[(NC - k) & (NC - 1)];
+      const float zkr = zr[k2], zki = zi[k2];
+      const float er = 0.5f * (zkr + zn.x), ei = 0.5f * (zki - zn.y);
+      const float orr = 0.5f * (zki + zn.y), oi = -0.5f * (zkr - zn.x);
+      const float2 t = tw512(S, k);
+      const float xr = er + (orr * t.x - oi * t.y), xi = ei + (orr * t.y + oi * t.x);
+      pw[k2] = xr * xr + xi * xi;
+    }
+    // k = 256 (Nyquist): E = Re Z[0], O = Im Z[0], W512^256 = -1
+    const float nyq = (zr[0] - zi[0]) * (zr[0] - zi[0]);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) P[c + 16 * k2] = pw[k2];
+    if (c == 0) P[NC] = nyq;
+    wave_sync();
+    if (f < total) {
+      for (int m = c; m < nbins; m += 16) {
+        const float* wm = S.melw + S.moff[m];
+        const float* pm = P + S.mlo[m];
+        float acc = 0.f;
+        for (int j = 0; j < S.mlen[m]; ++j) acc += wm[j] * pm[j];
+        feats[(long)f * nbins + m] = __logf(fmaxf(acc, flt_eps));
+      }
     }
     wave_sync();
   }

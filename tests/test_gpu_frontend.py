@@ -35,6 +35,25 @@ def test_fbank_matches_oracle(fe):
             assert np.abs(got - ref).max() < 2e-3, np.abs(got - ref).max()
 
 
+def test_fbank_many_utterances(fe):
+    """More utterances than the kernel stages in LDS (FB_MAXB = 256): the frame -> utterance lookup
+    falls back to a binary search over frame_off; ragged 0-4 frame utterances, frame quads that
+    straddle utterance boundaries."""
+    rng = np.random.default_rng(5)
+    waves = [(rng.standard_normal(int(n)) * 2000).astype(np.float32)
+             for n in rng.integers(100, 400 + 4 * 160, size=300)]
+    wb = fe.upload(waves)
+    feats = fe.features_f32(wb).cpu().numpy()
+    off = wb["frame_off"].cpu().numpy()
+    assert off[-1] > 0
+    for j, i in enumerate(wb["order"]):
+        ref = RF.fbank(waves[i])
+        got = feats[off[j]:off[j + 1]]
+        assert got.shape == ref.shape, (got.shape, ref.shape)
+        if ref.size:
+            assert np.abs(got - ref).max() < 2e-3, (i, np.abs(got - ref).max())
+
+
 def test_fbank_cmvn_collate(fe):
     rng = np.random.default_rng(4)
     frames = [80, 120, 31]
