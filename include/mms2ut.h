@@ -95,8 +95,8 @@ int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
 int mms2ut_gemm_set_pp(int mode);
 /* NT shapes of more than one round of 128x128 tiles (> 512) run on a persistent kernel whose blocks
  * walk several tiles and finish each tile's epilogue inside the next tile's k-loop (bit-identical
- * results).  mode 1: on, 0: off, 2: only K >= 1536, 3: only K < 1536 (default; env MMS2UT_GEMM_DP
- * overrides it at first use).                                                                     */
+ * results).  mode 1: on, 0: off (default; env MMS2UT_GEMM_DP overrides it at first use), 2: only
+ * K >= 1536, 3: only K < 1536.                                                                    */
 int mms2ut_gemm_set_dp(int mode);
 
 /* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the

@@ -890,15 +890,16 @@ extern "C" int mms2ut_gemm_set_pp(int mode) {
 }
 
 // Persistent deferred-epilogue kernel (gemm_dp.hip) for NT grids of more than one round of the
-// 512 block slots (mms2ut_gemm_set_dp / MMS2UT_GEMM_DP).  Default 3 = the short-K (K < 1536) wide
-// shapes only: step 17.29-17.32 ms against 17.43-17.48 for the one-tile-per-block kernel, and
-// 17.25-17.32 with every qualifying shape (the long-K N = 768 shapes alone: 17.55-17.57) --
-// round-4 A/B, gpurun_out r4o, three interleaved reps (profiles/round4_dp_ab.txt).
+// 512 block slots (mms2ut_gemm_set_dp / MMS2UT_GEMM_DP; 3 = the short-K (K < 1536) wide shapes
+// only).  Off by default: it won the step by 0.5-0.8 % (17.29-17.32 vs 17.43-17.48 ms, gpurun_out
+// r4o) until the epilogue dropout fast path shortened the one-tile-per-block kernel's C-store
+// phase; since then off is 0.2-0.4 % faster (16.77-16.88 vs 16.86-16.93 ms, and 17.38-17.47 vs
+// 17.41-17.46 over six interleaved pairs on a second box: profiles/round4_dp_ab.txt).
 static int g_dp_mode = -1;
 static int dp_mode() {
   if (g_dp_mode < 0) {
     const char* e = getenv("MMS2UT_GEMM_DP");
-    g_dp_mode = e ? atoi(e) : 3;
+    g_dp_mode = e ? atoi(e) : 0;
   }
   return g_dp_mode;
 }

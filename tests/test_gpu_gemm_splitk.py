@@ -181,4 +181,4 @@ def test_dp_gemm_bit_identical(M, N, K):
             assert torch.equal(outs[1][0].view(torch.int16), outs[0][0].view(torch.int16)), name
             assert torch.equal(outs[1][1].view(torch.int16), outs[0][1].view(torch.int16)), (name, "out2")
     finally:
-        K_.call("mms2ut_gemm_set_dp", 3)   # the library default
+        K_.call("mms2ut_gemm_set_dp", 0)   # the library default
