@@ -319,6 +319,95 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
   stamp_end(P.stamps, t_start);
 }
 
+// ------------------------------------------------------------------------------------------
+// 160 x 128 NT tile: each of the 4 waves owns 80 rows (5 MFMA fragments) x 64 columns; 2-stage
+// LDS-DMA ring of 36 KiB stages (A 160 x 64, B 128 x 64), two blocks per CU.  For NT grids just
+// past one round of 128x128 tiles (e.g. M = 11-16 k rows x N = 768: 564 tiles of 128 rows for 512
+// block slots, a second round for 52 of them) the 160-row tiles fit one round at 1.25x the work per
+// tile.  Same k order, same MFMA operands per accumulator, same staged epilogue per element:
+// bit-identical to gemm_dma_kernel<true, true, EPI, 2>.
+// ------------------------------------------------------------------------------------------
+constexpr int BMT = 160, FRT = 5, TILE_T = BMT * 64 * 2;   // 20 KiB A stage
+
+template <int EPI>
+__global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
+  if (P.thresh) P.seed = mms_step_seed(P.seed);
+  __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_T + TILE_BYTES)];
+  int z, tm, tn;
+  tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
+  (void)z;   // batch 1 (host)
+  const int bm = tm * BMT, bn = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const long a_ext = ((long)(P.M - 1) * P.lda + P.K) * 2;
+  const long b_ext = ((long)(P.N - 1) * P.ldb + P.K) * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)P.A, (short)0, (int)a_ext, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)P.B, (short)0, (int)b_ext, 0x00020000);
+#define SA(s) (smem + (s) * (TILE_T + TILE_BYTES))
+#define SB(s) (SA(s) + TILE_T)
+  // a 160-row A stage: the 128-row pattern (16 wave-instructions) and rows 128..159 (one more per
+  // wave, the same swizzled 8-row layout); rows past M read as zero through the descriptor
+  auto dma_a = [&](char* lds, int k0) {
+    dma_tile<true>(ra, lds, P.lda, bm, k0, wid, lane);
+#ifndef MMS_GEMM_NODMA
+    const int row = 128 + wid * 8 + (lane >> 3), c = (lane & 7) ^ (row & 7);
+    const int voff = (int)(((long)(bm + row) * P.lda + k0 + c * 8) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(lds + (16 + wid) * 1024), 16, voff, 0, 0, 0);
+#endif
+  };
+  f32x4 acc[FRT][4];
+#pragma unroll
+  for (int i = 0; i < FRT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = P.K / BK;   // K % 64 == 0 (host)
+  if (nk > 0) {
+    dma_a(SA(0), 0);
+    dma_tile<true>(rb, SB(0), P.ldb, bn, 0, wid, lane);
+  }
+  constexpr bool PR = PRIO && EPI != MMS_EPI_F32;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      dma_a(SA(cur ^ 1), (kt + 1) * BK);
+      dma_tile<true>(rb, SB(cur ^ 1), P.ldb, bn, (kt + 1) * BK, wid, lane);
+    }
+    h16x8 fa2[2][FRT], fb2[2][4];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int i = 0; i < FRT; ++i) fa2[kk][i] = read_frag<true>(SA(cur), wm * 80 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<true>(SB(cur), wn * 64 + j * 16, kk, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (PR) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FRT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb2[kk][j], fa2[kk][i], acc[i][j], 0, 0, 0);
+      if (PR) __builtin_amdgcn_s_setprio(0);
+    }
+  }
+#undef SA
+#undef SB
+  __syncthreads();   // the ring is idle (the last k-step waited for vmcnt(0))
+  // the wave's rows [bm + 80 wm, + 80): fragments 0-3 (64 rows), then fragment 4 (16 rows), each
+  // through the wave's 16 KiB staging area (staged_epilogue places wave rows at bm + 64 wm)
+  staged_epilogue<EPI, 4>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), bm + 16 * wm, bn, wm, wn, wid,
+                          lane, P.C, P.aux);
+  __syncthreads();
+  staged_epilogue<EPI, 1>(P, smem, reinterpret_cast<const f32x4(&)[1][4]>(acc[4]), bm + 16 * wm + 64, bn, wm, wn,
+                          wid, lane, P.C, P.aux);
+  stamp_end(P.stamps, t_start);
+}
+
 // Grouped weight gradients: the dW = dy^T x products of one transformer layer (QKV, out-proj, fc1,
 // fc2, and the decoder's cross-attention q / out) as ONE launch over the union of their 128x128
 // tiles, unsplit: fp16 dW and (first tile column) fp16 db written straight from the accumulators,
@@ -544,6 +633,18 @@ int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
   }
   return mms::check_launch("gemm_dma2");
+}
+
+int launch_tall(int epi, const GemmP& P, int tm, int tn, hipStream_t s) {
+  const int total = tm * tn;
+  dim3 grid(total), block(NT);
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_tall_kernel<E>), grid, block, 0, s, P, tm, tn, total); break;
+    MMS_EPI_CASES
+#undef CASE
+    default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
+  }
+  return mms::check_launch("gemm_tall");
 }
 
 template <bool A_KC, bool B_KC>
@@ -918,6 +1019,30 @@ extern "C" int mms2ut_gemm_set_dp(int mode) {
   return 0;
 }
 
+// 160-row NT tiles (gemm_tall_kernel) when they take fewer rounds of the 512 block slots than
+// 128-row ones, counting a 160-row tile as 1.3 128-row tiles (mms2ut_gemm_set_tall / env
+// MMS2UT_GEMM_TALL: 1 = by that rule (default), 0 = never, 2 = every qualifying NT shape).
+static int g_tall_mode = -1;
+static int tall_mode() {
+  if (g_tall_mode < 0) {
+    const char* e = getenv("MMS2UT_GEMM_TALL");
+    g_tall_mode = e ? atoi(e) : 1;
+  }
+  return g_tall_mode;
+}
+static bool tall_route(const mms2ut_gemm_args* a, int tm, int tn) {
+  const int mode = tall_mode();
+  if (mode == 0) return false;
+  if (mode == 2) return true;
+  const long r128 = ((long)tm * tn + 511) / 512, r160 = ((long)((a->M + BMT - 1) / BMT) * tn + 511) / 512;
+  return 13 * r160 < 10 * r128;
+}
+extern "C" int mms2ut_gemm_set_tall(int mode) {
+  MMS_REQUIRE(mode >= 0 && mode <= 2, "gemm_set_tall: mode must be 0..2 (got %d)", mode);
+  g_tall_mode = mode;
+  return 0;
+}
+
 // Tile height of the ping-pong kernel for an NT shape, 0 = use the 128x128 kernel.  One block per
 // CU: a launch of t tiles takes ceil(t / 256) rounds, each as long as one BM x 256 tile, so the
 // height that fills the last round best wins (per-tile cost ~ BM + a fixed 48-row overhead for
@@ -1049,6 +1174,12 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
       P.stamps = stamp_take((long)tmp * tnp);
       return mmsg::launch_pp(a->epi, bm, P, tmp, tnp, s);
     }
+  }
+  if (dma_ok && a_kc && b_kc && nz == 1 && tall_route(a, tm, tn)) {
+    const int tmt = (a->M + BMT - 1) / BMT;
+    P.group_m = group_m_for(tmt);
+    P.stamps = stamp_take((long)tmt * tn);
+    return launch_tall(a->epi, P, tmt, tn, s);
   }
   // (the deferred epilogue addresses C / aux / out2 through buffer descriptors: 31-bit extents)
   const long ep_ext = 2 * ((long)(a->M - 1) * std::max<long>({(long)a->ldc, (long)a->ldaux, (long)a->ldo2}) + 2L * a->N);

@@ -182,3 +182,44 @@ def test_dp_gemm_bit_identical(M, N, K):
             assert torch.equal(outs[1][1].view(torch.int16), outs[0][1].view(torch.int16)), (name, "out2")
     finally:
         K_.call("mms2ut_gemm_set_dp", 0)   # the library default
+
+
+@pytest.mark.parametrize("M,N,K", [(12000, 768, 768), (12000, 768, 3072), (11001, 768, 2304), (10000, 1000, 640),
+                                   (300, 520, 64), (16384, 768, 192)])
+def test_tall_gemm_bit_identical(M, N, K):
+    """gemm_tall_kernel (160 x 128 NT tiles, gemm.hip) against the 128x128 LDS-DMA kernel on the same
+    operands: bit-identical for every fused epilogue, incl. ragged M (rows past M in the last
+    160-row tile), ragged N, short K, dropout counters; mode 2 forces the 160-row tiles."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    mm = pkg()
+    K_ = mm.kernels
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + 2)
+    x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
+    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).half()
+    b = (torch.randn(N, device="cuda", generator=g) * 0.1).half()
+    aux = torch.randn(M, 2 * N, device="cuda", generator=g).half()
+    c0 = torch.randn(M, N, device="cuda", generator=g).half()
+    try:
+        for name in _PP_EPIS:
+            epi = getattr(K_, "EPI_" + name)
+            outs = []
+            for mode in (0, 2):
+                K_.call("mms2ut_gemm_set_tall", mode)
+                out = c0.clone()
+                out2 = torch.zeros(M, N, dtype=torch.float16, device="cuda")
+                p = 0.1 if name in ("RELU_DROP", "DROP_RESID", "GELU_DROP", "GELU_DROP_BWD", "RELU_DROP_BWD") else 0.0
+                K_.gemm(x, W, out, M, N, K, lda=K, ldb=K, ldc=N, epi=epi, bias=b,
+                        aux=aux if name in ("DROP_RESID", "RELU_DROP_BWD", "GATE", "GELU_DROP_BWD") else None,
+                        ldaux=2 * N, out2=out2 if name in ("GATE", "GELU_DROP") else None, ldo2=N,
+                        p=p, seed=79, offset=7 * N, ld_rng=N, fixup=False)
+                outs.append((out, out2))
+            torch.cuda.synchronize()
+            assert torch.equal(outs[1][0].view(torch.int16), outs[0][0].view(torch.int16)), name
+            assert torch.equal(outs[1][1].view(torch.int16), outs[0][1].view(torch.int16)), (name, "out2")
+        K_.call("mms2ut_gemm_set_tall", 2)
+        got = K_.linear(x, W, b)
+        ref = (x.float() @ W.float().t() + b.float())
+        assert _rel(got, ref) < 2e-3
+    finally:
+        K_.call("mms2ut_gemm_set_tall", 1)   # the library default
