@@ -320,17 +320,17 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
 }
 
 // ------------------------------------------------------------------------------------------
-// 160 x 128 NT tile: each of the 4 waves owns 80 rows (5 MFMA fragments) x 64 columns; 2-stage
-// LDS-DMA ring of 36 KiB stages (A 160 x 64, B 128 x 64), two blocks per CU.  For NT grids just
-// past one round of 128x128 tiles (e.g. M = 11-16 k rows x N = 768: 564 tiles of 128 rows for 512
-// block slots, a second round for 52 of them) the 160-row tiles fit one round at 1.25x the work per
-// tile.  Same k order, same MFMA operands per accumulator, same staged epilogue per element:
-// bit-identical to gemm_dma_kernel<true, true, EPI, 2>.
+// Tall NT tiles, 32 FRT x 128 (FRT = 5: 160 rows, 6: 192): each of the 4 waves owns 16 FRT rows
+// (FRT MFMA fragments) x 64 columns; 2-stage LDS-DMA ring of (4 FRT + 16) KiB stages, two blocks
+// per CU (192 rows: 80 KiB, exactly half the CU's LDS).  For NT grids just past a round of 128x128
+// tiles (e.g. M = 11-16 k rows x N = 768: 564 tiles of 128 rows for 512 block slots, a second
+// round for 52 of them) taller tiles fit fewer rounds at 1.25x / 1.5x the work per tile.  Same k
+// order, same MFMA operands per accumulator, same staged epilogue per element: bit-identical to
+// gemm_dma_kernel<true, true, EPI, 2>.
 // ------------------------------------------------------------------------------------------
-constexpr int BMT = 160, FRT = 5, TILE_T = BMT * 64 * 2;   // 20 KiB A stage
-
-template <int EPI>
+template <int EPI, int FRT>
 __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
+  constexpr int BMT = 32 * FRT, TILE_T = BMT * 64 * 2, XW = (BMT - 128) / 32;   // XW: extra A rows' DMA per wave / 8
   const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
   __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_T + TILE_BYTES)];
@@ -347,14 +347,18 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)P.B, (short)0, (int)b_ext, 0x00020000);
 #define SA(s) (smem + (s) * (TILE_T + TILE_BYTES))
 #define SB(s) (SA(s) + TILE_T)
-  // a 160-row A stage: the 128-row pattern (16 wave-instructions) and rows 128..159 (one more per
-  // wave, the same swizzled 8-row layout); rows past M read as zero through the descriptor
+  // a tall A stage: the 128-row pattern (16 wave-instructions) and rows 128.. (XW more per wave,
+  // the same swizzled 8-row layout); rows past M read as zero through the descriptor
   auto dma_a = [&](char* lds, int k0) {
     dma_tile<true>(ra, lds, P.lda, bm, k0, wid, lane);
 #ifndef MMS_GEMM_NODMA
-    const int row = 128 + wid * 8 + (lane >> 3), c = (lane & 7) ^ (row & 7);
-    const int voff = (int)(((long)(bm + row) * P.lda + k0 + c * 8) * 2);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(lds + (16 + wid) * 1024), 16, voff, 0, 0, 0);
+#pragma unroll
+    for (int x = 0; x < XW; ++x) {
+      const int ins = 16 + wid * XW + x;
+      const int row = ins * 8 + (lane >> 3), c = (lane & 7) ^ (row & 7);
+      const int voff = (int)(((long)(bm + row) * P.lda + k0 + c * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
+    }
 #endif
   };
   f32x4 acc[FRT][4];
@@ -380,7 +384,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int i = 0; i < FRT; ++i) fa2[kk][i] = read_frag<true>(SA(cur), wm * 80 + i * 16, kk, lane);
+      for (int i = 0; i < FRT; ++i) fa2[kk][i] = read_frag<true>(SA(cur), wm * 16 * FRT + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<true>(SB(cur), wn * 64 + j * 16, kk, lane);
     }
@@ -398,13 +402,14 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
 #undef SA
 #undef SB
   __syncthreads();   // the ring is idle (the last k-step waited for vmcnt(0))
-  // the wave's rows [bm + 80 wm, + 80): fragments 0-3 (64 rows), then fragment 4 (16 rows), each
+  // the wave's rows [bm + 16 FRT wm, + 16 FRT): fragments 0-3 (64 rows), then the rest, each
   // through the wave's 16 KiB staging area (staged_epilogue places wave rows at bm + 64 wm)
-  staged_epilogue<EPI, 4>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), bm + 16 * wm, bn, wm, wn, wid,
-                          lane, P.C, P.aux);
-  __syncthreads();
-  staged_epilogue<EPI, 1>(P, smem, reinterpret_cast<const f32x4(&)[1][4]>(acc[4]), bm + 16 * wm + 64, bn, wm, wn,
+  constexpr int WR = 16 * FRT;
+  staged_epilogue<EPI, 4>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), bm + (WR - 64) * wm, bn, wm, wn,
                           wid, lane, P.C, P.aux);
+  __syncthreads();
+  staged_epilogue<EPI, FRT - 4>(P, smem, reinterpret_cast<const f32x4(&)[FRT - 4][4]>(acc[4]),
+                                bm + (WR - 64) * wm + 64, bn, wm, wn, wid, lane, P.C, P.aux);
   stamp_end(P.stamps, t_start);
 }
 
@@ -635,11 +640,12 @@ int launch_dma(int epi, const GemmP& P, int tm, int tn, int nz, hipStream_t s) {
   return mms::check_launch("gemm_dma2");
 }
 
+template <int FRT>
 int launch_tall(int epi, const GemmP& P, int tm, int tn, hipStream_t s) {
   const int total = tm * tn;
   dim3 grid(total), block(NT);
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_tall_kernel<E>), grid, block, 0, s, P, tm, tn, total); break;
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_tall_kernel<E, FRT>), grid, block, 0, s, P, tm, tn, total); break;
     MMS_EPI_CASES
 #undef CASE
     default: mms::set_error("gemm: bad epilogue %d", epi); return 1;
@@ -1019,9 +1025,17 @@ extern "C" int mms2ut_gemm_set_dp(int mode) {
   return 0;
 }
 
-// 160-row NT tiles (gemm_tall_kernel) when they take fewer rounds of the 512 block slots than
-// 128-row ones, counting a 160-row tile as 1.3 128-row tiles (mms2ut_gemm_set_tall / env
-// MMS2UT_GEMM_TALL: 1 = by that rule (default), 0 = never, 2 = every qualifying NT shape).
+// Tall NT tiles (gemm_tall_kernel) by a round-count cost: a round of 160-row tiles costs 1.12
+// rounds of 128-row ones, a round of 192-row tiles 1.24 (isolated, one-round grids: the taller
+// tile reads less B per FLOP; profiles/round4_tall_ab.txt); the cheapest height wins, ties to the
+// shorter (mms2ut_gemm_set_tall / env MMS2UT_GEMM_TALL: 1 = by that rule (default), 0 = never,
+// 2 / 3 = 160 / 192 rows for every qualifying NT shape).
+#ifndef MMS_TALL_C160
+#define MMS_TALL_C160 112
+#endif
+#ifndef MMS_TALL_C192
+#define MMS_TALL_C192 124
+#endif
 static int g_tall_mode = -1;
 static int tall_mode() {
   if (g_tall_mode < 0) {
@@ -1030,15 +1044,22 @@ static int tall_mode() {
   }
   return g_tall_mode;
 }
-static bool tall_route(const mms2ut_gemm_args* a, int tm, int tn) {
+// -> the tile height (160 / 192), 0 = 128-row tiles
+static int tall_pick(const mms2ut_gemm_args* a, int tm, int tn) {
   const int mode = tall_mode();
-  if (mode == 0) return false;
-  if (mode == 2) return true;
-  const long r128 = ((long)tm * tn + 511) / 512, r160 = ((long)((a->M + BMT - 1) / BMT) * tn + 511) / 512;
-  return 13 * r160 < 10 * r128;
+  if (mode == 0) return 0;
+  if (mode == 2) return 160;
+  if (mode == 3) return 192;
+  auto rounds = [&](int bm) { return ((long)((a->M + bm - 1) / bm) * tn + 511) / 512; };
+  // costs in hundredths of a 128-row round
+  const long c128 = 100 * rounds(128), c160 = MMS_TALL_C160 * rounds(160), c192 = MMS_TALL_C192 * rounds(192);
+  (void)tm;
+  if (c160 < c128 && c160 <= c192) return 160;
+  if (c192 < c128) return 192;
+  return 0;
 }
 extern "C" int mms2ut_gemm_set_tall(int mode) {
-  MMS_REQUIRE(mode >= 0 && mode <= 2, "gemm_set_tall: mode must be 0..2 (got %d)", mode);
+  MMS_REQUIRE(mode >= 0 && mode <= 3, "gemm_set_tall: mode must be 0..3 (got %d)", mode);
   g_tall_mode = mode;
   return 0;
 }
@@ -1175,11 +1196,13 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
       return mmsg::launch_pp(a->epi, bm, P, tmp, tnp, s);
     }
   }
-  if (dma_ok && a_kc && b_kc && nz == 1 && tall_route(a, tm, tn)) {
-    const int tmt = (a->M + BMT - 1) / BMT;
-    P.group_m = group_m_for(tmt);
-    P.stamps = stamp_take((long)tmt * tn);
-    return launch_tall(a->epi, P, tmt, tn, s);
+  if (dma_ok && a_kc && b_kc && nz == 1) {
+    if (const int bmt = tall_pick(a, tm, tn)) {
+      const int tmt = (a->M + bmt - 1) / bmt;
+      P.group_m = group_m_for(tmt);
+      P.stamps = stamp_take((long)tmt * tn);
+      return bmt == 160 ? launch_tall<5>(a->epi, P, tmt, tn, s) : launch_tall<6>(a->epi, P, tmt, tn, s);
+    }
   }
   // (the deferred epilogue addresses C / aux / out2 through buffer descriptors: 31-bit extents)
   const long ep_ext = 2 * ((long)(a->M - 1) * std::max<long>({(long)a->ldc, (long)a->ldaux, (long)a->ldo2}) + 2L * a->N);

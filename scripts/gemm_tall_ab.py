@@ -1,5 +1,5 @@
 """Isolated A/B of the 128x128 NT kernel (tall mode 0) against the 160 x 128 one (mode 2) and the
-shape rule (mode 1) on the step's M x N x K shapes around the 512-slot round boundary; random fp16,
+192 x 128 one (mode 3) and the shape rule (mode 1) on the step's M x N x K shapes around the 512-slot round boundary; random fp16,
 warm, HIP events over 20 launches.  usage: python scripts/gemm_tall_ab.py"""
 import importlib
 import os
@@ -35,7 +35,7 @@ for M in (10000, 11001, 12000, 12160, 14000):
         out = torch.empty(M, N, dtype=torch.float16, device="cuda")
         epi = getattr(K, "EPI_" + name)
         res = {}
-        for mode in (0, 2, 1):
+        for mode in (0, 2, 3, 1):
             K.call("mms2ut_gemm_set_tall", mode)
             res[mode] = timeit(lambda: K.gemm(x, W, out, M, N, Kd, lda=Kd, ldb=Kd, ldc=N, epi=epi, bias=b,
                                               aux=aux if name == "DROP_RESID" else None, ldaux=N,
@@ -44,4 +44,4 @@ for M in (10000, 11001, 12000, 12160, 14000):
         K.call("mms2ut_gemm_set_tall", 1)
         tf = 2.0 * M * N * Kd / 1e12
         print(f"M={M:5d} N={N:4d} K={Kd:4d} {name:11s} t128 {res[0]:6.1f} us ({tf / res[0] * 1e6:5.0f} TF)  "
-              f"t160 {res[2]:6.1f} us ({tf / res[2] * 1e6:5.0f} TF)  rule {res[1]:6.1f}", flush=True)
+              f"t160 {res[2]:6.1f} us ({tf / res[2] * 1e6:5.0f} TF)  t192 {res[3]:6.1f}  rule {res[1]:6.1f}", flush=True)

@@ -187,9 +187,9 @@ def test_dp_gemm_bit_identical(M, N, K):
 @pytest.mark.parametrize("M,N,K", [(12000, 768, 768), (12000, 768, 3072), (11001, 768, 2304), (10000, 1000, 640),
                                    (300, 520, 64), (16384, 768, 192)])
 def test_tall_gemm_bit_identical(M, N, K):
-    """gemm_tall_kernel (160 x 128 NT tiles, gemm.hip) against the 128x128 LDS-DMA kernel on the same
-    operands: bit-identical for every fused epilogue, incl. ragged M (rows past M in the last
-    160-row tile), ragged N, short K, dropout counters; mode 2 forces the 160-row tiles."""
+    """gemm_tall_kernel (160 / 192 x 128 NT tiles, gemm.hip) against the 128x128 LDS-DMA kernel on
+    the same operands: bit-identical for every fused epilogue, incl. ragged M (rows past M in the
+    last tall tile), ragged N, short K, dropout counters; modes 2 / 3 force 160 / 192-row tiles."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     mm = pkg()
@@ -204,7 +204,7 @@ def test_tall_gemm_bit_identical(M, N, K):
         for name in _PP_EPIS:
             epi = getattr(K_, "EPI_" + name)
             outs = []
-            for mode in (0, 2):
+            for mode in (0, 2, 3):
                 K_.call("mms2ut_gemm_set_tall", mode)
                 out = c0.clone()
                 out2 = torch.zeros(M, N, dtype=torch.float16, device="cuda")
@@ -215,9 +215,10 @@ def test_tall_gemm_bit_identical(M, N, K):
                         p=p, seed=79, offset=7 * N, ld_rng=N, fixup=False)
                 outs.append((out, out2))
             torch.cuda.synchronize()
-            assert torch.equal(outs[1][0].view(torch.int16), outs[0][0].view(torch.int16)), name
-            assert torch.equal(outs[1][1].view(torch.int16), outs[0][1].view(torch.int16)), (name, "out2")
-        K_.call("mms2ut_gemm_set_tall", 2)
+            for mode, (o, o2) in zip((2, 3), outs[1:]):
+                assert torch.equal(o.view(torch.int16), outs[0][0].view(torch.int16)), (name, mode)
+                assert torch.equal(o2.view(torch.int16), outs[0][1].view(torch.int16)), (name, mode, "out2")
+        K_.call("mms2ut_gemm_set_tall", 3)
         got = K_.linear(x, W, b)
         ref = (x.float() @ W.float().t() + b.float())
         assert _rel(got, ref) < 2e-3
