@@ -707,8 +707,9 @@ def _group_ok(dy, x, dW):
 # grid cap of a grouped weight-gradient launch on the side stream (0: one block per tile).  A cap
 # makes the launch persistent: 128 blocks held their slots for ~600 us per layer and pushed the
 # critical path's 474-564-tile GEMMs into second rounds (22.4 ms per step against 18.1 uncapped
-# or at 512, 18.5 with no side stream; profiles/round3_v1_side_blocks_ab.json)
-SIDE_WGRAD_BLOCKS = 0
+# or at 512, 18.5 with no side stream; profiles/round3_v1_side_blocks_ab.json).  Env
+# MMS2UT_SIDE_WGRAD_BLOCKS overrides it (a multiple of 8; for A/B runs)
+SIDE_WGRAD_BLOCKS = int(os.environ.get("MMS2UT_SIDE_WGRAD_BLOCKS", "0"))
 
 
 def wgrad_group(problems, rows, max_blocks=0):
