@@ -98,11 +98,12 @@ int mms2ut_gemm_set_pp(int mode);
  * results).  mode 1: on, 0: off (default; env MMS2UT_GEMM_DP overrides it at first use), 2: only
  * K >= 1536, 3: only K < 1536.                                                                    */
 int mms2ut_gemm_set_dp(int mode);
-/* NT shapes (both operands K-contiguous, batch 1, no split) may run on 160 x 128 or 192 x 128 tiles
- * instead of 128 x 128 ones when that takes fewer rounds of the 512 block slots (e.g. M = 11-16 k
+/* NT shapes (both operands K-contiguous, batch 1, no split) may run on 96 / 160 / 192 x 128 tiles
+ * instead of 128 x 128 ones when that takes fewer rounds of the 512 block slots, or (96 rows) fills
+ * a short single round better, weighted by each height's measured per-round cost (e.g. M = 11-16 k
  * rows x N = 768: one round instead of two); bit-identical results.  mode 1: by that rule (default;
- * env MMS2UT_GEMM_TALL overrides it at first use), 0: never, 2 / 3: 160 / 192-row tiles for every
- * qualifying NT shape (tests).                                                                    */
+ * env MMS2UT_GEMM_TALL overrides it at first use), 0: never, 2 / 3 / 5: 160 / 192 / 96-row tiles
+ * for every qualifying NT shape (tests).                                                          */
 int mms2ut_gemm_set_tall(int mode);
 
 /* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the

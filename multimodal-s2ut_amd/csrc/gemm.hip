@@ -330,10 +330,12 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
 // ------------------------------------------------------------------------------------------
 template <int EPI, int FRT>
 __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
-  constexpr int BMT = 32 * FRT, TILE_T = BMT * 64 * 2, XW = (BMT - 128) / 32;   // XW: extra A rows' DMA per wave / 8
+  constexpr int BMT = 32 * FRT, TILE_T = BMT * 64 * 2;
+  // the ring, or the epilogue's 16 KiB staging area per wave if that is larger (96-row tiles)
+  constexpr int SMEM = 2 * (TILE_T + TILE_BYTES) > 4 * 64 * 64 * 4 ? 2 * (TILE_T + TILE_BYTES) : 4 * 64 * 64 * 4;
   const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
-  __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_T + TILE_BYTES)];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   int z, tm, tn;
   tile_coords(blockIdx.x, tiles_m, tiles_n, total, z, tm, tn, P.group_m);
   (void)z;   // batch 1 (host)
@@ -347,14 +349,13 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)P.B, (short)0, (int)b_ext, 0x00020000);
 #define SA(s) (smem + (s) * (TILE_T + TILE_BYTES))
 #define SB(s) (SA(s) + TILE_T)
-  // a tall A stage: the 128-row pattern (16 wave-instructions) and rows 128.. (XW more per wave,
-  // the same swizzled 8-row layout); rows past M read as zero through the descriptor
+  // an A stage of 32 FRT rows: 4 FRT wave-instructions of 8 rows (dma_tile's swizzled layout),
+  // FRT per wave; rows past M read as zero through the descriptor
   auto dma_a = [&](char* lds, int k0) {
-    dma_tile<true>(ra, lds, P.lda, bm, k0, wid, lane);
 #ifndef MMS_GEMM_NODMA
 #pragma unroll
-    for (int x = 0; x < XW; ++x) {
-      const int ins = 16 + wid * XW + x;
+    for (int x = 0; x < FRT; ++x) {
+      const int ins = wid * FRT + x;
       const int row = ins * 8 + (lane >> 3), c = (lane & 7) ^ (row & 7);
       const int voff = (int)(((long)(bm + row) * P.lda + k0 + c * 8) * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(lds + ins * 1024), 16, voff, 0, 0, 0);
@@ -404,12 +405,14 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
   __syncthreads();   // the ring is idle (the last k-step waited for vmcnt(0))
   // the wave's rows [bm + 16 FRT wm, + 16 FRT): fragments 0-3 (64 rows), then the rest, each
   // through the wave's 16 KiB staging area (staged_epilogue places wave rows at bm + 64 wm)
-  constexpr int WR = 16 * FRT;
-  staged_epilogue<EPI, 4>(P, smem, reinterpret_cast<const f32x4(&)[4][4]>(acc[0]), bm + (WR - 64) * wm, bn, wm, wn,
-                          wid, lane, P.C, P.aux);
-  __syncthreads();
-  staged_epilogue<EPI, FRT - 4>(P, smem, reinterpret_cast<const f32x4(&)[FRT - 4][4]>(acc[4]),
-                                bm + (WR - 64) * wm + 64, bn, wm, wn, wid, lane, P.C, P.aux);
+  constexpr int WR = 16 * FRT, F1 = FRT < 4 ? FRT : 4;
+  staged_epilogue<EPI, F1>(P, smem, reinterpret_cast<const f32x4(&)[F1][4]>(acc[0]), bm + (WR - 64) * wm, bn, wm,
+                           wn, wid, lane, P.C, P.aux);
+  if constexpr (FRT > 4) {
+    __syncthreads();
+    staged_epilogue<EPI, FRT - 4>(P, smem, reinterpret_cast<const f32x4(&)[FRT - 4][4]>(acc[4]),
+                                  bm + (WR - 64) * wm + 64, bn, wm, wn, wid, lane, P.C, P.aux);
+  }
   stamp_end(P.stamps, t_start);
 }
 
@@ -1036,6 +1039,9 @@ extern "C" int mms2ut_gemm_set_dp(int mode) {
 #ifndef MMS_TALL_C192
 #define MMS_TALL_C192 124
 #endif
+#ifndef MMS_TALL_C96   // 96-row tiles: a fuller single round for short grids; <= 0: never by the rule
+#define MMS_TALL_C96 89
+#endif
 static int g_tall_mode = -1;
 static int tall_mode() {
   if (g_tall_mode < 0) {
@@ -1050,16 +1056,20 @@ static int tall_pick(const mms2ut_gemm_args* a, int tm, int tn) {
   if (mode == 0) return 0;
   if (mode == 2) return 160;
   if (mode == 3) return 192;
+  if (mode == 5) return 96;
   auto rounds = [&](int bm) { return ((long)((a->M + bm - 1) / bm) * tn + 511) / 512; };
   // costs in hundredths of a 128-row round
   const long c128 = 100 * rounds(128), c160 = MMS_TALL_C160 * rounds(160), c192 = MMS_TALL_C192 * rounds(192);
-  (void)tm;
-  if (c160 < c128 && c160 <= c192) return 160;
-  if (c192 < c128) return 192;
-  return 0;
+  const long c96 = MMS_TALL_C96 > 0 ? MMS_TALL_C96 * rounds(96) : 1L << 40;
+  int best = 0;
+  long cb = c128;
+  if (c160 < cb) { best = 160; cb = c160; }
+  if (c192 < cb) { best = 192; cb = c192; }
+  if (c96 < cb) { best = 96; cb = c96; }
+  return best;
 }
 extern "C" int mms2ut_gemm_set_tall(int mode) {
-  MMS_REQUIRE(mode >= 0 && mode <= 3, "gemm_set_tall: mode must be 0..3 (got %d)", mode);
+  MMS_REQUIRE(mode >= 0 && mode <= 5 && mode != 4, "gemm_set_tall: mode must be 0..3 or 5 (got %d)", mode);
   g_tall_mode = mode;
   return 0;
 }
@@ -1201,6 +1211,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
       const int tmt = (a->M + bmt - 1) / bmt;
       P.group_m = group_m_for(tmt);
       P.stamps = stamp_take((long)tmt * tn);
+      if (bmt == 96) return launch_tall<3>(a->epi, P, tmt, tn, s);
       return bmt == 160 ? launch_tall<5>(a->epi, P, tmt, tn, s) : launch_tall<6>(a->epi, P, tmt, tn, s);
     }
   }

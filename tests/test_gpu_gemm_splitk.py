@@ -187,9 +187,9 @@ def test_dp_gemm_bit_identical(M, N, K):
 @pytest.mark.parametrize("M,N,K", [(12000, 768, 768), (12000, 768, 3072), (11001, 768, 2304), (10000, 1000, 640),
                                    (300, 520, 64), (16384, 768, 192)])
 def test_tall_gemm_bit_identical(M, N, K):
-    """gemm_tall_kernel (160 / 192 x 128 NT tiles, gemm.hip) against the 128x128 LDS-DMA kernel on
-    the same operands: bit-identical for every fused epilogue, incl. ragged M (rows past M in the
-    last tall tile), ragged N, short K, dropout counters; modes 2 / 3 force 160 / 192-row tiles."""
+    """gemm_tall_kernel (96 / 160 / 192 x 128 NT tiles, gemm.hip) against the 128x128 LDS-DMA kernel
+    on the same operands: bit-identical for every fused epilogue, incl. ragged M (rows past M in the
+    last tile), ragged N, short K, dropout counters; modes 2 / 3 / 5 force 160 / 192 / 96 rows."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     mm = pkg()
@@ -204,7 +204,7 @@ def test_tall_gemm_bit_identical(M, N, K):
         for name in _PP_EPIS:
             epi = getattr(K_, "EPI_" + name)
             outs = []
-            for mode in (0, 2, 3):
+            for mode in (0, 2, 3, 5):
                 K_.call("mms2ut_gemm_set_tall", mode)
                 out = c0.clone()
                 out2 = torch.zeros(M, N, dtype=torch.float16, device="cuda")
@@ -215,7 +215,7 @@ def test_tall_gemm_bit_identical(M, N, K):
                         p=p, seed=79, offset=7 * N, ld_rng=N, fixup=False)
                 outs.append((out, out2))
             torch.cuda.synchronize()
-            for mode, (o, o2) in zip((2, 3), outs[1:]):
+            for mode, (o, o2) in zip((2, 3, 5), outs[1:]):
                 assert torch.equal(o.view(torch.int16), outs[0][0].view(torch.int16)), (name, mode)
                 assert torch.equal(o2.view(torch.int16), outs[0][1].view(torch.int16)), (name, mode, "out2")
         K_.call("mms2ut_gemm_set_tall", 3)
