@@ -320,13 +320,13 @@ __global__ void __launch_bounds__(NT, (STAGES <= 2 ? 2 : 1)) gemm_dma_kernel(Gem
 }
 
 // ------------------------------------------------------------------------------------------
-// Tall NT tiles, 32 FRT x 128 (FRT = 5: 160 rows, 6: 192): each of the 4 waves owns 16 FRT rows
-// (FRT MFMA fragments) x 64 columns; 2-stage LDS-DMA ring of (4 FRT + 16) KiB stages, two blocks
-// per CU (192 rows: 80 KiB, exactly half the CU's LDS).  For NT grids just past a round of 128x128
-// tiles (e.g. M = 11-16 k rows x N = 768: 564 tiles of 128 rows for 512 block slots, a second
-// round for 52 of them) taller tiles fit fewer rounds at 1.25x / 1.5x the work per tile.  Same k
-// order, same MFMA operands per accumulator, same staged epilogue per element: bit-identical to
-// gemm_dma_kernel<true, true, EPI, 2>.
+// NT tiles of 32 FRT x 128 (FRT = 3: 96 rows, 5: 160, 6: 192): each of the 4 waves owns 16 FRT
+// rows (FRT MFMA fragments) x 64 columns; 2-stage LDS-DMA ring of (4 FRT + 16) KiB stages, two
+// blocks per CU (192 rows: 80 KiB, exactly half the CU's LDS).  For NT grids just past a round of
+// 128x128 tiles (e.g. M = 11-16 k rows x N = 768: 564 tiles of 128 rows for 512 block slots, a
+// second round for 52 of them) taller tiles fit fewer rounds at 1.25x / 1.5x the work per tile;
+// 96-row tiles fill a short single round better.  Same k order, same MFMA operands per
+// accumulator, same staged epilogue per element: bit-identical to gemm_dma_kernel<true, true, EPI, 2>.
 // ------------------------------------------------------------------------------------------
 template <int EPI, int FRT>
 __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, int tiles_n, int total) {
