@@ -28,6 +28,8 @@ const char* mms2ut_last_error(void);
  * (lower = more urgent): the trainer's critical-path and weight-gradient side streams, so that no
  * work a caller leaves on the legacy NULL stream implicitly orders itself behind them.           */
 int mms2ut_stream_create(int priority, hipStream_t* out);
+/* Destroys a stream from mms2ut_stream_create (after the work enqueued on it has completed).     */
+int mms2ut_stream_destroy(hipStream_t stream);
 int mms2ut_version(void);
 
 /* ---------------------------------------------------------------- GEMM (MFMA fp16, fp32 acc)
@@ -88,16 +90,6 @@ typedef struct mms2ut_gemm_args {
 } mms2ut_gemm_args;
 
 int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
-/* NT shapes (both operands K-contiguous, batch 1, no split) may run on the ping-pong 256-column
- * kernel instead of the 128x128 one (bit-identical results).  mode -1: automatic choice by shape,
- * 0: never (default; env MMS2UT_GEMM_PP overrides it at first use), 128 / 192 / 256: always, with
- * that tile height.  Process-global; for A/B measurements and tests.                            */
-int mms2ut_gemm_set_pp(int mode);
-/* NT shapes of more than one round of 128x128 tiles (> 512) run on a persistent kernel whose blocks
- * walk several tiles and finish each tile's epilogue inside the next tile's k-loop (bit-identical
- * results).  mode 1: on, 0: off (default; env MMS2UT_GEMM_DP overrides it at first use), 2: only
- * K >= 1536, 3: only K < 1536.                                                                    */
-int mms2ut_gemm_set_dp(int mode);
 /* NT shapes (both operands K-contiguous, batch 1, no split) may run on 96 / 160 / 192 x 128 tiles
  * instead of 128 x 128 ones when that takes fewer rounds of the 512 block slots, or (96 rows) fills
  * a short single round better, weighted by each height's measured per-round cost (e.g. M = 11-16 k

@@ -134,9 +134,8 @@ SIGNATURES = {
     "mms2ut_last_error": (C.c_char_p, []),
     "mms2ut_version": (i32, []),
     "mms2ut_stream_create": (i32, [i32, vp]),
+    "mms2ut_stream_destroy": (i32, [vp]),
     "mms2ut_gemm_f16": (i32, [vp, vp]),   # GEMM_ARGS.pack(...) bytes or C.byref(GemmArgs)
-    "mms2ut_gemm_set_pp": (i32, [i32]),
-    "mms2ut_gemm_set_dp": (i32, [i32]),
     "mms2ut_gemm_set_tall": (i32, [i32]),
     "mms2ut_wgrad_group": (i32, [vp, i32, i64, i32, vp]),
     "mms2ut_profile_begin": (i32, [i32]),

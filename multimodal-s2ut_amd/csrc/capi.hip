@@ -47,6 +47,19 @@ extern "C" int mms2ut_stream_create(int priority, hipStream_t* out) {
   return 0;
 }
 
+extern "C" int mms2ut_stream_destroy(hipStream_t stream) {
+  if (!stream) {
+    mms::set_error("stream_destroy: null stream");
+    return 1;
+  }
+  const hipError_t e = hipStreamDestroy(stream);
+  if (e != hipSuccess) {
+    mms::set_error("stream_destroy: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return 0;
+}
+
 namespace {
 __global__ void splitk_reduce_kernel(const float* __restrict__ slabs, int nsplit, long slab,
                                      int rows, int cols, void* out, long ldo, int out_f16,

@@ -479,7 +479,8 @@ extern "C" int mms2ut_fbank_f32(const float* wave, const int64_t* wave_off, cons
   if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fbank_kernel, 64 * FB_WAVES, 0) != hipSuccess ||
                       per_cu <= 0))
     per_cu = 4;
-  const int grid = std::min((total_frames + FB_WAVES - 1) / FB_WAVES, per_cu * ncu);
+  // a block consumes FR_W * FB_WAVES frames per sweep: no more blocks than that covers
+  const int grid = std::min((total_frames + FR_W * FB_WAVES - 1) / (FR_W * FB_WAVES), per_cu * ncu);
   hipLaunchKernelGGL(fbank_kernel, dim3(grid), dim3(64 * FB_WAVES), 0, s, wave, wave_off,
                      frame_off, B, total_frames, mel_banks, mel_range, nbins, feats);
   return mms::check_launch("fbank");

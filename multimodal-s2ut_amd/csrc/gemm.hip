@@ -982,52 +982,6 @@ extern "C" int mms2ut_profile_bytes(double* bytes) {
   return 0;
 }
 
-// Ping-pong 256-column kernel (gemm_pp.hip) for NT shapes.  Mode: -1 auto (pp_pick), 0 off (default),
-// 128 / 192 / 256 a forced tile height (A/B and tests; mms2ut_gemm_set_pp / MMS2UT_GEMM_PP).
-static int g_pp_mode = -2;
-static int pp_mode() {
-  if (g_pp_mode == -2) {
-    const char* e = getenv("MMS2UT_GEMM_PP");
-    g_pp_mode = e ? atoi(e) : 0;   // off by default: slower than the 128x128 kernel on the step's shapes so far
-  }
-  return g_pp_mode;
-}
-extern "C" int mms2ut_gemm_set_pp(int mode) {
-  MMS_REQUIRE(mode == -1 || mode == 0 || mode == 128 || mode == 192 || mode == 256,
-              "gemm_set_pp: mode must be -1, 0, 128, 192 or 256 (got %d)", mode);
-  g_pp_mode = mode;
-  return 0;
-}
-
-// Persistent deferred-epilogue kernel (gemm_dp.hip) for NT grids of more than one round of the
-// 512 block slots (mms2ut_gemm_set_dp / MMS2UT_GEMM_DP; 3 = the short-K (K < 1536) wide shapes
-// only).  Off by default: it won the step by 0.5-0.8 % (17.29-17.32 vs 17.43-17.48 ms, gpurun_out
-// r4o) until the epilogue dropout fast path shortened the one-tile-per-block kernel's C-store
-// phase; since then off is 0.2-0.4 % faster (16.77-16.88 vs 16.86-16.93 ms, and 17.38-17.47 vs
-// 17.41-17.46 over six interleaved pairs on a second box: profiles/round4_dp_ab.txt).
-static int g_dp_mode = -1;
-static int dp_mode() {
-  if (g_dp_mode < 0) {
-    const char* e = getenv("MMS2UT_GEMM_DP");
-    g_dp_mode = e ? atoi(e) : 0;
-  }
-  return g_dp_mode;
-}
-// mode 2: only K >= 1536 (the long-K, N = 768 projections); mode 3: only K < 1536
-static bool dp_route(const mms2ut_gemm_args* a) {
-  switch (dp_mode()) {
-    case 1: return true;
-    case 2: return a->K >= 1536;
-    case 3: return a->K < 1536;
-    default: return false;
-  }
-}
-extern "C" int mms2ut_gemm_set_dp(int mode) {
-  MMS_REQUIRE(mode >= 0 && mode <= 3, "gemm_set_dp: mode must be 0..3 (got %d)", mode);
-  g_dp_mode = mode;
-  return 0;
-}
-
 // Tall NT tiles (gemm_tall_kernel) by a round-count cost: a round of 160-row tiles costs 1.12
 // rounds of 128-row ones, a round of 192-row tiles 1.24 (isolated, one-round grids: the taller
 // tile reads less B per FLOP; profiles/round4_tall_ab.txt); the cheapest height wins, ties to the
@@ -1042,6 +996,19 @@ extern "C" int mms2ut_gemm_set_dp(int mode) {
 #ifndef MMS_TALL_C96   // 96-row tiles: a fuller single round for short grids; <= 0: never by the rule
 #define MMS_TALL_C96 89
 #endif
+// CUs of the current device (cached per device): the block slots a round of tiles fills
+static int gemm_cu_count() {
+  static int cached[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 static int g_tall_mode = -1;
 static int tall_mode() {
   if (g_tall_mode < 0) {
@@ -1057,10 +1024,15 @@ static int tall_pick(const mms2ut_gemm_args* a, int tm, int tn) {
   if (mode == 2) return 160;
   if (mode == 3) return 192;
   if (mode == 5) return 96;
-  auto rounds = [&](int bm) { return ((long)((a->M + bm - 1) / bm) * tn + 511) / 512; };
+  // a round = one block per slot: two blocks per CU (every NT kernel here holds <= 80 KiB of LDS
+  // and <= 256 VGPRs at 256 threads)
+  const long slots = 2L * gemm_cu_count();
+  auto rounds = [&](int bm) { return ((long)((a->M + bm - 1) / bm) * tn + slots - 1) / slots; };
   // costs in hundredths of a 128-row round
   const long c128 = 100 * rounds(128), c160 = MMS_TALL_C160 * rounds(160), c192 = MMS_TALL_C192 * rounds(192);
-  const long c96 = MMS_TALL_C96 > 0 ? MMS_TALL_C96 * rounds(96) : 1L << 40;
+  // 96-row tiles were measured on single-round grids of M = 4-7 k rows (profiles/round4_tall_ab.txt);
+  // below ~3 k rows (short batches, decode) the 128-row tile keeps the rule's measured range
+  const long c96 = MMS_TALL_C96 > 0 && a->M >= 3072 ? MMS_TALL_C96 * rounds(96) : 1L << 40;
   int best = 0;
   long cb = c128;
   if (c160 < cb) { best = 160; cb = c160; }
@@ -1072,24 +1044,6 @@ extern "C" int mms2ut_gemm_set_tall(int mode) {
   MMS_REQUIRE(mode >= 0 && mode <= 5 && mode != 4, "gemm_set_tall: mode must be 0..3 or 5 (got %d)", mode);
   g_tall_mode = mode;
   return 0;
-}
-
-// Tile height of the ping-pong kernel for an NT shape, 0 = use the 128x128 kernel.  One block per
-// CU: a launch of t tiles takes ceil(t / 256) rounds, each as long as one BM x 256 tile, so the
-// height that fills the last round best wins (per-tile cost ~ BM + a fixed 48-row overhead for
-// the prologue fill and the epilogue).
-static int pp_pick(const mms2ut_gemm_args* a) {
-  const int mode = pp_mode();
-  if (mode >= 0) return mode;
-  if (a->M < 2048 || a->N < 2304) return 0;
-  int best = 0;
-  long best_cost = 0;
-  for (int bm : {256, 192, 128}) {
-    const long tiles = (long)((a->M + bm - 1) / bm) * ((a->N + 255) / 256);
-    const long cost = (tiles + 255) / 256 * (bm + 48);
-    if (!best || cost < best_cost) { best = bm; best_cost = cost; }
-  }
-  return best;
 }
 
 // 256x256-tile kernel or the 128x128 one
@@ -1197,15 +1151,6 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     hipLaunchKernelGGL((gemm_dma_kernel<false, false, MMS_EPI_F32, 2, true>), grid, block, 0, s, P, tm, tn, tm * tn * nz);
     return mms::check_launch("gemm_dma_rs");
   }
-  if (a_kc && b_kc && nz == 1 && a->K % 32 == 0 && a_ext * 2 < (1L << 31) && b_ext * 2 < (1L << 31)) {
-    const int bm = pp_pick(a);
-    if (bm) {
-      const int tmp = (a->M + bm - 1) / bm, tnp = (a->N + 255) / 256;
-      P.group_m = group_m_for(tmp);
-      P.stamps = stamp_take((long)tmp * tnp);
-      return mmsg::launch_pp(a->epi, bm, P, tmp, tnp, s);
-    }
-  }
   if (dma_ok && a_kc && b_kc && nz == 1) {
     if (const int bmt = tall_pick(a, tm, tn)) {
       const int tmt = (a->M + bmt - 1) / bmt;
@@ -1214,14 +1159,6 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
       if (bmt == 96) return launch_tall<3>(a->epi, P, tmt, tn, s);
       return bmt == 160 ? launch_tall<5>(a->epi, P, tmt, tn, s) : launch_tall<6>(a->epi, P, tmt, tn, s);
     }
-  }
-  // (the deferred epilogue addresses C / aux / out2 through buffer descriptors: 31-bit extents)
-  const long ep_ext = 2 * ((long)(a->M - 1) * std::max<long>({(long)a->ldc, (long)a->ldaux, (long)a->ldo2}) + 2L * a->N);
-  if (dma_ok && a_kc && b_kc && nz == 1 && a->epi != MMS_EPI_F32 && P.vec16 && a->N % 4 == 0 &&
-      (long)tm * tn > 512 && a->K >= 10 * BK && ep_ext < (1L << 31) && dp_route(a)) {
-    const int grid = 512;   // two blocks per CU, each walking its XCD's tiles
-    P.stamps = stamp_take(grid);
-    return mmsg::launch_dp(a->epi, P, tm, tn, grid, s);
   }
   if (dma_ok) {
     if (use_256(a, nz)) {

@@ -1,11 +1,11 @@
-// Shared pieces of the MFMA GEMM kernels (gemm.hip: 128x128 / 256x256 tiles; gemm_pp.hip: the
-// ping-pong 256-wide tile): launch parameters, tile order, LDS fragment reads, fused epilogues.
-// Included by both; everything but GemmP and launch_pp has internal linkage.
+// Shared pieces of the MFMA GEMM kernels (gemm.hip: 128x128 / tall / 256x256 tiles; the GEMM lab,
+// scripts/micro): launch parameters, tile order, LDS fragment reads, fused epilogues.  Everything
+// but GemmP has internal linkage.
 #pragma once
 #include "common.h"
 #include "../../include/mms2ut.h"
 
-// Launch parameters of every GEMM kernel (external linkage: gemm.hip and gemm_pp.hip share it)
+// Launch parameters of every GEMM kernel
 namespace mmsg {
 struct GemmP {
   const h16* A; const h16* B; void* C;
@@ -27,10 +27,6 @@ struct GemmP {
   unsigned long long* stamps;  // profiling: per block {first, last} s_memrealtime tick, or null
 };
 
-// ping-pong 256-column NT kernel (gemm_pp.hip): tile height bm (128 / 192 / 256) x 256 columns
-int launch_pp(int epi, int bm, const GemmP& P, int tiles_m, int tiles_n, hipStream_t s);
-// persistent 128x128 NT kernel with the deferred epilogue (gemm_dp.hip) on `grid` blocks
-int launch_dp(int epi, const GemmP& P, int tiles_m, int tiles_n, int grid, hipStream_t s);
 }  // namespace mmsg
 
 namespace {

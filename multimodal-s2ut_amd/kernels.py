@@ -3,6 +3,7 @@
 Every function enqueues HIP kernels on PyTorch's current stream through libmms2ut_hip.so.
 Tensors are fp16 (``torch.float16``) unless stated; shapes are checked before the call.
 """
+import atexit
 import ctypes
 import math
 import os
@@ -401,8 +402,11 @@ class ConvCall:
             self.a.wt[i] = 0 if img is None else img.data_ptr()
         self.wt_of = wt
 
-    def sizes(self):
-        a = self.a
+    def sizes(self, a=None):
+        """Arena / scratch / workspace sizes of the call described by `a` (the live argument block
+        by default; a backward passes its forward's snapshot, which a later forward of the same
+        call may have overwritten in self.a)."""
+        a = self.a if a is None else a
         key = (a.B, a.T, a.C, a.nlayers, tuple(a.k), tuple(a.cout))
         s = ConvCall._sizes.get(key)
         if s is None:
@@ -435,7 +439,7 @@ class ConvCall:
 
     def bwd(self, snap, arena, dy):
         """Backward of the forward whose argument snapshot is ``snap`` (weight / bias gradients)."""
-        nb, _, sbytes, mw, sw = self.sizes()
+        nb, _, sbytes, mw, sw = self.sizes(_lib.ConvArgs.from_buffer_copy(snap))
         dev = dy.device
         scratch = torch.empty(sbytes, dtype=torch.uint8, device=dev)
         if TransposedWeights.active is not None:
@@ -487,8 +491,9 @@ class FusionCall:
             setattr(self.a, f, 0 if img is None else img.data_ptr())
         self.wt_of = wt
 
-    def sizes(self, want_dimg):
-        a = self.a
+    def sizes(self, want_dimg, a=None):
+        """As ConvCall.sizes: `a` = a forward's argument snapshot (default: the live block)."""
+        a = self.a if a is None else a
         key = (a.B, a.Te, a.Ti, a.Di, a.d, a.extra, a.gate, a.image_pre_norm, a.p_img > 0, a.p_txt > 0, a.p_attn > 0,
                bool(want_dimg))
         s = FusionCall._sizes.get(key)
@@ -526,7 +531,7 @@ class FusionCall:
     def bwd(self, snap, arena, keep, dres, want_dimg=False):
         """-> d(text) [B*Te, d] (and d(img) [B*Ti, Di] with want_dimg)."""
         a = _lib.FusionArgs.from_buffer_copy(snap)
-        _, _, sbytes, so, mw, sw = self.sizes(want_dimg)
+        _, _, sbytes, so, mw, sw = self.sizes(want_dimg, a)
         dev = dres.device
         scratch = torch.empty(sbytes, dtype=torch.uint8, device=dev)
         if TransposedWeights.active is not None:
@@ -626,14 +631,38 @@ class _SideRegion:
 _SIDE_REGION = _SideRegion()
 
 
+_STREAMS = {}   # (device index, priority) -> ExternalStream, one per process
+
+
 def make_stream(device, priority):
     """A non-blocking stream (include/mms2ut.h mms2ut_stream_create) wrapped for torch: work a
     caller leaves on the legacy NULL stream does not implicitly wait for it (measured equal to
-    torch's pool streams in the bench, 17.05 vs 17.01-17.08 ms, round 4)."""
-    with torch.cuda.device(device):
-        h = ctypes.c_void_p()
-        call("mms2ut_stream_create", int(priority), ctypes.addressof(h))
-        return torch.cuda.ExternalStream(h.value, device=device)
+    torch's pool streams in the bench, 17.05 vs 17.01-17.08 ms, round 4).  One stream per
+    (device, priority) for the process: every Trainer reuses it, so building many trainers (test
+    suites, tools) creates no more HIP streams (ExternalStream never destroys its handle; the cached
+    ones are destroyed at exit, mms2ut_stream_destroy)."""
+    dev = torch.device(device)
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), int(priority))
+    s = _STREAMS.get(key)
+    if s is None:
+        with torch.cuda.device(key[0]):
+            h = ctypes.c_void_p()
+            call("mms2ut_stream_create", int(priority), ctypes.addressof(h))
+            s = torch.cuda.ExternalStream(h.value, device=dev)
+        if not _STREAMS:
+            atexit.register(_destroy_streams)
+        _STREAMS[key] = s
+    return s
+
+
+def _destroy_streams():
+    for s in _STREAMS.values():
+        try:
+            s.synchronize()
+            _lib.load().mms2ut_stream_destroy(ctypes.c_void_p(s.cuda_stream))
+        except Exception:   # interpreter teardown: the runtime may already be gone
+            pass
+    _STREAMS.clear()
 
 
 def make_side_stream(device):

@@ -18,6 +18,7 @@ Reference path restated here:
   fairseq TransformerUnitDecoder             (6 pre-LN layers, tied output projection)
 """
 import math
+import os
 import re
 from collections import OrderedDict
 
@@ -112,6 +113,8 @@ def _decoder_param_specs(S, spec, mha, ln):
     S.append((f"{p0}.embed_tokens.weight", (spec.V, dd)))
 
 EXT = "encoder.multimodal_transformer.0"
+# parameters of the fusion tail (mm_s2s_transformer.py:471-622) and its image-side extractors
+FUSION_PREFIXES = ("encoder.gate", "encoder.multimodal", "encoder.selective", "encoder.image", "encoder.q_former")
 
 
 def external_dims(cfg):
@@ -315,6 +318,9 @@ class ParamStore:
         self.g = {k: self.view(k, grad=True) for k in self.offsets}
         self.groups = self._forward_groups()
         self.pending = {}   # group -> event of its (deferred) optimizer update, see await_group
+        # The backward writes every gradient outright (or zeroes the ones a branch skips), so the
+        # trainer never clears this buffer; True restores a per-micro-batch fill (A/B, tests).
+        self.zero_each_step = os.environ.get("MMS2UT_GRAD_ZERO") == "1"
 
     @staticmethod
     def group_of(name):
@@ -651,6 +657,15 @@ class MMS2UTModel:
 
     def P(self, n):
         return self.params.p[n]
+
+    def _zero_grads(self, prefixes):
+        """Zero the gradients of every parameter whose name starts with one of `prefixes`: a branch
+        whose backward does not run leaves them untouched this step, and nothing else clears the
+        gradient buffer (every other gradient is written outright by its backward, see
+        ParamStore)."""
+        for n, _ in self.params.specs:
+            if n.startswith(prefixes):
+                self.params.g[n].zero_()
 
     def G(self, n):
         return self.params.g[n]
@@ -1354,6 +1369,9 @@ class MMS2UTModel:
         N = ctx["N"]
         d = dout
         out = {}
+        # the shared layer_norm1 gradient is summed over the layers above layer 0 (dgb_accumulate;
+        # with one layer it is unused and stays 0)
+        self.params.span(EXT + ".layer_norm1.weight", EXT + ".layer_norm1.bias", grad=True).zero_()
         for i in reversed(range(N)):
             dinp = self.ext_layer_bwd(i, ctx["layers"][i], d)
             ctx["layers"][i] = None
@@ -1606,7 +1624,8 @@ class MMS2UTModel:
                 l = L - N + i
                 dstates[l] = g if l not in dstates else K.add_f16(dstates[l], g)
             self._ready(EXT + ".layer_norm1.bias")
-            self._ready("encoder.layer_norm.bias")   # unused by this fusion type: its gradient stays 0
+            self._zero_grads(("encoder.layer_norm.",))   # unused by this fusion type: its gradient is 0
+            self._ready("encoder.layer_norm.bias")
             return self._encoder_layers_bwd(ctx, dstates.pop(L - 1), None, dstates)
         qf = ctx.get("qformer")
         dimg = None
@@ -1615,15 +1634,19 @@ class MMS2UTModel:
                 denc, dimg = self.fusion_bwd(ctx["fusion"], denc, want_dimg=True)
             else:
                 denc = self.fusion_bwd(ctx["fusion"], denc)
+                if qf is not None:      # zeroed images (requires_grad=False): no QFormer gradient
+                    self._zero_grads((QF + ".",))
+            if not self.cfg["use_selective_gate"]:   # built by the reference, unused without the gate
+                self._zero_grads(("encoder.gate_denses.",))
+        elif self.cfg["fusion"]:        # a batch without image features: the fusion tail did not run
+            self._zero_grads(FUSION_PREFIXES)
         if dimg is not None:
             # the QFormer read the (pre-modality-dropout) encoder output as its query layers'
             # memory: that gradient reaches the encoder even when the audio branch was dropped
             if ctx.get("audio_dropped"):
                 denc = torch.zeros_like(denc)
             self.qformer_bwd(qf, dimg.view(-1, dimg.shape[-1]), denc)
-        last_fusion = [n for n, _ in self.params.specs if n.startswith(("encoder.gate", "encoder.multimodal",
-                                                                         "encoder.selective", "encoder.image",
-                                                                         "encoder.q_former"))]
+        last_fusion = [n for n, _ in self.params.specs if n.startswith(FUSION_PREFIXES)]
         if last_fusion:
             self._ready(last_fusion[-1])
         if ctx.get("audio_dropped") and dimg is not None:
@@ -1631,8 +1654,9 @@ class MMS2UTModel:
         elif ctx.get("audio_dropped") and not dstates:
             # the reference replaces encoder_out by zeros_like(..., requires_grad=False)
             # (mm_s2s_transformer.py:500): no gradient reaches the encoder, whose gradients stay
-            # at the step's zeros -- skip its whole backward, only flush the reducer
+            # at zero -- skip its whole backward, zero its gradients, flush the reducer
             ctx["layers"] = None
+            self._zero_grads(("encoder.layer_norm.", "encoder.transformer_layers.", "encoder.subsample."))
             self._ready(None)
             return
         elif ctx.get("audio_dropped"):

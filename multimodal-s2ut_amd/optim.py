@@ -85,14 +85,6 @@ class FP16Adam:
                 ev = torch.cuda.Event()
                 ev.record(side)
                 ps.pending[grp] = ev
-            # the gradients are consumed: zero them here, behind the last chunk on the side stream,
-            # so the fill overlaps the next forward instead of sitting on the critical path (the
-            # next step's await_all orders it before any gradient write)
-            ps.grad.zero_()
-            ev = torch.cuda.Event()
-            ev.record(side)
-            ps.pending["__grad_zero__"] = ev
-            ps.grad_zeroed = True
 
     def check_fatal(self, st=None):
         """Raise fairseq's FloatingPointError if the device state turned FATAL (sticky: an

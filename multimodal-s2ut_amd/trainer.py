@@ -22,8 +22,7 @@ state vector).  The modality-dropout draws (two numpy draws per forward, as the 
 made before the step and select the graph.  Batches must stay resident (the graph bakes their
 device pointers): the first step on a new batch runs eagerly, then captures.
 
-Buffer access: the Adam update and the gradient zeroing run deferred on the side stream
-(optim.FP16Adam.step).  Call ``trainer.sync()`` (or ``model.params.await_all()``) before reading
+Buffer access: the Adam update runs deferred on the side stream (optim.FP16Adam.step).  Call ``trainer.sync()`` (or ``model.params.await_all()``) before reading
 ``params.flat`` / ``params.grad`` / ``opt.master`` directly after a step; ``state_dict``,
 ``opt.stats`` and the next forward wait by themselves.
 """
@@ -203,13 +202,14 @@ class Trainer:
                 self.reducer.acc = self.acc if n > 1 else None
                 m.grad_ready_hook = self.reducer.ready
             logits, aux = runtime.model_outputs(m, batch)
-            # zeroed after the forward: by then every deferred optimizer chunk of the previous step
-            # (which reads the gradients) has been waited for (ParamStore.await_group).  Every
-            # micro-batch starts from zero (a backward writes, not adds, most of its gradients).
+            # The hand-written backward defines every gradient outright: each parameter's gradient
+            # is written (not added to) by its backward, or zeroed where a branch skips it
+            # (model._zero_grads), so the flat buffer is never cleared as a whole (that fill moved
+            # 301 MB per step).  By now every deferred optimizer chunk of the previous step (which
+            # reads the gradients) has been waited for (ParamStore.await_group).
             m.params.await_all()
-            if i > 0 or not getattr(m.params, "grad_zeroed", False):
+            if m.params.zero_each_step:
                 m.params.grad.zero_()
-            m.params.grad_zeroed = False
             loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
                                                   cfg["label_smoothing"], cfg["padding_idx"])
             del logits

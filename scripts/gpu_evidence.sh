@@ -15,7 +15,6 @@
 #   attn_bits    O / LSE / dQKV dumps of this build and of $AB_LIB, compared bit for bit
 #   attn_bench   isolated attention timings of this build (and of $AB_LIB when set)
 #   gemm_bench   isolated NT GEMM timings on the step's shapes (scripts/gemm_bits.py) of this build (and $AB_LIB)
-#   gemm_pp      isolated A/B of the 128x128 and ping-pong NT kernels on the step's shapes (scripts/gemm_pp_ab.py)
 #   test         pytest on $TEST (a file or node id), verbose
 #   gemm_bits    GEMM output dumps of this build and of $AB_LIB, compared bit for bit
 #   lib_ab       step A/B: bench.py interleaved $AB_REPS times over "default" and $AB_LIB
@@ -51,7 +50,6 @@ for s in "$@"; do
     gemm_bench)
       run gemm_bench 200 python scripts/gemm_bits.py /tmp/gemm_t.npz
       if [ -n "$AB_LIB" ]; then run gemm_bench_ab 200 env MMS2UT_LIB="$AB_LIB" python scripts/gemm_bits.py /tmp/gemm_t.npz; fi ;;
-    gemm_pp) run gemm_pp 300 python scripts/gemm_pp_ab.py "$O/gemm_pp_ab.json" ;;
     test) run "test_${TEST//[^a-zA-Z0-9_]/_}" 600 python -u -m pytest "$TEST" -x -v --timeout 120 --timeout-method thread ;;
     gemm_bits)
       run gemm_dump_new 120 python scripts/gemm_bits.py /tmp/gemm_new.npz

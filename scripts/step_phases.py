@@ -36,9 +36,8 @@ def main():
             batch.src = fe(wb)
             logits, aux = runtime.model_outputs(m, [batch][0])
             m.params.await_all()
-            if not getattr(m.params, "grad_zeroed", False):
+            if m.params.zero_each_step:
                 m.params.grad.zero_()
-            m.params.grad_zeroed = False
             loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"], cfg["label_smoothing"],
                                                   cfg["padding_idx"])
             del logits

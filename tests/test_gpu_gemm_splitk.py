@@ -97,91 +97,8 @@ def test_fixup_accumulate_dgrad():
     assert _rel(outs[1], exact) < 2e-3
 
 
-# ------------------------------------------------------------------ ping-pong 256-column kernel
+# ------------------------------------------------------------------ tall NT tiles
 _PP_EPIS = ["F16", "RELU_DROP", "DROP_RESID", "RELU_DROP_BWD", "GATE", "F16_ACC", "GELU_DROP", "GELU_DROP_BWD"]
-
-
-@pytest.mark.parametrize("M,N,K", [(10000, 3072, 768), (1000, 2304, 768), (777, 1000, 96), (300, 520, 32),
-                                   (2500, 768, 3072), (129, 256, 64)])
-def test_pp_gemm_bit_identical(M, N, K):
-    """gemm_pp.hip (ping-pong BM x 256 tiles, one block per CU) against the 128x128 LDS-DMA kernel on
-    the same operands: bit-identical for every tile height and fused epilogue (same k-chunk order,
-    same MFMA, same staged epilogue), incl. ragged M / N, K of 1-3 slots (ring not yet full) and
-    dropout counters."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    mm = pkg()
-    K_ = mm.kernels
-    g = torch.Generator(device="cuda").manual_seed(M + N + K)
-    x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
-    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).half()
-    b = (torch.randn(N, device="cuda", generator=g) * 0.1).half()
-    aux = torch.randn(M, 2 * N, device="cuda", generator=g).half()
-    c0 = torch.randn(M, N, device="cuda", generator=g).half()
-    try:
-        for name in _PP_EPIS:
-            epi = getattr(K_, "EPI_" + name)
-            outs = []
-            for mode in (0, 128, 192, 256):
-                K_.call("mms2ut_gemm_set_pp", mode)
-                out = c0.clone()
-                out2 = torch.zeros(M, N, dtype=torch.float16, device="cuda")
-                p = 0.1 if name in ("RELU_DROP", "DROP_RESID", "GELU_DROP", "GELU_DROP_BWD", "RELU_DROP_BWD") else 0.0
-                K_.gemm(x, W, out, M, N, K, lda=K, ldb=K, ldc=N, epi=epi, bias=b,
-                        aux=aux if name in ("DROP_RESID", "RELU_DROP_BWD", "GATE", "GELU_DROP_BWD") else None,
-                        ldaux=2 * N, out2=out2 if name in ("GATE", "GELU_DROP") else None, ldo2=N,
-                        p=p, seed=77, offset=5 * N, ld_rng=N, fixup=False)
-                outs.append((out, out2))
-            torch.cuda.synchronize()
-            for mode, (o, o2) in zip((128, 192, 256), outs[1:]):
-                assert torch.equal(o.view(torch.int16), outs[0][0].view(torch.int16)), (name, mode)
-                assert torch.equal(o2.view(torch.int16), outs[0][1].view(torch.int16)), (name, mode, "out2")
-        ref = (x.float() @ W.float().t() + b.float())
-        K_.call("mms2ut_gemm_set_pp", 256)
-        got = K_.linear(x, W, b)
-        assert _rel(got, ref) < 2e-3
-    finally:
-        K_.call("mms2ut_gemm_set_pp", 0)   # the library default (off)
-
-
-@pytest.mark.parametrize("M,N,K", [(10000, 3072, 768), (9001, 2304, 768), (12000, 768, 3072), (9000, 1000, 640),
-                                   (9000, 1000, 704), (4500, 3072, 832)])
-def test_dp_gemm_bit_identical(M, N, K):
-    """gemm_dp.hip (persistent blocks, each tile's epilogue run inside the next tile's k-loop, the
-    next tile's first stage prefetched) against the one-tile-per-block 128x128 kernel: bit-identical
-    outputs for every fused epilogue, incl. ragged M / N, the shortest routed K (10 k-steps) and odd
-    k-step counts (ring parity carried across tiles).  Tiles come from per-XCD atomic ticket queues,
-    so the repeated launches also check that each launch's counters are reset for the next."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    mm = pkg()
-    K_ = mm.kernels
-    assert -(-M // 128) * -(-N // 128) > 512
-    g = torch.Generator(device="cuda").manual_seed(M + N + K + 1)
-    x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
-    W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).half()
-    b = (torch.randn(N, device="cuda", generator=g) * 0.1).half()
-    aux = torch.randn(M, 2 * N, device="cuda", generator=g).half()
-    c0 = torch.randn(M, N, device="cuda", generator=g).half()
-    try:
-        for name in _PP_EPIS:
-            epi = getattr(K_, "EPI_" + name)
-            outs = []
-            for mode in (0, 1):
-                K_.call("mms2ut_gemm_set_dp", mode)
-                out = c0.clone()
-                out2 = torch.zeros(M, N, dtype=torch.float16, device="cuda")
-                p = 0.1 if name in ("RELU_DROP", "DROP_RESID", "GELU_DROP", "GELU_DROP_BWD", "RELU_DROP_BWD") else 0.0
-                K_.gemm(x, W, out, M, N, K, lda=K, ldb=K, ldc=N, epi=epi, bias=b,
-                        aux=aux if name in ("DROP_RESID", "RELU_DROP_BWD", "GATE", "GELU_DROP_BWD") else None,
-                        ldaux=2 * N, out2=out2 if name in ("GATE", "GELU_DROP") else None, ldo2=N,
-                        p=p, seed=78, offset=3 * N, ld_rng=N, fixup=False)
-                outs.append((out, out2))
-            torch.cuda.synchronize()
-            assert torch.equal(outs[1][0].view(torch.int16), outs[0][0].view(torch.int16)), name
-            assert torch.equal(outs[1][1].view(torch.int16), outs[0][1].view(torch.int16)), (name, "out2")
-    finally:
-        K_.call("mms2ut_gemm_set_dp", 0)   # the library default
 
 
 @pytest.mark.parametrize("M,N,K", [(12000, 768, 768), (12000, 768, 3072), (11001, 768, 2304), (10000, 1000, 640),
