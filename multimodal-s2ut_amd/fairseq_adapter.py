@@ -41,23 +41,68 @@ from . import manifest as M
 from . import plugins, runtime
 
 
-class _ParamBridge(torch.autograd.Function):
-    """Connects fairseq's per-name parameters to the model node.  Forward: zero the flat gradient
-    buffer (the hand-written backward writes it) and hand out an anchor; backward (reached after
-    the model node's backward has filled the flat gradient and joined its side stream): every
-    parameter's gradient = its view of the flat gradient buffer (autograd accumulates it into
-    ``p.grad``, so fairseq's --update-freq accumulation holds)."""
+class _GroupBridge(torch.autograd.Function):
+    """The gradient hand-off of one parameter group (a contiguous run of the flat layout, e.g. one
+    encoder layer).  Its output is a graph root of its own, not connected to the loss: the
+    hand-written backward runs this node's backward re-entrantly (torch.autograd.backward from
+    inside runtime._ModelFn.backward) as soon as the group's gradients are final, and the backward
+    hands autograd each parameter's view of the flat gradient buffer.  AccumulateGrad adds it into
+    ``p.grad`` (fairseq's --update-freq accumulation) and fires torch DDP's per-parameter hook, so
+    DDP's bucket all-reduces start while the rest of the backward still runs (fairseq
+    distributed_fairseq_model wraps the model in DDP, bucket_cap_mb 25)."""
 
     @staticmethod
     def forward(fctx, net, names, *params):
         fctx.net, fctx.names = net, names
-        net.params.grad.zero_()
-        return net.anchor.detach().clone()
+        return torch.zeros(1, dtype=torch.float32, device=params[0].device)
 
     @staticmethod
     def backward(fctx, g):
         P = fctx.net.params
         return (None, None, *[P.g[n] for n in fctx.names])
+
+
+class _GradRelease:
+    """Installed as the model's ``grad_ready_hook`` for one forward/backward.  The backward calls
+    ``ready(offset)`` each time the flat gradient below ``offset`` is final (after every layer);
+    a group is released two ready points later, once the current stream has waited for the
+    weight-gradient side stream's work up to that older point (an event recorded then) — so the
+    main stream never waits for the layer whose weight gradients are still running beside its
+    dgrad chain.  ``finish()`` (after the side stream is joined) releases the rest."""
+
+    LAG = 2
+
+    def __init__(self, net, groups):
+        self.net, self.groups = net, list(groups)   # [(end offset, anchor)] in release order
+        self.marks = []     # (offset, side-stream event or None) per ready point
+        self.next = 0
+
+    def _release(self, upto):
+        todo = []
+        while self.next < len(self.groups) and self.groups[self.next][0] <= upto:
+            todo.append(self.groups[self.next][1])
+            self.next += 1
+        if todo:
+            torch.autograd.backward(todo, [torch.ones_like(a) for a in todo])
+
+    def ready(self, upto):
+        from . import kernels as K
+        side = K._Side.stream if K._Side.used else None
+        ev = None
+        if side is not None:
+            ev = torch.cuda.Event()
+            ev.record(side)
+        self.marks.append((upto, ev))
+        if len(self.marks) > self.LAG:
+            off, old = self.marks[-1 - self.LAG]
+            if old is not None:
+                torch.cuda.current_stream().wait_event(old)
+            self._release(off)
+
+    def finish(self):
+        self._release(self.net.params.numel)
+        self.net.grad_ready_hook = None
+        self.net.grad_release_finish = None
 
 
 def _module_path(root, dotted):
@@ -223,6 +268,14 @@ def register(fairseq):
             m, leaf = _module_path(self, "decoder.output_projection.weight")
             m.register_parameter(leaf, self.get_parameter("decoder.embed_tokens.weight"))
             self._params = [self.get_parameter(n) for n in self._names]
+            # release groups: the forward-consumption groups of the flat layout, in the order the
+            # backward completes them (ascending end offset)
+            self._groups = []
+            for _, a, b in sorted(P.groups, key=lambda g: g[2]):
+                names = [n for n in self._names if a <= P.offsets[n][0] < b]
+                if names:   # final once the backward reports its last parameter's end (model._ready)
+                    end = max(P.offsets[n][0] + P.offsets[n][2] for n in names)
+                    self._groups.append((end, names, [self.get_parameter(n) for n in names]))
             self.encoder_adapter, self.decoder_adapter = impl.encoder, impl.decoder
             self.multitask_decoders = {}
 
@@ -262,8 +315,10 @@ def register(fairseq):
             impl, net = self.impl, self.impl.net
             batch = impl._batch(src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list,
                                 extra_input=kw)
-            anchor = _ParamBridge.apply(net, self._names, *self._params)
-            outs = runtime._ModelFn.apply(anchor, net, batch, True)
+            if torch.is_grad_enabled():
+                rel = _GradRelease(net, [(end, _GroupBridge.apply(net, names, *ps)) for end, names, ps in self._groups])
+                net.grad_ready_hook, net.grad_release_finish = rel.ready, rel.finish
+            outs = runtime._ModelFn.apply(net.anchor, net, batch, True)
             logits = outs[0]
             B, Tt = prev_output_tokens.shape
             cfg = impl.cfg

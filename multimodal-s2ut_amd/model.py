@@ -636,6 +636,7 @@ class MMS2UTModel:
 
     # -------------------------------------------------------------- helpers
     grad_ready_hook = None  # callable(offset): grads [0, offset) of the flat buffer are final
+    grad_release_finish = None  # callable(): after the backward joined its side stream (fairseq_adapter)
 
     def _ready(self, last_param=None):
         if self.grad_ready_hook is None:

@@ -155,9 +155,7 @@ class _ModelFn(torch.autograd.Function):
         model.last_aux_losses = alog
         fctx.model = model
         fctx.saved = (ectx, dctx, enc, batch, actx, Te)
-        # an anchor other than the model's own leaf comes from fairseq_adapter's parameter bridge,
-        # whose backward (handing out the flat gradient per parameter) must be reached
-        fctx.bridged = anchor is not model.anchor
+        fctx.bridged = anchor is not model.anchor   # a caller-provided anchor must get a gradient
         if aux is None:
             aux = torch.zeros(1, dtype=torch.float32, device=logits.device)
         if not states:
@@ -193,6 +191,9 @@ class _ModelFn(torch.autograd.Function):
         _add_state_grads(dstates, {j: g for j, g in enumerate(dhidden[:n_enc]) if g is not None})
         model.encoder_backward(ectx, denc, dstates or None)
         K.side_join()  # weight gradients (side stream) complete before anyone reads them
+        fin = getattr(model, "grad_release_finish", None)
+        if fin is not None:     # fairseq_adapter: hand the last parameter groups to autograd
+            fin()
         if prof is not None:
             prof.disable()
         BWD_CPU_S[0] += time.thread_time() - t_cpu
