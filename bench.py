@@ -466,7 +466,8 @@ def main():
             e[2] += 1
             # per kernel template (rocprofv3 names them gemm_dma_kernel<A_KC, B_KC, EPI, ...>)
             t = f"gemm<{'true' if c_ & 1 else 'false'}, {'true' if c_ & 2 else 'false'}, {(c_ >> 2) & 63}>" + \
-                (" batched" if c_ & 256 else "") + (" split-K" if c_ & 512 else "") + (" grouped" if c_ & 1024 else "")
+                (" batched" if c_ & 256 else "") + (" split-K" if c_ & 512 else "") + (" grouped" if c_ & 1024 else "") + \
+                (" short-M" if c_ & 2048 else "")
             e = templates.setdefault(t, [0.0, 0.0, 0])
             e[0] += ms_
             e[1] += fl_

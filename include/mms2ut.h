@@ -98,6 +98,15 @@ int mms2ut_gemm_f16(const mms2ut_gemm_args* args, hipStream_t stream);
  * for every qualifying NT shape (tests).                                                          */
 int mms2ut_gemm_set_tall(int mode);
 
+/* Short-M NT GEMMs (a 128x128 grid of fewer than 128 tiles: the decoder's ~470-row projections).
+ * mode 1 (default; env MMS2UT_GEMM_SKINNY overrides it at first use): a measured route table —
+ * N <= 1024 on the short-M kernel (one-shot operand loads per small tile, K split across blocks
+ * with an in-kernel last-arrival reduction into the caller's splitk_ws, epilogue fused, no second
+ * launch), N > 1024 with K <= 1024 unsplit on the 128-row tiles, the rest on the split-K + fixup
+ * route the caller asked for; 0: always the caller's route (A/B runs, tests); 2: the short-M kernel
+ * for every short-M shape (tests).                                                              */
+int mms2ut_gemm_set_skinny(int mode);
+
 /* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the
  * reference layer's projections): for each of the n <= 8 problems, dW[N, K] = dy[rows, N]^T @
  * x[rows, K] (fp16, row stride K, overwritten) and, when db != NULL, db[N] = column sums of dy —

@@ -22,6 +22,8 @@
 
 namespace {
 
+#include "gemm_skinny.h"
+
 template <bool KC>
 MMS_DEV void load_tile(const h16* __restrict__ X, long ld, int rows_total, int kdim,
                        int row0, int k0, int kend, s16x8 (&r)[4]) {
@@ -720,6 +722,37 @@ int launch_fixup(int epi, const GemmP& P, const float* ws, int nsplit, hipStream
   return mms::check_launch("splitk_fixup");
 }
 
+template <int TM, int TN, int NLOC>
+int launch_skinny_t(int epi, const GemmP& P, int nsplit, float* part, int* ticket, hipStream_t s) {
+  const int tm = (P.M + 16 * TM - 1) / (16 * TM), tn = (P.N + 16 * TN - 1) / (16 * TN);
+  dim3 grid(8 * ((tm * tn + 7) / 8) * nsplit), block(NT);   // gemm_skinny.h: 8 XCD ranges x splits
+  switch (epi) {
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_skinny_kernel<E, TM, TN, NLOC>), grid, block, 0, s, P, tm, tn, nsplit, part, ticket); break;
+    CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID)
+    CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
+#undef CASE
+    default: mms::set_error("gemm: bad epilogue %d for the short-M kernel", epi); return 1;
+  }
+  return mms::check_launch("gemm_skinny");
+}
+
+// (tile code, chunks per wave): 44 = 64x64 tiles (NLOC <= 2: 64 accumulator + 2 x 64 operand VGPRs
+// keep two blocks per CU), 24 = 32x64 and 22 = 32x32 (NLOC <= 3)
+struct SkinnyPlan { int code = 0, nloc = 0, nsplit = 1; };
+int launch_skinny(const SkinnyPlan& pl, int epi, const GemmP& P, float* part, int* ticket, hipStream_t s) {
+  switch (pl.code * 10 + pl.nloc) {
+    case 441: return launch_skinny_t<4, 4, 1>(epi, P, pl.nsplit, part, ticket, s);
+    case 442: return launch_skinny_t<4, 4, 2>(epi, P, pl.nsplit, part, ticket, s);
+    case 241: return launch_skinny_t<2, 4, 1>(epi, P, pl.nsplit, part, ticket, s);
+    case 242: return launch_skinny_t<2, 4, 2>(epi, P, pl.nsplit, part, ticket, s);
+    case 243: return launch_skinny_t<2, 4, 3>(epi, P, pl.nsplit, part, ticket, s);
+    case 221: return launch_skinny_t<2, 2, 1>(epi, P, pl.nsplit, part, ticket, s);
+    case 222: return launch_skinny_t<2, 2, 2>(epi, P, pl.nsplit, part, ticket, s);
+    case 223: return launch_skinny_t<2, 2, 3>(epi, P, pl.nsplit, part, ticket, s);
+    default: mms::set_error("gemm: bad short-M plan %d/%d", pl.code, pl.nloc); return 1;
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
@@ -817,6 +850,9 @@ static int group_m_for(int tiles_m) {
   return env;
 }
 
+static int skinny_pick(const mms2ut_gemm_args* a);
+static bool short_m_unsplit(const mms2ut_gemm_args* a);
+
 extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   if (!g_prof.on || g_prof.n >= g_prof.cap) return gemm_dispatch(a, stream);
   const int i = g_prof.n++;
@@ -832,12 +868,14 @@ extern "C" int mms2ut_gemm_f16(const mms2ut_gemm_args* a, hipStream_t stream) {
   }
   if (a) {
     const double nb = a->batch > 0 ? a->batch : 1;
+    const bool skinny = skinny_pick(a) != 0;
+    const int nsplit = skinny || short_m_unsplit(a) ? 1 : (a->splitk > 0 ? a->splitk : 1);
     g_prof.flops += 2.0 * a->M * a->N * a->K * nb;
     g_prof.l_flops[i] = 2.0 * a->M * a->N * a->K * nb;
     g_prof.l_mnk[4 * i] = a->M; g_prof.l_mnk[4 * i + 1] = a->N; g_prof.l_mnk[4 * i + 2] = a->K;
-    g_prof.l_mnk[4 * i + 3] = (a->batch > 0 ? a->batch : 1) * (a->splitk > 0 ? a->splitk : 1);
+    g_prof.l_mnk[4 * i + 3] = (a->batch > 0 ? a->batch : 1) * nsplit;
     g_prof.l_cls[i] = (a->a_kcontig ? 1 : 0) | (a->b_kcontig ? 2 : 0) | (a->epi << 2) | (nb > 1 ? 256 : 0) |
-                      ((a->splitk > 1 ? 1 : 0) << 9);
+                      ((nsplit > 1 ? 1 : 0) << 9) | (skinny ? 2048 : 0);
     const double c_bytes = (double)a->M * a->N * (a->epi == MMS_EPI_F32 ? 4.0 * (a->splitk > 0 ? a->splitk : 1) : 2.0);
     double extra = 0.0;
     if (a->epi == MMS_EPI_DROP_RESID || a->epi == MMS_EPI_RELU_DROP_BWD || a->epi == MMS_EPI_F16_ACC) extra = 2.0 * a->M * a->N;
@@ -1046,6 +1084,101 @@ extern "C" int mms2ut_gemm_set_tall(int mode) {
   return 0;
 }
 
+// Short-M NT GEMMs (gemm_skinny.h): those whose 128x128 grid would cover fewer than 128 tiles
+// (the decoder's ~470-row projections and the fusion's short image rows), which otherwise take the
+// split-K + fixup route.  The plan minimises a latency model of the kernel: the busiest CU's
+// operand bytes at ~60 GB/s per CU (the rate a block's one-shot VGPR loads were measured to
+// draw), plus, with a K split, the partial-tile round trip and the last block's reduction reads.
+// A split needs the caller's split-K workspace (splitk_ws) and the stream's ticket array.
+// MMS2UT_GEMM_SKINNY / mms2ut_gemm_set_skinny: 1 = the measured route table below (default),
+// 0 = the split-K + fixup route as the caller asked (A/B), 2 = this kernel for every short-M shape.
+static int g_skinny_mode = -1;
+static int skinny_mode() {
+  if (g_skinny_mode < 0) {
+    const char* e = getenv("MMS2UT_GEMM_SKINNY");
+    g_skinny_mode = e ? atoi(e) : 1;
+  }
+  return g_skinny_mode;
+}
+constexpr int kTicketCap = 16384;   // tiles per launch with a K split
+static bool skinny_eligible(const mms2ut_gemm_args* a) {
+  if (!skinny_mode() || !a || !a->a_kcontig || !a->b_kcontig || a->batch != 1 || a->epi == MMS_EPI_F32 ||
+      a->rowsum || a->K <= 0 || a->K % 256 || a->M <= 0 || a->N <= 0)
+    return false;
+  if ((long)((a->M + 127) / 128) * ((a->N + 127) / 128) >= 128) return false;
+  // measured route table (profiles/round5_short_m_gemm.txt, M = 470 / 900 decoder shapes): the
+  // short-M kernel wins for N <= 1024 (K = 768 at any M; K = 2304-3072 at M <= ~600); the 128-row
+  // tiles unsplit win for N >= 1536 at K <= 1024; the split-K + fixup route keeps the rest
+  return skinny_mode() == 2 || (a->N <= 1024 && (a->M <= 640 || a->K <= 1024));
+}
+// a short-M fused-epilogue GEMM whose caller asked for the split-K fixup but that runs faster on
+// the unsplit 128-row tiles (wide N, short K: enough tiles already)
+static bool short_m_unsplit(const mms2ut_gemm_args* a) {
+  return skinny_mode() == 1 && a && a->a_kcontig && a->b_kcontig && a->batch == 1 && a->epi != MMS_EPI_F32 &&
+         a->splitk > 1 && a->N > 1024 && a->K <= 1024;
+}
+// The partial-tile workspace a split plan may use: what every caller of the split-K fixup sizes
+// (kernels.py _fixup_splits / layers.hip fixup_splits: s * M * N floats), so the plan — and the bits —
+// do not depend on which caller (or how large a workspace) issued the GEMM.
+static double skinny_ws_budget(const mms2ut_gemm_args* a) {
+  if (a->N % 4 || a->K < 512) return 0.0;
+  const long tiles = (long)((a->M + 127) / 128) * ((a->N + 127) / 128);
+  const long s = std::max(1L, std::min(std::min(512L / tiles, (long)a->K / 256), 16L));
+  if (s < 2 || !a->splitk_ws || a->splitk_ws_floats < s * a->M * (long)a->N) return 0.0;
+  return (double)s * a->M * a->N;
+}
+static SkinnyPlan skinny_plan(const mms2ut_gemm_args* a, bool can_split) {
+  SkinnyPlan best;
+  if (!skinny_eligible(a)) return best;
+  const double ws_budget = skinny_ws_budget(a);
+  const long cus = gemm_cu_count();
+  const int kq = a->K / 256;                  // 256-wide k quarters: one 64-chunk per wave
+  double best_t = 1e30;
+  const int codes[3] = {44, 24, 22};
+  for (int code : codes) {
+    const int bm = 16 * (code / 10), bn = 16 * (code % 10);
+    const long tiles = (long)((a->M + bm - 1) / bm) * ((a->N + bn - 1) / bn);
+    for (int nloc = (code == 44 ? 2 : 3); nloc >= 1; --nloc) {
+      if (kq % nloc) continue;
+      const int S = kq / nloc;
+      if (S > 16 || (S > 1 && (!can_split || tiles > kTicketCap ||
+                               (double)tiles * S * bm * bn > ws_budget)))
+        continue;
+      const long blocks = tiles * S;
+      const double per_cu = (double)((blocks + cus - 1) / cus);
+      const double bytes = (double)(bm + bn) * 256.0 * nloc * 2.0;
+      double t = per_cu * bytes / 60e3;                               // us at 60 GB/s per CU
+      if (S > 1) t += 2.5 + (double)S * bm * bn * 4.0 / 60e3;       // partial round trip + reduction reads
+      if (t < best_t) { best_t = t; best.code = code; best.nloc = nloc; best.nsplit = S; }
+    }
+  }
+  return best;
+}
+// Per-stream ticket arrays of the split plans (zeroed once; every launch leaves them zero).
+// Allocated on a stream's first split launch; none while the stream is capturing (that launch
+// takes an unsplit plan).
+static int* skinny_tickets(hipStream_t stream) {
+  static hipStream_t keys[64];
+  static int* vals[64];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (keys[i] == stream) return vals[i];
+  if (n == 64) return nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
+  int* p = nullptr;
+  if (hipMalloc(&p, kTicketCap * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, kTicketCap * sizeof(int), stream) != hipSuccess) { hipFree(p); return nullptr; }
+  keys[n] = stream; vals[n] = p; ++n;
+  return p;
+}
+static int skinny_pick(const mms2ut_gemm_args* a) { return skinny_plan(a, a && a->splitk_ws).code; }
+extern "C" int mms2ut_gemm_set_skinny(int mode) {
+  MMS_REQUIRE(mode >= 0 && mode <= 2, "gemm_set_skinny: mode must be 0, 1 or 2 (got %d)", mode);
+  g_skinny_mode = mode;
+  return 0;
+}
+
 // 256x256-tile kernel or the 128x128 one
 static bool use_256(const mms2ut_gemm_args* a, int nz) {
   // measured (round-2 A/B, scripts/gemm_ab.py in git history): the 256 tile wins only with a long K and enough tiles to keep
@@ -1071,6 +1204,16 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
   P.bdiv = a->bdiv > 0 ? a->bdiv : 1;
   P.sA1 = a->sA1; P.sA2 = a->sA2; P.sB1 = a->sB1; P.sB2 = a->sB2; P.sC1 = a->sC1; P.sC2 = a->sC2;
   int splitk = a->splitk > 0 ? a->splitk : 1;
+  if (splitk > 1 && a->epi != MMS_EPI_F32 && skinny_pick(a)) {
+    mms2ut_gemm_args b = *a;   // the caller's split-K request is the fallback route; its workspace
+    b.splitk = 1;              // holds the short-M kernel's partial tiles
+    return gemm_dispatch(&b, stream);
+  }
+  if (short_m_unsplit(a)) {
+    mms2ut_gemm_args b = *a;
+    b.splitk = 1; b.splitk_ws = nullptr; b.splitk_ws_floats = 0;
+    return gemm_dispatch(&b, stream);
+  }
   if (splitk > 1 && a->epi != MMS_EPI_F32) {
     // split-K + fixup: the splits as an fp32-slab GEMM into the workspace, then the epilogue pass
     MMS_REQUIRE(a->batch == 1 && !a->rowsum && a->N % 4 == 0, "gemm: split-K fixup needs batch 1, N %% 4 == 0");
@@ -1128,6 +1271,16 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     if (a->out2) v = v && al16(a->out2) && a->ldo2 % 8 == 0;
     if (a->bias) v = v && al16(a->bias);
     P.vec16 = v ? 1 : 0;
+  }
+  if (splitk == 1 && skinny_eligible(a)) {
+    int* tickets = a->splitk_ws ? skinny_tickets(stream) : nullptr;
+    const SkinnyPlan pl = skinny_plan(a, tickets != nullptr);
+    if (pl.code) {
+      const int q = pl.code / 10, r = pl.code % 10;
+      const long tiles = (long)((a->M + 16 * q - 1) / (16 * q)) * ((a->N + 16 * r - 1) / (16 * r));
+      P.stamps = stamp_take(8 * ((tiles + 7) / 8) * pl.nsplit);
+      return launch_skinny(pl, a->epi, P, pl.nsplit > 1 ? a->splitk_ws : nullptr, tickets, stream);
+    }
   }
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;
   const int nz = a->batch * splitk;

@@ -8,12 +8,14 @@ from collections import defaultdict
 
 import numpy as np
 
-EPI = {0: "f16", 1: "relu_drop", 2: "drop_resid", 3: "f32", 4: "gate", 5: "relu_drop_bwd", 6: "f16_acc"}
+EPI = {0: "f16", 1: "relu_drop", 2: "drop_resid", 3: "f32", 4: "gate", 5: "relu_drop_bwd", 6: "f16_acc", 7: "gelu_drop",
+       8: "gelu_drop_bwd"}
 z = np.load(sys.argv[1])
 steps = int(z["steps"])
 rows = defaultdict(lambda: [0, 0.0, 0.0])
 for ms, fl, c, (M, N, K, nz) in zip(z["ms"], z["flops"], z["cls"], z["mnk"]):
     kind = "batched" if c & 256 else ("TN" if not (c & 3) else ("NT" if (c & 3) == 3 else "NN"))
+    kind += "/sm" if c & 2048 else ""   # short-M kernel (csrc/gemm_skinny.h)
     key = (kind, EPI[(int(c) >> 2) & 63], N, K, nz, M // 2000 * 2000)
     r = rows[key]
     r[0] += 1

@@ -1,9 +1,10 @@
-"""Split-K with a fused-epilogue fixup (include/mms2ut.h splitk_ws): the short-M GEMMs of the unit
-decoder (M = target tokens of a batch, a few hundred rows) split K over ~512 workgroups and apply
-their epilogue in a second pass.  Checked against the unsplit kernel on the same operands:
-values within fp32-summation-order noise (fp16 outputs: 2e-3 relative L2) and the dropout masks
-identical (a large positive bias keeps every ReLU open, so the zero pattern IS the mask), plus
-the fp32 torch product for the plain epilogue."""
+"""Short-M GEMM routes (the unit decoder's projections: M = target tokens of a batch, a few hundred
+rows).  The default is the whole-K small-tile kernel (csrc/gemm_skinny.h); the split-K route (K split
+over ~512 workgroups, fused epilogue applied in a fixup pass, include/mms2ut.h splitk_ws) and the
+unsplit 128x128 kernel remain behind mms2ut_gemm_set_skinny(0).  Checked against each other on the
+same operands: values within fp32-summation-order noise (fp16 outputs: 2e-3 relative L2) and the
+dropout masks identical, plus the fp32 torch product for the plain epilogue.  Also: the tall NT tiles
+are bit-identical to the 128x128 kernel."""
 import pytest
 import torch
 
@@ -29,50 +30,76 @@ def _linear(K_, x, W, bias, fixup, epi, aux=None, out2=None, p=0.0, drop=None):
     return out
 
 
+ROUTES = (("skinny", 2, True), ("default", 1, True), ("fixup", 0, True), ("unsplit", 0, False))
+
+
 @pytest.mark.parametrize("M,N,K", [(466, 768, 3072), (466, 3072, 768), (300, 768, 768), (700, 2304, 768),
-                                   (129, 768, 3072)])
-def test_fixup_matches_unsplit(M, N, K):
+                                   (129, 768, 3072), (470, 1536, 2560), (1000, 1536, 768), (17, 1004, 768),
+                                   (1, 768, 768), (50, 256, 64), (2000, 768, 512), (20, 256, 3072)])
+def test_short_m_routes_agree(M, N, K):
+    """The routes of a short-M fused-epilogue GEMM on the same operands: the short-M kernel forced
+    (mode 2; tile codes 64x64 / 32x64 / 32x32, with and without a K split, all covered), the default
+    route table (mode 1), split-K + fixup, and the unsplit 128x128 kernel.  Values agree within fp32-summation-order noise, dropout masks are
+    identical (a large positive bias keeps every ReLU open, so the zero pattern IS the mask), and the
+    plain epilogue matches the fp32 torch product."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     mm = pkg()
     K_ = mm.kernels
-    assert K_._fixup_splits(M, N, K) > 1
-    g = torch.Generator(device="cuda").manual_seed(0)
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
     x = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
     W = (torch.randn(N, K, device="cuda", generator=g) * 0.05).half()
     b = (torch.randn(N, device="cuda", generator=g) * 0.1).half()
     aux = torch.randn(M, N, device="cuda", generator=g).half()
     big = torch.full((N,), 30.0, device="cuda").half()
+    c0 = torch.randn(M, N, device="cuda", generator=g).half()
     cases = [("f16", dict(epi=K_.EPI_F16)),
              ("relu_drop_open", dict(epi=K_.EPI_RELU_DROP, p=0.1, drop=(11, 4096), bias=big)),
              ("relu_drop", dict(epi=K_.EPI_RELU_DROP, p=0.1, drop=(11, 4096))),
              ("drop_resid", dict(epi=K_.EPI_DROP_RESID, p=0.1, drop=(5, 0), aux=aux)),
              ("relu_drop_bwd", dict(epi=K_.EPI_RELU_DROP_BWD, p=0.1, drop=(5, 0), aux=aux)),
+             ("gelu_drop", dict(epi=K_.EPI_GELU_DROP, p=0.1, drop=(3, 64),
+                                out2=torch.empty(M, N, device="cuda", dtype=torch.float16))),
+             ("gelu_drop_bwd", dict(epi=K_.EPI_GELU_DROP_BWD, p=0.1, drop=(3, 64), aux=aux)),
+             ("f16_acc", dict(epi=K_.EPI_F16_ACC)),
              ("gate", dict(epi=K_.EPI_GATE, aux=torch.randn(M, 2 * N, device="cuda", generator=g).half(),
                            out2=torch.empty(M, N, device="cuda", dtype=torch.float16)))]
     if N % 8:
         cases = [c for c in cases if c[0] != "gate"]
-    for name, kw in cases:
-        kw = dict(kw)
-        bias = kw.pop("bias", b if kw["epi"] not in (K_.EPI_RELU_DROP_BWD,) else None)
-        outs = []
-        for fix in (False, True):
-            o2 = kw.get("out2")
-            if o2 is not None:
-                o2.zero_()
-            outs.append((_linear(K_, x, W, bias, fix, **kw).clone(), None if o2 is None else o2.clone()))
-        torch.cuda.synchronize()
-        (ref, ref2), (got, got2) = outs
-        assert _rel(got, ref) < 2e-3, (name, _rel(got, ref))
-        if ref2 is not None:
-            assert _rel(got2, ref2) < 2e-3, name
-        if name == "relu_drop_open":
-            assert torch.equal(got == 0, ref == 0), name
-            frac = (got == 0).float().mean().item()
-            assert 0.08 < frac < 0.12, frac
-        if name == "f16":
-            exact = (x.float() @ W.float().t() + b.float())
-            assert _rel(got, exact) < 2e-3
+    try:
+        for name, kw in cases:
+            kw = dict(kw)
+            bias = kw.pop("bias", b if kw["epi"] not in (K_.EPI_RELU_DROP_BWD, K_.EPI_GELU_DROP_BWD) else None)
+            outs = {}
+            for route, skinny, fix in ROUTES:
+                K_.call("mms2ut_gemm_set_skinny", skinny)
+                o2 = kw.get("out2")
+                if o2 is not None:
+                    o2.zero_()
+                if kw["epi"] == K_.EPI_F16_ACC:
+                    out = c0.clone()
+                    K_.gemm(x, W, out, M, N, K, lda=K, ldb=K, ldc=N, epi=K_.EPI_F16_ACC, fixup=fix)
+                else:
+                    out = _linear(K_, x, W, bias, fix, **kw).clone()
+                outs[route] = (out, None if o2 is None else o2.clone())
+            torch.cuda.synchronize()
+            ref, ref2 = outs["unsplit"]
+            for route in ("skinny", "default", "fixup"):
+                got, got2 = outs[route]
+                assert torch.isfinite(got.float()).all(), (name, route)
+                assert _rel(got, ref) < 2e-3, (name, route, _rel(got, ref))
+                if ref2 is not None:
+                    assert _rel(got2, ref2) < 2e-3, (name, route)
+                if name == "relu_drop_open":
+                    assert torch.equal(got == 0, ref == 0), (name, route)
+            if name == "relu_drop_open" and M * N > 10000:
+                frac = (outs["skinny"][0] == 0).float().mean().item()
+                assert 0.08 < frac < 0.12, frac
+            if name == "f16":
+                exact = (x.float() @ W.float().t() + b.float())
+                assert _rel(outs["skinny"][0], exact) < 2e-3
+    finally:
+        K_.call("mms2ut_gemm_set_skinny", 1)   # the library default
 
 
 def test_fixup_accumulate_dgrad():
@@ -117,6 +144,7 @@ def test_tall_gemm_bit_identical(M, N, K):
     b = (torch.randn(N, device="cuda", generator=g) * 0.1).half()
     aux = torch.randn(M, 2 * N, device="cuda", generator=g).half()
     c0 = torch.randn(M, N, device="cuda", generator=g).half()
+    K_.call("mms2ut_gemm_set_skinny", 0)     # (300, 520, 64) is short-M: keep it on the NT tiles
     try:
         for name in _PP_EPIS:
             epi = getattr(K_, "EPI_" + name)
@@ -140,4 +168,5 @@ def test_tall_gemm_bit_identical(M, N, K):
         ref = (x.float() @ W.float().t() + b.float())
         assert _rel(got, ref) < 2e-3
     finally:
-        K_.call("mms2ut_gemm_set_tall", 1)   # the library default
+        K_.call("mms2ut_gemm_set_tall", 1)   # the library defaults
+        K_.call("mms2ut_gemm_set_skinny", 1)
