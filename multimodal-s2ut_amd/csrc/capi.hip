@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // Error plumbing + split-K reduction.
 #include <stdarg.h>
 #include <stdio.h>
@@ -127,6 +128,10 @@ extern "C" int mms2ut_splitk_reduce_bias(const float* slabs, int nsplit, int64_t
 // stream fork/join for the weight-gradient side stream: `waiter` waits for everything enqueued
 // on `signaler` so far.  A small ring of timing-disabled events (created once per process) is
 // re-recorded round-robin; a wait binds to the record that precedes it, so reuse is safe.
+// The events skip the system-scope fence (hipEventDisableSystemFence): both streams are on this
+// device, whose kernels already release / acquire at device scope, and the default system-scope
+// release made every fork a full cache writeback — a ~7 us bubble on the main stream after each
+// layer's LayerNorm backward, ~1 ms per step (round-5 trace, profiles/round5_fork_fence.txt).
 // ------------------------------------------------------------------------------------------
 namespace {
 constexpr int kEvRing = 64;
@@ -137,8 +142,10 @@ int g_ev_n = -1, g_ev_i = 0;
 extern "C" int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler) {
   if (waiter == signaler) return 0;
   if (g_ev_n < 0) {
+    const char* e = getenv("MMS2UT_FORK_SYSTEM_FENCE");   // 1: the default system-scope events (A/B)
+    const unsigned flags = hipEventDisableTiming | (e && atoi(e) ? 0u : (unsigned)hipEventDisableSystemFence);
     for (int i = 0; i < kEvRing; ++i)
-      if (hipEventCreateWithFlags(&g_ev[i], hipEventDisableTiming) != hipSuccess) {
+      if (hipEventCreateWithFlags(&g_ev[i], flags) != hipSuccess) {
         mms::set_error("stream_wait: hipEventCreate failed");
         return 1;
       }
