@@ -2,8 +2,9 @@
  * libmms2ut_hip — C-ABI of the MI355X-native mm_s2ut_transformer training path.
  *
  * Every entry point takes raw device pointers, int64 sizes/strides, scalars and the HIP stream to
- * enqueue on (PyTorch's current stream).  The library never allocates or frees: all buffers,
- * including workspaces, belong to the caller (PyTorch's caching allocator).  Functions return 0 on
+ * enqueue on (PyTorch's current stream).  All buffers, including workspaces, belong to the caller
+ * (PyTorch's caching allocator); the one library allocation is a 64 KiB zeroed ticket array per
+ * stream for the short-M GEMM's in-kernel split-K (made on the stream's first such launch).  Functions return 0 on
  * success and non-zero on error; mms2ut_last_error() returns the message (thread-local).  The
  * library is stateless and re-entrant; kernels are only ever enqueued on the passed stream.
  *
@@ -177,6 +178,14 @@ int mms2ut_transpose_batch(const mms2ut_half* src, mms2ut_half* dst, const mms2u
 /* `waiter` waits for all work enqueued on `signaler` so far (event record + stream wait).
  * Forks/joins the weight-gradient side stream (the reference's DDP/autograd stream overlap). */
 int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler);
+/* Device-scope events (no timing, no system-scope fence): ordering between this process's streams
+ * on one GPU — the deferred optimizer chunks before the next forward reads them, the weight
+ * transpose before the dgrad GEMMs, per-group gradient hand-offs (torch's CUDA events in the
+ * reference's DDP / autograd stream syncs).  Not for host synchronisation.                       */
+int mms2ut_event_create(hipEvent_t* out);
+int mms2ut_event_record(hipEvent_t event, hipStream_t stream);
+int mms2ut_event_wait(hipStream_t stream, hipEvent_t event);
+int mms2ut_event_destroy(hipEvent_t event);
 /* HIP-graph replay of the training step: every dropout kernel adds *delta (a device uint64) to
  * the seed it was launched or captured with; delta == NULL (the default) leaves seeds unchanged.
  * mms2ut_step_seed_advance(delta, inc) is the first node of a captured step (delta += inc), so

@@ -135,6 +135,10 @@ SIGNATURES = {
     "mms2ut_version": (i32, []),
     "mms2ut_stream_create": (i32, [i32, vp]),
     "mms2ut_stream_destroy": (i32, [vp]),
+    "mms2ut_event_create": (i32, [vp]),
+    "mms2ut_event_record": (i32, [vp, vp]),
+    "mms2ut_event_wait": (i32, [vp, vp]),
+    "mms2ut_event_destroy": (i32, [vp]),
     "mms2ut_gemm_f16": (i32, [vp, vp]),   # GEMM_ARGS.pack(...) bytes or C.byref(GemmArgs)
     "mms2ut_gemm_set_tall": (i32, [i32]),
     "mms2ut_gemm_set_skinny": (i32, [i32]),

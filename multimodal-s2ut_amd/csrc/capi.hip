@@ -160,6 +160,33 @@ extern "C" int mms2ut_stream_wait(hipStream_t waiter, hipStream_t signaler) {
   return 0;
 }
 
+// Device-scope events for ordering this process's streams on one GPU (same flags as the fork ring):
+// deferred optimizer chunks -> the next forward, weight-transpose refresh -> dgrad, per-group
+// gradient hand-offs.  No timing, no host synchronisation.
+extern "C" int mms2ut_event_create(hipEvent_t* out) {
+  MMS_REQUIRE(out != nullptr, "event_create: null out");
+  const char* e = getenv("MMS2UT_FORK_SYSTEM_FENCE");
+  const unsigned flags = hipEventDisableTiming | (e && atoi(e) ? 0u : (unsigned)hipEventDisableSystemFence);
+  const hipError_t r = hipEventCreateWithFlags(out, flags);
+  MMS_REQUIRE(r == hipSuccess, "event_create: %s", hipGetErrorString(r));
+  return 0;
+}
+extern "C" int mms2ut_event_record(hipEvent_t ev, hipStream_t stream) {
+  const hipError_t r = hipEventRecord(ev, stream);
+  MMS_REQUIRE(r == hipSuccess, "event_record: %s", hipGetErrorString(r));
+  return 0;
+}
+extern "C" int mms2ut_event_wait(hipStream_t stream, hipEvent_t ev) {
+  const hipError_t r = hipStreamWaitEvent(stream, ev, 0);
+  MMS_REQUIRE(r == hipSuccess, "event_wait: %s", hipGetErrorString(r));
+  return 0;
+}
+extern "C" int mms2ut_event_destroy(hipEvent_t ev) {
+  const hipError_t r = hipEventDestroy(ev);
+  MMS_REQUIRE(r == hipSuccess, "event_destroy: %s", hipGetErrorString(r));
+  return 0;
+}
+
 // ------------------------------------------------------------------------------------------
 // Step-seed indirection (HIP-graph replay of the training step; common.h mms_step_seed).
 // ------------------------------------------------------------------------------------------

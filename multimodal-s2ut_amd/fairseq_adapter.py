@@ -85,18 +85,22 @@ class _GradRelease:
         if todo:
             torch.autograd.backward(todo, [torch.ones_like(a) for a in todo])
 
+    _ring = []   # K.DevEvent, reused round-robin (a wait binds to the record preceding it)
+
     def ready(self, upto):
         from . import kernels as K
         side = K._Side.stream if K._Side.used else None
         ev = None
         if side is not None:
-            ev = torch.cuda.Event()
-            ev.record(side)
+            ring = _GradRelease._ring
+            if len(ring) < self.LAG + 2:
+                ring.append(K.DevEvent())
+            ev = ring[len(self.marks) % len(ring)].record(side)
         self.marks.append((upto, ev))
         if len(self.marks) > self.LAG:
             off, old = self.marks[-1 - self.LAG]
             if old is not None:
-                torch.cuda.current_stream().wait_event(old)
+                old.wait(torch.cuda.current_stream())
             self._release(off)
 
     def finish(self):

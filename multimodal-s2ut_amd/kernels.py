@@ -215,11 +215,12 @@ class TransposedWeights:
         if self.n == 0:
             return
         side = side_stream(self.flat.device)
-        side.wait_stream(torch.cuda.current_stream(self.flat.device))
+        stream_wait(side, torch.cuda.current_stream(self.flat.device))
         with torch.cuda.stream(side):
             call("mms2ut_transpose_batch", self.flat.data_ptr(), self.flatT.data_ptr(), self.desc.data_ptr(),
                  self.n, self.tiles, _s())
-        self.event = torch.cuda.Event()
+        if self.event is None:
+            self.event = DevEvent()
         self.event.record(side)
         self.waited = False
 
@@ -236,7 +237,7 @@ class TransposedWeights:
     def wait_ready(self):
         """The current stream waits for this step's refresh (once per refresh)."""
         if not self.waited and self.event is not None:
-            torch.cuda.current_stream(self.flat.device).wait_event(self.event)
+            self.event.wait(torch.cuda.current_stream(self.flat.device))
             self.waited = True
 
 
@@ -629,6 +630,39 @@ class _SideRegion:
 
 
 _SIDE_REGION = _SideRegion()
+
+
+class DevEvent:
+    """A device-scope event (include/mms2ut.h mms2ut_event_*): orders work between this process's
+    streams on one GPU without torch's system-scope fence (a full cache writeback per record,
+    ~6 us of idle GPU each; profiles/round5_fork_fence.txt).  No timing, no host sync.  Owners
+    re-record one event per use site; a wait binds to the record that precedes it."""
+    __slots__ = ("h",)
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        call("mms2ut_event_create", ctypes.addressof(h))
+        self.h = h.value
+
+    def record(self, stream):
+        call("mms2ut_event_record", self.h, stream.cuda_stream)
+        return self
+
+    def wait(self, stream):
+        call("mms2ut_event_wait", stream.cuda_stream, self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.load().mms2ut_event_destroy(ctypes.c_void_p(self.h))
+        except Exception:   # interpreter teardown
+            pass
+
+
+def stream_wait(waiter, signaler):
+    """`waiter` waits for everything enqueued on `signaler` so far (device-scope event)."""
+    if waiter.cuda_stream != signaler.cuda_stream:
+        call("mms2ut_stream_wait", waiter.cuda_stream, signaler.cuda_stream)
 
 
 _STREAMS = {}   # (device index, priority) -> ExternalStream, one per process

@@ -363,7 +363,7 @@ class ParamStore:
         """Make the current stream wait for a deferred optimizer update of `grp` (no-op if none)."""
         ev = self.pending.pop(grp, None)
         if ev is not None:
-            torch.cuda.current_stream(self.flat.device).wait_event(ev)
+            ev.wait(torch.cuda.current_stream(self.flat.device))
 
     def await_all(self):
         for grp in list(self.pending):

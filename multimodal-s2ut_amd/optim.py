@@ -36,6 +36,7 @@ class FP16Adam:
         ost[K.OST_CLIP_COEF] = 1.0
         self.ost = ost.to(params.flat.device)
         self.defer = True   # False: one Adam launch in stream order (tests compare both)
+        self._events = {}   # group -> K.DevEvent re-recorded by each deferred update
 
     def resync_master(self):
         """After loading fp16 weights: master := fp32 copy of the fp16 params."""
@@ -77,14 +78,15 @@ class FP16Adam:
             return
         ps.await_all()  # the previous step's chunks (normally already awaited by the forward)
         side = K.side_stream(ps.flat.device)
-        side.wait_stream(torch.cuda.current_stream(ps.flat.device))
+        K.stream_wait(side, torch.cuda.current_stream(ps.flat.device))
         with torch.cuda.stream(side):
             for grp, a, b in ps.groups:
                 K.adam(ps.flat[a:b], ps.grad[a:b], self.master[a:b], self.exp_avg[a:b], self.exp_avg_sq[a:b],
                        self.ost, b1, b2, self.eps, self.wd)
-                ev = torch.cuda.Event()
-                ev.record(side)
-                ps.pending[grp] = ev
+                ev = self._events.get(grp)
+                if ev is None:
+                    ev = self._events[grp] = K.DevEvent()
+                ps.pending[grp] = ev.record(side)
 
     def check_fatal(self, st=None):
         """Raise fairseq's FloatingPointError if the device state turned FATAL (sticky: an

@@ -81,7 +81,7 @@ class GradAllReducer:
         side = K._Side.stream
         ctx = None
         if side is not None and K._Side.used:
-            side.wait_stream(torch.cuda.current_stream())
+            K.stream_wait(side, torch.cuda.current_stream())
             ctx = torch.cuda.stream(side)
         with (ctx or K._NULLCTX):
             while self.next < len(self.bounds) and self.bounds[self.next][1] <= upto:

@@ -132,10 +132,10 @@ class Trainer:
         if self.stream is None:
             return self._train_step(batches)
         cur = torch.cuda.current_stream()
-        self.stream.wait_stream(cur)
+        K.stream_wait(self.stream, cur)
         with torch.cuda.stream(self.stream):
             log = self._train_step(batches)
-        cur.wait_stream(self.stream)
+        K.stream_wait(cur, self.stream)
         return log
 
     def _graph_step(self, batches, prologue, eager, draws):
@@ -151,7 +151,7 @@ class Trainer:
                 branches.append(None)
         key = (tuple(id(b) for b in batches), tuple(branches))
         cur = torch.cuda.current_stream()
-        self.stream.wait_stream(cur)
+        K.stream_wait(self.stream, cur)
         entry = None if eager else self.graphs.get(key)
         if entry is None:
             # first time: a real eager step (lazy allocations, table growth), then capture the same
@@ -180,7 +180,7 @@ class Trainer:
             with torch.cuda.stream(self.stream):
                 entry[0].replay()
             log = self.log
-        cur.wait_stream(self.stream)
+        K.stream_wait(cur, self.stream)
         return log
 
     def _train_step(self, batches):
