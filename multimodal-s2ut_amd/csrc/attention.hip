@@ -48,7 +48,12 @@ struct AttnP {
 
 template <int HD>
 struct Tile {
-  static constexpr int LD = HD + 8;  // padded LDS row (halves): 16 rows of a ds_read_b128 hit distinct banks
+  // padded LDS row (halves).  HD + 16 (a row stride of 8 dwords mod 16): the 16-lane groups that
+  // gfx950 services per ds_read_b128 cycle ({0-3,12-15,20-27}, ...: rows 0-3 and 12-15 of one
+  // 8-half column block with rows 4-11 of the next) and the 32-lane groups of ds_read_b64_tr_b16
+  // then touch every bank once; HD + 8 (round 1-4) conflicted 2-way on both reads
+  // (SQ_LDS_BANK_CONFLICT 1.6x the LDS-active cycles of the fused backward, round-5 PMC)
+  static constexpr int LD = HD + 16;
   static constexpr int CH = HD / 8;  // 16-B chunks per row
 };
 
