@@ -1181,6 +1181,12 @@ extern "C" int mms2ut_gemm_set_skinny(int mode) {
 
 // 256x256-tile kernel or the 128x128 one
 static bool use_256(const mms2ut_gemm_args* a, int nz) {
+  static int force = -2;   // MMS2UT_GEMM_256=1 / 0: every / no eligible shape on the 256 tile (A/B)
+  if (force == -2) {
+    const char* e = getenv("MMS2UT_GEMM_256");
+    force = e ? atoi(e) : -1;
+  }
+  if (force >= 0) return force == 1 && nz == 1;
   // measured (round-2 A/B, scripts/gemm_ab.py in git history): the 256 tile wins only with a long K and enough tiles to keep
   // one block per CU busy (subsampler conv2, large squares); the step's K = 768 projections and
   // every N = 768 shape run faster on 128x128 tiles at two blocks per CU
