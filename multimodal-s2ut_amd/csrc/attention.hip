@@ -159,14 +159,10 @@ MMS_DEV h16x8 pack8(f32x4 a, f32x4 b) {
   return h16x8{(h16)a[0], (h16)a[1], (h16)a[2], (h16)a[3], (h16)b[0], (h16)b[1], (h16)b[2], (h16)b[3]};
 }
 
-MMS_DEV float xmax16_32(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
-}
-MMS_DEV float xsum16_32(float v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
-}
+// over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (one query row's 4 key groups): permlane swaps,
+// no LDS round trip
+MMS_DEV float xmax16_32(float v) { return xmax32(xmax16(v)); }
+MMS_DEV float xsum16_32(float v) { return xsum32(xsum16(v)); }
 
 #ifdef MMS_ATTN_PHASES
 // diagnostic build only (scripts/attn_phases.py): s_memtime at the phase boundaries of the first

@@ -117,18 +117,53 @@ static inline uint32_t mms_drop_thresh(float p) {
 }
 
 // ------------------------------------------------------------------------------------------
-// wave64 reductions
+// wave64 reductions without LDS.  __shfl_xor lowers to ds_bpermute_b32 on gfx950 — an LDS round
+// trip (tens of cycles) per step, six of them in series for a wave sum, on the critical path of
+// every LayerNorm row and softmax tile.  Here: DPP row rotates (8, 4, 2, 1) inside each 16-lane
+// row, then gfx950's v_permlane16_swap / v_permlane32_swap across rows (plain VALU).  Every stage
+// adds (or maxes) a value with its partner in the same order on both lanes, so all 64 lanes end
+// with bit-identical results.  Call from wave-uniform control flow (all lanes active).
 // ------------------------------------------------------------------------------------------
-MMS_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+template <int CTRL>
+MMS_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
-MMS_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+constexpr int DPP_ROR8 = 0x128, DPP_ROR4 = 0x124, DPP_ROR2 = 0x122, DPP_ROR1 = 0x121;
+// the two values of lane pairs (l, l ^ 16) / (l, l ^ 32): .x = the lower row's, .y = the upper's
+struct f32pair { float lo, hi; };
+// The swap is written as inline asm: through the builtins, ROCm 7.2's compiler folds the two
+// results of a swap whose results are combined in one expression into the first one
+// (v_permlane16_swap v0, v1; v_add_f32 v0, v0, v0 — scripts/micro/permlane_probe.hip).  The
+// s_nop covers the VALU-write -> permlane-read hazard the compiler would otherwise insert.
+MMS_DEV f32pair xpair16(float v) {
+  unsigned a = __builtin_bit_cast(unsigned, v), b = a;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return {__builtin_bit_cast(float, a), __builtin_bit_cast(float, b)};
 }
+MMS_DEV f32pair xpair32(float v) {
+  unsigned a = __builtin_bit_cast(unsigned, v), b = a;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return {__builtin_bit_cast(float, a), __builtin_bit_cast(float, b)};
+}
+MMS_DEV float xsum16(float v) { const f32pair p = xpair16(v); return p.lo + p.hi; }
+MMS_DEV float xsum32(float v) { const f32pair p = xpair32(v); return p.lo + p.hi; }
+MMS_DEV float xmax16(float v) { const f32pair p = xpair16(v); return fmaxf(p.lo, p.hi); }
+MMS_DEV float xmax32(float v) { const f32pair p = xpair32(v); return fmaxf(p.lo, p.hi); }
+// sum / max over each 16-lane row
+MMS_DEV float row16_sum(float v) {
+  v += dpp_f<DPP_ROR8>(v);
+  v += dpp_f<DPP_ROR4>(v);
+  v += dpp_f<DPP_ROR2>(v);
+  return v + dpp_f<DPP_ROR1>(v);
+}
+MMS_DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_f<DPP_ROR8>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR4>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR2>(v));
+  return fmaxf(v, dpp_f<DPP_ROR1>(v));
+}
+MMS_DEV float wave_sum(float v) { return xsum32(xsum16(row16_sum(v))); }
+MMS_DEV float wave_max(float v) { return xmax32(xmax16(row16_max(v))); }
 MMS_DEV double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

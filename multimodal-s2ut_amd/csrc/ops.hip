@@ -88,11 +88,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const h16* __restrict__ x, 
 // D % 256 == 0 (the model widths 256 / 512 / 768 / 1024): a half-wave per row, C8 16-B chunks per
 // lane, two rows per wave and 8 per block -- twice the bytes per load instruction of the 4-wide
 // kernel and two independent rows in flight per wave.  Same statistics / dropout counters.
-MMS_DEV float half_sum(float v) {
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+MMS_DEV float half_sum(float v) { return xsum16(row16_sum(v)); }   // over each 32-lane half
 
 template <int C8>
 __global__ void __launch_bounds__(256) ln_fwd16_kernel(const h16* __restrict__ x, const h16* __restrict__ g,

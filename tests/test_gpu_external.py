@@ -137,9 +137,10 @@ def test_model_parity_qformer_dropout_replay(mm, saf, modality):
     print(report(r))
     check_outputs(r)
     # audio branch dropped: the decoder attends to the gate mix of a zero text stream and the fused
-    # image features, so its cross-attention logits are nearly flat and the q-side gradients
-    # (q_proj and the LayerNorm in front of it) carry fewer significant fp16 bits: 2e-2 there
-    loose = ("encoder_attn.q_proj", "encoder_attn_layer_norm") if modality == "audio" else ()
+    # image features, so its cross-attention logits are nearly flat and the gradients through the
+    # score matrix (q_proj / k_proj and the LayerNorm in front of q) carry fewer significant fp16
+    # bits: 2e-2 there (k_proj measured 0.8-1.1e-2 across reduction orders)
+    loose = ("encoder_attn.q_proj", "encoder_attn.k_proj", "encoder_attn_layer_norm") if modality == "audio" else ()
     bad = {k: e for k, e in grad_errors(r).items() if e > (2e-2 if any(s in k for s in loose) else 1e-2)}
     assert not bad, report(r)
     if modality == "image":
