@@ -9,7 +9,7 @@
 // exp(S) is converted in registers and fed straight back as the B operand of O^T = V^T P^T,
 // with the key order of the two 16-key tiles of a 32-key step permuted identically on the V side
 // (two ds_read_b64_tr_b16 at key rows 4g.. and 16+4g..).  Row statistics are lane-local + two
-// xor-shuffles; the O rescale is lane-local.  Dropout on the probabilities uses the same counter
+// permlane swaps (lanes l ^ 16, l ^ 32: xmax16_32 / xsum16_32); the O rescale is lane-local.  Dropout on the probabilities uses the same counter
 // RNG as the unfused path: counter = offset + (z*Tq + q)*Tk + key.
 //
 // Backward: D = rowsum(dO*O) (prep kernel); dK/dV with keys stationary (kernel A), dQ with queries
