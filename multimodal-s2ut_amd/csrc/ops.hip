@@ -285,6 +285,11 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float dscale = thresh ? 1.f / (1.f - p) : 1.f;
   const float invD = 1.f / D;
+  // emitted dropout: when every counter pair of the site shares one high word (always but across a
+  // 2^33 boundary) one mixer per two elements with the site's constant half hoisted (mms_keep4_hi,
+  // bit-identical to mms_keep4)
+  const bool emit_hi = thresh && mms_same_hi(offset, offset + (uint64_t)rows * D - 1);
+  const uint32_t emit_mix = emit_hi ? mms_hi_mix(seed, offset) : 0u;
   float gam[C][4], dg[C][4], db[C][4];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -380,7 +385,8 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
           st4(dx + (long)off, o[0], o[1], o[2], o[3]);
           if (dxd) {
             bool kp[4] = {true, true, true, true};
-            if (thresh) mms_keep4(seed, offset + (uint64_t)off, thresh, kp);
+            if (emit_hi) mms_keep4_hi(emit_mix, offset + (uint64_t)off, thresh, kp);
+            else if (thresh) mms_keep4(seed, offset + (uint64_t)off, thresh, kp);
             st4(dxd + (long)off, kp[0] ? o[0] * dscale : 0.f, kp[1] ? o[1] * dscale : 0.f, kp[2] ? o[2] * dscale : 0.f,
                 kp[3] ? o[3] * dscale : 0.f);
           }
