@@ -95,6 +95,26 @@ MMS_DEV void mms_keep4_hi(uint32_t hi_mix, uint64_t ctr0, uint32_t thresh, bool 
     for (int e = 0; e < 4; ++e) k[e] = mms_keep_hi(hi_mix, ctr0 + e, thresh);
   }
 }
+// A dropout site's hash constant hoisted out of the per-element work: when every counter pair of the
+// site [ctr0, ctr_last] shares one high word (always, unless the site straddles a 2^33 boundary)
+// a keep flag costs one mixer per counter pair instead of two (bit-identical to mms_keep*).
+struct MmsSite {
+  bool hi;
+  uint32_t mix;
+};
+MMS_DEV MmsSite mms_site(uint64_t seed, uint64_t ctr0, uint64_t ctr_last) {
+  MmsSite s;
+  s.hi = mms_same_hi(ctr0, ctr_last);
+  s.mix = s.hi ? mms_hi_mix(seed, ctr0) : 0u;
+  return s;
+}
+MMS_DEV void mms_keep4_site(const MmsSite& s, uint64_t seed, uint64_t ctr0, uint32_t thresh, bool (&k)[4]) {
+  if (s.hi) mms_keep4_hi(s.mix, ctr0, thresh, k);
+  else mms_keep4(seed, ctr0, thresh, k);
+}
+MMS_DEV bool mms_keep_site(const MmsSite& s, uint64_t seed, uint64_t ctr, uint32_t thresh) {
+  return s.hi ? mms_keep_hi(s.mix, ctr, thresh) : mms_keep(seed, ctr, thresh);
+}
 // Step-seed indirection for HIP-graph replay.  A captured launch keeps the host seed it was
 // captured with; the per-step variation comes from a device-resident 64-bit delta that every
 // dropout kernel adds to its seed argument on entry (the step's first kernel advances it, see

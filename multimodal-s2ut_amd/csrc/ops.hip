@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(const h16* __restrict__ x
   const long orow = grp ? (row / grp) * grp_out + row % grp : row;
   h16* yr = y + orow * D;
   const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  const MmsSite site = thresh ? mms_site(seed, offset, offset + (uint64_t)rows * D - 1) : MmsSite{false, 0u};
 #pragma unroll
   for (int c = 0; c < C8; ++c) {
     const int col = (hl + 32 * c) * 8;
@@ -130,8 +131,8 @@ __global__ void __launch_bounds__(256) ln_fwd16_kernel(const h16* __restrict__ x
     if (thresh) {
       bool k0[4], k1[4];
       const uint64_t c0 = offset + (uint64_t)(row * D + col);
-      mms_keep4(seed, c0, thresh, k0);
-      mms_keep4(seed, c0 + 4, thresh, k1);
+      mms_keep4_site(site, seed, c0, thresh, k0);
+      mms_keep4_site(site, seed, c0 + 4, thresh, k1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         o[e] = k0[e] ? (float)(h16)o[e] * ds : 0.f;
@@ -290,6 +291,7 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
   // bit-identical to mms_keep4)
   const bool emit_hi = thresh && mms_same_hi(offset, offset + (uint64_t)rows * D - 1);
   const uint32_t emit_mix = emit_hi ? mms_hi_mix(seed, offset) : 0u;
+  const MmsSite in_site = thin ? mms_site(sin, oin, oin + (uint64_t)rows * D - 1) : MmsSite{false, 0u};
   float gam[C][4], dg[C][4], db[C][4];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -340,7 +342,7 @@ __global__ void __launch_bounds__(256) ln_bwd_w_kernel(const h16* __restrict__ d
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         bool kp[4];
-        mms_keep4(sin, oin + (uint64_t)((int)row * D + (lane + 64 * c) * 4), thin, kp);
+        mms_keep4_site(in_site, sin, oin + (uint64_t)((int)row * D + (lane + 64 * c) * 4), thin, kp);
 #pragma unroll
         for (int e = 0; e < 4; ++e) cur.dv[c][e] = (h16)(kp[e] ? (float)cur.dv[c][e] * dsi : 0.f);
       }
@@ -604,9 +606,10 @@ __global__ void dropout_kernel(const h16* __restrict__ x, h16* __restrict__ y, l
                                uint32_t thresh, uint64_t seed, uint64_t offset) {
   if (thresh) seed = mms_step_seed(seed);
   const float ds = 1.f / (1.f - p);
+  const MmsSite site = mms_site(seed, offset, offset + (uint64_t)n - 1);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float v = (float)x[i];
-    y[i] = (h16)(mms_keep(seed, offset + i, thresh) ? v * ds : 0.f);
+    y[i] = (h16)(mms_keep_site(site, seed, offset + i, thresh) ? v * ds : 0.f);
   }
 }
 
@@ -623,6 +626,7 @@ __global__ void encoder_embed_kernel(const h16* __restrict__ h, const h16* __res
   if (thresh) seed = mms_step_seed(seed);
   const long n4 = (long)B * T * (D / 4);
   const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  const MmsSite site = thresh ? mms_site(seed, offset, offset + (uint64_t)n4 * 4 - 1) : MmsSite{false, 0u};
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const long e0 = i * 4;
     const long bt = e0 / D;
@@ -634,7 +638,7 @@ __global__ void encoder_embed_kernel(const h16* __restrict__ h, const h16* __res
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float v = scale * (float)hv[e] + (float)pv[e];
-      if (thresh) v = mms_keep(seed, offset + e0 + e, thresh) ? v * ds : 0.f;
+      if (thresh) v = mms_keep_site(site, seed, offset + e0 + e, thresh) ? v * ds : 0.f;
       o[e] = v;
     }
     st4(x + e0, o[0], o[1], o[2], o[3]);
@@ -646,9 +650,10 @@ __global__ void scale_dropout_bwd_kernel(const h16* __restrict__ dx, h16* __rest
                                          uint64_t offset) {
   if (thresh) seed = mms_step_seed(seed);
   const float ds = thresh ? 1.f / (1.f - p) : 1.f;
+  const MmsSite site = thresh ? mms_site(seed, offset, offset + (uint64_t)n - 1) : MmsSite{false, 0u};
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float v = (float)dx[i] * scale;
-    if (thresh) v = mms_keep(seed, offset + i, thresh) ? v * ds : 0.f;
+    if (thresh) v = mms_keep_site(site, seed, offset + i, thresh) ? v * ds : 0.f;
     dh[i] = (h16)v;
   }
 }
