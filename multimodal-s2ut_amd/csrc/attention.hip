@@ -674,8 +674,14 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
         vf[j][kk] = __builtin_bit_cast(h16x8, ld16b(rV, (key * (int)P.ldv + kk * 32 + 8 * g) * 2));
     }
   };
-  // persistent: block handles heads blockIdx.x, + gridDim.x, ...; the next head's rows, K and V
-  // are loaded into registers while the current head's MFMA phases run
+  // persistent: block i handles the heads of a snake order over rounds of G = gridDim.x heads --
+  // i, 2G - 1 - i, 2G + i, 4G - 1 - i, ... -- so the blocks that take a head of the last, partial
+  // round took a shorter one in the round before (heads come in batch-row order, and the collater
+  // sorts rows by length); the next head's rows, K and V are loaded into registers while the
+  // current head's MFMA phases run.  Once a block's next head is past Z, every later one is too.
+  const int G = gridDim.x, bid = blockIdx.x;
+  auto head_at = [&](int k) { return (k & 1) ? (k + 1) * G - 1 - bid : k * G + bid; };
+  int hk = 0;
   int z = blockIdx.x;
   if (z >= Z) return;
   const int ph_blk = blockIdx.x;
@@ -685,8 +691,8 @@ __global__ void __launch_bounds__(512) attn_bwd_fused_kernel(AttnP P, int Z) {
   load_kv(z, true);
   static_assert(QC * CH * sizeof(float) <= sizeof(sDS), "D partials must fit the dS^T buffer");
   int gc = 0;  // running chunk counter: parity selects the sL / sD buffer
-  for (; z < Z; z += gridDim.x) {
-    const int b = z / P.H, h = z % P.H, znext = z + gridDim.x;
+  for (; z < Z; z = head_at(++hk)) {
+    const int b = z / P.H, h = z % P.H, znext = head_at(hk + 1);
     const int klen = key_len_of(P, b);
     __syncthreads();  // the previous head's phase 3 is done with sK
 #pragma unroll
