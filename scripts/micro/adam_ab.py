@@ -1,6 +1,6 @@
 """Isolated Adam (fp16 params, fp32 master / moments) over one optimizer chunk of the step's size,
-timed with HIP events over 50 launches; the kernel variant is chosen by MMS_ADAM_V (read once per
-process).  Prints the mean launch time, the HBM rate at 28 B per parameter and a checksum of the
+timed with HIP events over 50 launches (the round-5 A/B built its variants behind an MMS_ADAM_V
+switch, since removed: profiles/round5_adam_ab.txt).  Prints the mean launch time, the HBM rate at 28 B per parameter and a checksum of the
 updated buffers (variants must agree bit for bit)."""
 import hashlib
 import importlib
