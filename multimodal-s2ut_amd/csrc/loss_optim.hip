@@ -109,8 +109,20 @@ __global__ void __launch_bounds__(256) ls_xent_bwd_kernel(const h16* __restrict_
 __global__ void grad_sqnorm_kernel(const h16* __restrict__ g, long n, float* __restrict__ part) {
   __shared__ float red[4];
   float s = 0.f;
-  const long n8 = n / 8;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+  const long n8 = n / 8, S = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  // four 16-B loads in flight per thread before the first add (one at a time left the sweep
+  // latency-bound); the per-thread summation order is the strided loop's
+  for (; i + 3 * S < n8; i += 4 * S) {
+    h16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const h16x8*>(g + (i + u * S) * 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float x = (float)v[u][e]; s += x * x; }
+  }
+  for (; i < n8; i += S) {
     h16x8 v = *reinterpret_cast<const h16x8*>(g + i * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) { const float x = (float)v[e]; s += x * x; }
