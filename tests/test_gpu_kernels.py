@@ -465,6 +465,25 @@ def test_gemm_tile256(K, a_kc, b_kc, M, N, K_):
     assert rel(C[:, :N], Af @ Bf.t()) < 2e-3
 
 
+def test_transposed_weight_images_many(K):
+    """More descriptors than one wave's lanes (the block's matrix lookup counts them 256 at a time):
+    300 ragged matrices, every image equals W^T."""
+    g = torch.Generator().manual_seed(5)
+    shapes = [(8 * int(torch.randint(1, 20, (1,), generator=g)), 8 * int(torch.randint(1, 20, (1,), generator=g)))
+              for _ in range(300)]
+    flat = torch.randn(sum(r * c for r, c in shapes) + 8 * len(shapes), device="cuda").half()
+    mats, off = [], 0
+    for r, c in shapes:
+        mats.append(flat[off:off + r * c].view(r, c))
+        off += r * c + 8
+    wt = K.TransposedWeights(flat, mats)
+    wt.refresh()
+    for W in mats:
+        T = wt.get(W)
+        torch.cuda.synchronize()
+        assert T is not None and torch.equal(T, W.t())
+
+
 def test_transposed_weight_images(K):
     """One transpose_batch launch writes W^T for every registered matrix (ragged tile edges); the
     dgrad through the image equals the dgrad through W."""
