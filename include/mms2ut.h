@@ -3,10 +3,13 @@
  *
  * Every entry point takes raw device pointers, int64 sizes/strides, scalars and the HIP stream to
  * enqueue on (PyTorch's current stream).  All buffers, including workspaces, belong to the caller
- * (PyTorch's caching allocator); the one library allocation is a 64 KiB zeroed ticket array per
- * stream for the short-M GEMM's in-kernel split-K (made on the stream's first such launch).  Functions return 0 on
- * success and non-zero on error; mms2ut_last_error() returns the message (thread-local).  The
- * library is stateless and re-entrant; kernels are only ever enqueued on the passed stream.
+ * (PyTorch's caching allocator).  The library keeps one piece of state: a per-device pool of
+ * zeroed ticket arrays for the short-M GEMM's in-kernel split-K (4 MiB, allocated on the device's
+ * first such launch; one 8 KiB slice per (device, stream), handed out under a mutex; every completed
+ * launch leaves its slice zero).  Apart from that pool, the GEMM route switches below and the bound
+ * step seed, entry points keep no state and may be called from several host threads; kernels are
+ * only ever enqueued on the passed stream.  Functions return 0 on success and non-zero on error;
+ * mms2ut_last_error() returns the message (thread-local).
  *
  * Each entry cites the reference interface (or the fairseq/PyTorch op it executes for the
  * reference) that it replaces — see SURVEY.md §8(a)/(b) and INTEGRATION.md.
@@ -107,6 +110,12 @@ int mms2ut_gemm_set_tall(int mode);
  * route the caller asked for; 0: always the caller's route (A/B runs, tests); 2: the short-M kernel
  * for every short-M shape (tests).                                                              */
 int mms2ut_gemm_set_skinny(int mode);
+/* Test hook of the short-M kernel's split-K hand-off (placement-independent: write-through partials,
+ * a relaxed agent-scope ticket, write-through reads).  scatter != 0 deals the splits of every tile
+ * over different XCD groups (bid % 8) instead of keeping them together; xcc_out (device, >= grid
+ * ints, or NULL) receives each block's hardware XCD id (HW_REG_XCC_ID).  Bits are identical either
+ * way.                                                                                         */
+int mms2ut_gemm_skinny_debug(int scatter, int* xcc_out);
 
 /* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the
  * reference layer's projections): for each of the n <= 8 problems, dW[N, K] = dy[rows, N]^T @

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "gemm_common.h"
 
@@ -230,6 +231,9 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
 #define MMS_GEMM_DMA_AFTER_READS 0
 #endif
   constexpr bool READ_FIRST = !A_KC || !B_KC || MMS_GEMM_DMA_AFTER_READS;
+  // dropout keep bits of the lane's 8 epilogue passes, a share per k-step (epi_bits_step)
+  const EpiDrop D = epi_drop_setup<EPI>(P, bm + wm * 64 + (lane >> 3), bn + wn * 64 + 8 * (lane & 7), 8, nk);
+  uint64_t kb[1] = {0};
   // All 16 fragments of the stage are read before its MFMAs (the second k-half's reads no longer
   // wait behind the first half's MFMAs): 0-5 % faster isolated on the step's NT shapes, step flat
   // (profiles/round3_v5_gemm_read_all_ab.txt).
@@ -260,6 +264,7 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
       dma_tile<A_KC>(ra, SA(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
       dma_tile<B_KC>(rb, SB(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
     }
+    if (epi_drops<EPI>() && D.pre) epi_bits_step<8>(P, D, kt, nk, kb);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       h16x8 fa[4], fb[4];
@@ -306,7 +311,7 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
     for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
   (void)Cz; (void)auxz;
 #else
-  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz, D.pre, kb[0]);
 #endif
 }
 
@@ -375,6 +380,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
     dma_tile<true>(rb, SB(0), P.ldb, bn, 0, wid, lane);
   }
   constexpr bool PR = PRIO && EPI != MMS_EPI_F32;
+  // dropout keep bits of the lane's 2 FRT epilogue passes, a share per k-step (epi_bits_step)
+  constexpr int NP = 2 * FRT;
+  const EpiDrop D = epi_drop_setup<EPI>(P, bm + 16 * FRT * wm + (lane >> 3), bn + wn * 64 + 8 * (lane & 7), NP, nk);
+  uint64_t kb[(NP + 7) / 8] = {};
   for (int kt = 0; kt < nk; ++kt) {
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
@@ -391,6 +400,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<true>(SB(cur), wn * 64 + j * 16, kk, lane);
     }
+    if (epi_drops<EPI>() && D.pre) epi_bits_step<NP>(P, D, kt, nk, kb);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       if (PR) __builtin_amdgcn_s_setprio(1);
@@ -409,11 +419,12 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
   // through the wave's 16 KiB staging area (staged_epilogue places wave rows at bm + 64 wm)
   constexpr int WR = 16 * FRT, F1 = FRT < 4 ? FRT : 4;
   staged_epilogue<EPI, F1>(P, smem, reinterpret_cast<const f32x4(&)[F1][4]>(acc[0]), bm + (WR - 64) * wm, bn, wm,
-                           wn, wid, lane, P.C, P.aux);
+                           wn, wid, lane, P.C, P.aux, D.pre, kb[0]);
   if constexpr (FRT > 4) {
     __syncthreads();
     staged_epilogue<EPI, FRT - 4>(P, smem, reinterpret_cast<const f32x4(&)[FRT - 4][4]>(acc[4]),
-                                  bm + (WR - 64) * wm + 64, bn, wm, wn, wid, lane, P.C, P.aux);
+                                  bm + (WR - 64) * wm + 64, bn, wm, wn, wid, lane, P.C, P.aux, D.pre,
+                                  kb[(NP + 7) / 8 - 1]);
   }
   stamp_end(P.stamps, t_start);
 }
@@ -723,11 +734,12 @@ int launch_fixup(int epi, const GemmP& P, const float* ws, int nsplit, hipStream
 }
 
 template <int TM, int TN, int NLOC>
-int launch_skinny_t(int epi, const GemmP& P, int nsplit, float* part, int* ticket, hipStream_t s) {
+int launch_skinny_t(int epi, const GemmP& P, int nsplit, float* part, int* ticket, int scatter, int* xcc_out,
+                    hipStream_t s) {
   const int tm = (P.M + 16 * TM - 1) / (16 * TM), tn = (P.N + 16 * TN - 1) / (16 * TN);
   dim3 grid(8 * ((tm * tn + 7) / 8) * nsplit), block(NT);   // gemm_skinny.h: 8 XCD ranges x splits
   switch (epi) {
-#define CASE(E) case E: hipLaunchKernelGGL((gemm_skinny_kernel<E, TM, TN, NLOC>), grid, block, 0, s, P, tm, tn, nsplit, part, ticket); break;
+#define CASE(E) case E: hipLaunchKernelGGL((gemm_skinny_kernel<E, TM, TN, NLOC>), grid, block, 0, s, P, tm, tn, nsplit, part, ticket, scatter, xcc_out); break;
     CASE(MMS_EPI_F16) CASE(MMS_EPI_RELU_DROP) CASE(MMS_EPI_DROP_RESID)
     CASE(MMS_EPI_GATE) CASE(MMS_EPI_RELU_DROP_BWD) CASE(MMS_EPI_F16_ACC) CASE(MMS_EPI_GELU_DROP) CASE(MMS_EPI_GELU_DROP_BWD)
 #undef CASE
@@ -739,16 +751,22 @@ int launch_skinny_t(int epi, const GemmP& P, int nsplit, float* part, int* ticke
 // (tile code, chunks per wave): 44 = 64x64 tiles (NLOC <= 2: 64 accumulator + 2 x 64 operand VGPRs
 // keep two blocks per CU), 24 = 32x64 and 22 = 32x32 (NLOC <= 3)
 struct SkinnyPlan { int code = 0, nloc = 0, nsplit = 1; };
+// test hooks (mms2ut_gemm_skinny_debug): deal a tile's splits over different XCDs; record each
+// block's hardware XCD id
+int g_skinny_scatter = 0;
+int* g_skinny_xcc = nullptr;
 int launch_skinny(const SkinnyPlan& pl, int epi, const GemmP& P, float* part, int* ticket, hipStream_t s) {
+  const int sc = pl.nsplit > 1 ? g_skinny_scatter : 0;
+  int* xo = g_skinny_xcc;
   switch (pl.code * 10 + pl.nloc) {
-    case 441: return launch_skinny_t<4, 4, 1>(epi, P, pl.nsplit, part, ticket, s);
-    case 442: return launch_skinny_t<4, 4, 2>(epi, P, pl.nsplit, part, ticket, s);
-    case 241: return launch_skinny_t<2, 4, 1>(epi, P, pl.nsplit, part, ticket, s);
-    case 242: return launch_skinny_t<2, 4, 2>(epi, P, pl.nsplit, part, ticket, s);
-    case 243: return launch_skinny_t<2, 4, 3>(epi, P, pl.nsplit, part, ticket, s);
-    case 221: return launch_skinny_t<2, 2, 1>(epi, P, pl.nsplit, part, ticket, s);
-    case 222: return launch_skinny_t<2, 2, 2>(epi, P, pl.nsplit, part, ticket, s);
-    case 223: return launch_skinny_t<2, 2, 3>(epi, P, pl.nsplit, part, ticket, s);
+    case 441: return launch_skinny_t<4, 4, 1>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
+    case 442: return launch_skinny_t<4, 4, 2>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
+    case 241: return launch_skinny_t<2, 4, 1>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
+    case 242: return launch_skinny_t<2, 4, 2>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
+    case 243: return launch_skinny_t<2, 4, 3>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
+    case 221: return launch_skinny_t<2, 2, 1>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
+    case 222: return launch_skinny_t<2, 2, 2>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
+    case 223: return launch_skinny_t<2, 2, 3>(epi, P, pl.nsplit, part, ticket, sc, xo, s);
     default: mms::set_error("gemm: bad short-M plan %d/%d", pl.code, pl.nloc); return 1;
   }
 }
@@ -1100,7 +1118,7 @@ static int skinny_mode() {
   }
   return g_skinny_mode;
 }
-constexpr int kTicketCap = 16384;   // tiles per launch with a K split
+constexpr int kTicketCap = 2048;   // tiles per launch with a K split (every short-M grid of 32x32 tiles fits)
 static bool skinny_eligible(const mms2ut_gemm_args* a) {
   if (!skinny_mode() || !a || !a->a_kcontig || !a->b_kcontig || a->batch != 1 || a->epi == MMS_EPI_F32 ||
       a->rowsum || a->K <= 0 || a->K % 256 || a->M <= 0 || a->N <= 0)
@@ -1154,25 +1172,57 @@ static SkinnyPlan skinny_plan(const mms2ut_gemm_args* a, bool can_split) {
   }
   return best;
 }
-// Per-stream ticket arrays of the split plans (zeroed once; every launch leaves them zero).
-// Allocated on a stream's first split launch; none while the stream is capturing (that launch
-// takes an unsplit plan).
+// Ticket arrays of the split plans: one 8 KiB slice (kTicketCap tiles) per (device, stream) out of
+// a per-device pool allocated and zeroed once, on the first split launch of the device; every
+// completed launch leaves its slice zero (the reducers re-arm their tickets), a failed launch gets
+// its slice re-zeroed in stream order.  Slices are handed out under a mutex (autograd's device
+// thread and the main thread both issue GEMMs).  A stream that first needs a slice while the device
+// has no pool yet and the stream is capturing cannot get one: that launch fails loudly (the plan —
+// and so the bits — never depends on whether tickets exist).
+constexpr int kTicketSlices = 512;
 static int* skinny_tickets(hipStream_t stream) {
-  static hipStream_t keys[64];
-  static int* vals[64];
-  static int n = 0;
-  for (int i = 0; i < n; ++i)
-    if (keys[i] == stream) return vals[i];
-  if (n == 64) return nullptr;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-  int* p = nullptr;
-  if (hipMalloc(&p, kTicketCap * sizeof(int)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(p, 0, kTicketCap * sizeof(int), stream) != hipSuccess) { hipFree(p); return nullptr; }
-  keys[n] = stream; vals[n] = p; ++n;
-  return p;
+  static std::mutex mu;
+  struct Slot { int dev; hipStream_t s; };
+  static int* pool[16] = {nullptr};
+  static Slot slots[16][kTicketSlices];
+  static int used[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) {
+    mms::set_error("gemm: short-M split tickets: no current device");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  for (int i = 0; i < used[dev]; ++i)
+    if (slots[dev][i].s == stream) return pool[dev] + (long)i * kTicketCap;
+  if (!pool[dev]) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) {
+      mms::set_error("gemm: short-M split tickets are allocated on the device's first split launch, which must "
+                     "not be inside a stream capture (run the step eagerly once first)");
+      return nullptr;
+    }
+    int* p = nullptr;
+    const size_t bytes = (size_t)kTicketSlices * kTicketCap * sizeof(int);
+    if (hipMalloc(&p, bytes) != hipSuccess || hipMemset(p, 0, bytes) != hipSuccess) {
+      if (p) (void)hipFree(p);
+      mms::set_error("gemm: short-M split tickets: allocation failed");
+      return nullptr;
+    }
+    pool[dev] = p;
+  }
+  if (used[dev] == kTicketSlices) {
+    mms::set_error("gemm: short-M split tickets: more than %d streams on device %d", kTicketSlices, dev);
+    return nullptr;
+  }
+  slots[dev][used[dev]] = Slot{dev, stream};
+  return pool[dev] + (long)(used[dev]++) * kTicketCap;
 }
 static int skinny_pick(const mms2ut_gemm_args* a) { return skinny_plan(a, a && a->splitk_ws).code; }
+extern "C" int mms2ut_gemm_skinny_debug(int scatter, int* xcc_out) {
+  g_skinny_scatter = scatter ? 1 : 0;
+  g_skinny_xcc = xcc_out;
+  return 0;
+}
 extern "C" int mms2ut_gemm_set_skinny(int mode) {
   MMS_REQUIRE(mode >= 0 && mode <= 2, "gemm_set_skinny: mode must be 0, 1 or 2 (got %d)", mode);
   g_skinny_mode = mode;
@@ -1279,13 +1329,16 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     P.vec16 = v ? 1 : 0;
   }
   if (splitk == 1 && skinny_eligible(a)) {
-    int* tickets = a->splitk_ws ? skinny_tickets(stream) : nullptr;
-    const SkinnyPlan pl = skinny_plan(a, tickets != nullptr);
+    const SkinnyPlan pl = skinny_plan(a, a->splitk_ws != nullptr);
     if (pl.code) {
+      int* tickets = nullptr;
+      if (pl.nsplit > 1 && !(tickets = skinny_tickets(stream))) return 1;
       const int q = pl.code / 10, r = pl.code % 10;
       const long tiles = (long)((a->M + 16 * q - 1) / (16 * q)) * ((a->N + 16 * r - 1) / (16 * r));
       P.stamps = stamp_take(8 * ((tiles + 7) / 8) * pl.nsplit);
-      return launch_skinny(pl, a->epi, P, pl.nsplit > 1 ? a->splitk_ws : nullptr, tickets, stream);
+      const int rc = launch_skinny(pl, a->epi, P, pl.nsplit > 1 ? a->splitk_ws : nullptr, tickets, stream);
+      if (rc && tickets) (void)hipMemsetAsync(tickets, 0, kTicketCap * sizeof(int), stream);   // re-arm after a failure
+      return rc;
     }
   }
   const int tm = (a->M + BM - 1) / BM, tn = (a->N + BN - 1) / BN;

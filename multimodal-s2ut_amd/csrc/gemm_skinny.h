@@ -11,33 +11,46 @@
 //     NLOC chunks each), each accumulating the whole tile; the four partial tiles are summed through
 //     LDS in wave order;
 //   * S == 1: the epilogue runs right there;  S > 1: the block writes its fp32 partial tile to the
-//     workspace, and the LAST of the tile's S blocks to arrive (one atomic ticket per tile; all S
-//     blocks of a tile run on one XCD, so the partials meet in its L2) sums the S partials in split
-//     order and runs the epilogue, then re-arms the ticket (0) for the next launch on the stream.
-//     Split order and wave order are fixed, so results do not depend on scheduling.
+//     workspace and the LAST of the tile's S blocks to arrive (one atomic ticket per tile) sums the
+//     S partials in split order and runs the epilogue, then re-arms the ticket (0) for the next
+//     launch on the stream.  Split order and wave order are fixed, so results do not depend on
+//     scheduling or placement.
+// The partial-tile hand-off is placement-independent (cdna_hip_programming.md §6 Guideline 16, the
+// split-K recipe's write-through form): partials are stored sc1 (write-through, no release fence
+// needed), every storing wave drains (vmcnt(0)) before the block's barrier, one lane takes the
+// ticket (relaxed agent-scope atomic), and the reducer reads EVERY partial with sc1 loads (L1
+// bypassed, so no stale line of this CU can be read).  Keeping a tile's splits on one XCD (the
+// bid % 8 ranges below) is a speed choice only; `scatter` deals them over different XCDs (tests).
 // Rows past M / columns past N read a clamped (valid) row and are dropped at the store.
 // Requires A and B K-contiguous, K % (256 * NLOC * S) == 0, batch 1 (host routing: skinny_pick).
 
+typedef unsigned int sk_u32x4 __attribute__((ext_vector_type(4)));
+
 template <int EPI, int TM, int TN, int NLOC>
 __global__ void __launch_bounds__(NT, 2) gemm_skinny_kernel(GemmP P, int tiles_m, int tiles_n, int nsplit,
-                                                             float* __restrict__ part, int* __restrict__ ticket) {
+                                                             float* __restrict__ part, int* __restrict__ ticket,
+                                                             int scatter, int* __restrict__ xcc_out) {
   constexpr int BMS = 16 * TM, BNS = 16 * TN, LDR = BNS + 4;   // LDR: padded fp32 row of the reduction tile
   __shared__ __attribute__((aligned(16))) float red[4 * BMS * LDR];
   __shared__ int is_last;
   const unsigned long long t_start = P.stamps ? stamp_now() : 0ull;
   if (P.thresh) P.seed = mms_step_seed(P.seed);
-  // XCD-aware order (workgroups go round-robin over the 8 XCDs, bid % 8): XCD x owns one contiguous
-  // range of column-major tiles (tiles sharing a weight slice share its L2) with ALL splits of each
-  // of them, so a tile's partials meet in one L2 — no cross-XCD traffic, no L2 writeback/invalidate.
-  // The grid is 8 x (longest range) x nsplit; blocks past a shorter range only stamp.
+  // XCD-aware order (workgroups are observed to go round-robin over the 8 XCDs, bid % 8): group x
+  // owns one contiguous range of column-major tiles (tiles sharing a weight slice share an L2) with
+  // ALL splits of each of them, so a tile's partials stay in one L2 — a speed choice, the hand-off
+  // below is correct for any placement.  scatter != 0 puts split s of a tile in group (owner + s) % 8
+  // instead (tests: the splits then meet across XCDs).  The grid is 8 x (longest range) x nsplit;
+  // blocks past a shorter range only stamp.
   const int T = tiles_m * tiles_n, q = T / 8, r = T % 8;
   const int x = blockIdx.x % 8, j = blockIdx.x / 8;
   const int lt = j / nsplit, split = j % nsplit;
-  if (lt >= q + (x < r ? 1 : 0)) {
+  const int owner = scatter ? (x + 8 * nsplit - split) % 8 : x;
+  if (xcc_out && threadIdx.x == 0) xcc_out[blockIdx.x] = (int)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11));
+  if (lt >= q + (owner < r ? 1 : 0)) {
     stamp_end(P.stamps, t_start);
     return;
   }
-  const int tile = x * q + min(x, r) + lt;
+  const int tile = owner * q + min(owner, r) + lt;
   const int tm = tile % tiles_m, tn = tile / tiles_m;
   const int bm = tm * BMS, bn = tn * BNS;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -115,39 +128,38 @@ __global__ void __launch_bounds__(NT, 2) gemm_skinny_kernel(GemmP P, int tiles_m
     return;
   }
 
-  // split-K: partial tile -> workspace [tile][split][BMS x BNS]; the last arrival reduces
+  // split-K: partial tile -> workspace [tile][split][BMS x BNS], written through (sc1)
   float* tile_part = part + (long)tile * nsplit * (BMS * BNS);
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)tile_part, (short)0, (int)((long)nsplit * BMS * BNS * 4), 0x00020000);
   for (int o = threadIdx.x; o < ITEMS; o += NT) {
     const int row = o / (BNS / 8), c8 = (o % (BNS / 8)) * 8;
     float v[8];
     wave_sum(row, c8, v);
-    float* dst = tile_part + (long)split * (BMS * BNS) + row * BNS + c8;
-    *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<f32x4*>(dst + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    const int off = ((split * (BMS * BNS)) + row * BNS + c8) * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sk_u32x4, f32x4{v[0], v[1], v[2], v[3]}), rp, off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sk_u32x4, f32x4{v[4], v[5], v[6], v[7]}), rp, off + 16, 0, 16);
   }
-  // Release: every thread's partial stores have completed (acknowledged by the XCD's L2, the one
-  // all the tile's splits share) before the ticket is taken.  No agent-scope fence: on this chip it
-  // writes back / invalidates the whole L2 (measured: 60-100 us per block).  The reducing block reads
-  // the partials from that L2 — its L1 never held those lines in this launch (invalidated at kernel
-  // start, never read since).
+  // every storing wave drains its write-through stores, then ONE lane takes the ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) is_last = atomicAdd(ticket + tile, 1) == nsplit - 1;
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add(ticket + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
   __syncthreads();
   if (is_last) {
     for (int o = threadIdx.x; o < ITEMS; o += NT) {
       const int row = o / (BNS / 8), c8 = (o % (BNS / 8)) * 8;
       float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const float* src = tile_part + row * BNS + c8;
+      const int src = (row * BNS + c8) * 4;
       // four splits' loads in flight at a time (indices clamped: the loads are unconditional, the
-      // adds of clamped duplicates are skipped), summed in split order
+      // adds of clamped duplicates are skipped), summed in split order; every load sc1
       for (int s0 = 0; s0 < nsplit; s0 += 4) {
         f32x4 lo[4], hi[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const long off = (long)min(s0 + u, nsplit - 1) * (BMS * BNS);
-          lo[u] = *reinterpret_cast<const f32x4*>(src + off);
-          hi[u] = *reinterpret_cast<const f32x4*>(src + off + 4);
+          const int off = src + min(s0 + u, nsplit - 1) * (BMS * BNS * 4);
+          lo[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 16));
+          hi[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, off + 16, 0, 16));
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -157,7 +169,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_skinny_kernel(GemmP P, int tiles_m
       }
       epilogue_store8<EPI>(P, P.C, P.aux, bm + row, bn + c8, v);
     }
-    if (threadIdx.x == 0) ticket[tile] = 0;   // re-armed for the next launch (stream-ordered)
+    // re-armed for the next launch on the stream (every block of this tile has taken its ticket)
+    if (threadIdx.x == 0) __hip_atomic_store(ticket + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   stamp_end(P.stamps, t_start);
 }

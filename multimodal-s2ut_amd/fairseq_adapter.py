@@ -62,6 +62,36 @@ class _GroupBridge(torch.autograd.Function):
         return (None, None, *[P.g[n] for n in fctx.names])
 
 
+class _LinkedBridge(torch.autograd.Function):
+    """The gradient hand-off connected to the loss (``grad_release = "at_end"``): its output is the
+    model node's anchor, so the loss graph reaches every parameter through it and the engine runs
+    this backward after the model node's backward has filled the flat gradient and joined its side
+    stream.  Needed wherever something walks the graph from the loss to the parameters: torch DDP
+    with find_unused_parameters (fairseq --find-unused-parameters) or static_graph,
+    ``loss.backward(inputs=params)``, ``torch.autograd.grad(loss, params)``."""
+
+    @staticmethod
+    def forward(fctx, net, names, *params):
+        fctx.net, fctx.names = net, names
+        return net.anchor.detach().clone()
+
+    @staticmethod
+    def backward(fctx, g):
+        P = fctx.net.params
+        return (None, None, *[P.g[n] for n in fctx.names])
+
+
+def _ddp_walks_graph():
+    """True inside the forward of a torch DDP wrapper that walks the autograd graph from the outputs
+    (find_unused_parameters or static_graph): the per-group bridges' outputs are graph roots of
+    their own, so such a DDP would find no parameter behind the loss, mark every one unused and
+    then see each marked ready a second time when the groups are released."""
+    get = getattr(torch.nn.parallel.DistributedDataParallel, "_get_active_ddp_module", None)
+    ddp = get() if get is not None else None
+    return ddp is not None and bool(getattr(ddp, "find_unused_parameters", False) or
+                                    getattr(ddp, "static_graph", False))
+
+
 class _GradRelease:
     """Installed as the model's ``grad_ready_hook`` for one forward/backward.  The backward calls
     ``ready(offset)`` each time the flat gradient below ``offset`` is final (after every layer);
@@ -282,12 +312,20 @@ def register(fairseq):
                     self._groups.append((end, names, [self.get_parameter(n) for n in names]))
             self.encoder_adapter, self.decoder_adapter = impl.encoder, impl.decoder
             self.multitask_decoders = {}
+            # "per_group": each parameter group's gradients reach autograd (and torch DDP's bucket
+            # hooks) as soon as the hand-written backward has finished them; "at_end": one bridge on
+            # the loss path hands every gradient over after the backward (the form for a DDP that
+            # walks the graph — chosen automatically for one — and for backward(inputs=...) /
+            # autograd.grad over the parameters)
+            self.grad_release = "per_group"
 
         @classmethod
         def build_model(cls, args, task):
             cfg = plugins.cfg_from_args(args, task.impl.multimodal_translation_config, task.impl.vocab_size)
             dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
             model = cls(plugins.MM_S2UTTransformerModel(cfg, device=dev, seed=getattr(args, "seed", 1)))
+            if getattr(args, "find_unused_parameters", False):   # fairseq wraps DDP with it
+                model.grad_release = "at_end"
             if task.multitask_tasks:
                 # fairseq S2STransformerMultitaskModelBase.build_model: one decoder per task on the
                 # encoder (or decoder) states, fairseq's own modules
@@ -319,10 +357,17 @@ def register(fairseq):
             impl, net = self.impl, self.impl.net
             batch = impl._batch(src_tokens, src_lengths, prev_output_tokens, imgs_list, img_masks_list,
                                 extra_input=kw)
+            anchor = net.anchor
             if torch.is_grad_enabled():
-                rel = _GradRelease(net, [(end, _GroupBridge.apply(net, names, *ps)) for end, names, ps in self._groups])
-                net.grad_ready_hook, net.grad_release_finish = rel.ready, rel.finish
-            outs = runtime._ModelFn.apply(net.anchor, net, batch, True)
+                if self.grad_release not in ("per_group", "at_end"):
+                    raise ValueError(f"grad_release must be 'per_group' or 'at_end' (got {self.grad_release!r})")
+                if self.grad_release == "per_group" and not _ddp_walks_graph():
+                    rel = _GradRelease(net, [(end, _GroupBridge.apply(net, names, *ps))
+                                             for end, names, ps in self._groups])
+                    net.grad_ready_hook, net.grad_release_finish = rel.ready, rel.finish
+                else:
+                    anchor = _LinkedBridge.apply(net, self._names, *self._params)
+            outs = runtime._ModelFn.apply(anchor, net, batch, True)
             logits = outs[0]
             B, Tt = prev_output_tokens.shape
             cfg = impl.cfg

@@ -135,7 +135,10 @@ class Trainer:
         K.stream_wait(self.stream, cur)
         with torch.cuda.stream(self.stream):
             log = self._train_step(batches)
-        K.stream_wait(cur, self.stream)
+        # the hand-back to the caller's stream is where the host reads the loss or starts copies /
+        # peer collectives: a system-scope event (torch's), one per step; the internal fork / joins
+        # stay on device-scope events
+        cur.wait_stream(self.stream)
         return log
 
     def _graph_step(self, batches, prologue, eager, draws):
@@ -180,7 +183,7 @@ class Trainer:
             with torch.cuda.stream(self.stream):
                 entry[0].replay()
             log = self.log
-        K.stream_wait(cur, self.stream)
+        cur.wait_stream(self.stream)   # system-scope hand-back (see train_step)
         return log
 
     def _train_step(self, batches):

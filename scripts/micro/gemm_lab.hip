@@ -13,6 +13,7 @@
 
 #include "lab_gemm_wide.h"
 #include "lab_gemm_persist.h"
+#include "lab_gemm_stagger.h"
 
 
 // ---------------------------------------------------------------------------------------------
@@ -229,15 +230,22 @@ static int run_variant(const Variant& v, const mms2ut_gemm_args& a, hipStream_t 
   GemmP P = make_p(a);
   if (v.kind == 4) return launch_tallp(a.epi, v.bm, v.var, P, s);
   if (v.kind == 5) return launch_persist(a.epi, v.bm, v.var, P, s);
+  if (v.kind == 6) return mmst::launch_stag(a.epi, v.bm, v.var, P, s);
   return mmsw::launch_wide(a.epi, v.bm, v.var, P, s, v.kind == 3);
 }
 
 int main(int argc, char** argv) {
+#ifdef MMS_LAB_NOSTORE
+  printf("# build: staged epilogue without its C stores (MMS_LAB_NOSTORE)\n");
+#endif
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
   const int only = argc > 2 ? atoi(argv[2]) : -1;
   std::vector<Shape> shapes = {
       {"sq8192", 8192, 8192, 8192, MMS_EPI_F16, 0.f},
       {"fc1_fwd", 10000, 3072, 768, MMS_EPI_RELU_DROP, 0.1f},
+      {"fc1_plain", 10000, 3072, 768, MMS_EPI_F16, 0.f},
+      {"fc1_relu", 10000, 3072, 768, MMS_EPI_RELU_DROP, 0.f},
+      {"fc1_resid", 10000, 3072, 768, MMS_EPI_DROP_RESID, 0.1f},
       {"qkv_fwd", 10000, 2304, 768, MMS_EPI_F16, 0.f},
       {"fc2_dgrad", 10000, 3072, 768, MMS_EPI_RELU_DROP_BWD, 0.1f},
       {"out_proj", 10000, 768, 768, MMS_EPI_DROP_RESID, 0.1f},
@@ -249,10 +257,11 @@ int main(int argc, char** argv) {
   };
   std::vector<Variant> vars = {
       {"lib", 0, 0, 0},
-      {"w2_256", 2, 2256, 0},
-      {"ne2_256", 3, 2256, 0},
-      {"ne2_256_nodma", 3, 2256, 1},
-      {"ne2_256_nomfma", 3, 2256, 4},
+      {"st160", 6, 160, 0},
+      {"st160_noepi", 6, 160, 2000},
+      {"st160_raw", 6, 160, 3000},
+      {"st192", 6, 192, 0},
+      {"st192_noepi", 6, 192, 2000},
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -289,7 +298,7 @@ int main(int argc, char** argv) {
       for (size_t i = 0; i < hc.size(); ++i) m += hc[i] != href[i];
       mism[vi] = m;
     }
-    if (si == 1) {   // co-residency census of the persistent grid (512 blocks)
+    if (si == 99) {   // co-residency census of the persistent grid (512 blocks)
       unsigned long long* d_hw;
       CK(hipMalloc(&d_hw, 512 * 8));
       CK(hipMemcpyToSymbol(HIP_SYMBOL(g_lab_hw), &d_hw, sizeof(d_hw)));

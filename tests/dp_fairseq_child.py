@@ -8,7 +8,8 @@ both ranks sharing cuda:0) — launched by tests/test_gpu_dp_fairseq.py as a fre
 fairseq-train's distributed path restated (tests/fairseq_stub.py stands in for fairseq, which is
 not importable): setup_task -> load_dataset -> build_model -> .half() -> torch DDP with fairseq's
 settings (distributed_fairseq_model: bucket_cap_mb 25, broadcast_buffers False,
-find_unused_parameters False; a 1 MB variant as well) behind fairseq's ModuleProxyWrapper ->
+find_unused_parameters False; a 1 MB variant, and a 25 MB one with find_unused_parameters True
+= fairseq --find-unused-parameters) behind fairseq's ModuleProxyWrapper ->
 criterion(model, sample) -> loss.backward().  Rank r trains on batch r of the iterator.  Two
 iterations per bucket size (DDP rebuilds its buckets in gradient-ready order after the first);
 a DDP communication hook logs, per bucket, whether the hand-written backward was still running
@@ -34,6 +35,7 @@ mm = importlib.import_module("multimodal-s2ut_amd")
 
 NODROP = "--dropout 0 --attention-dropout 0 --relu-dropout 0"
 BUCKETS_MB = (25, 1)
+RUNS = ((25, False), (1, False), (25, True))   # (bucket MB, find_unused_parameters)
 
 
 class _SetItem:
@@ -78,11 +80,12 @@ def setup(tmp):
     return fs, model, crit, batches
 
 
-def run(rank, world, bucket_mb, tmp, out_dir):
-    fs, model, crit, batches = setup(os.path.join(tmp, f"r{rank}_b{bucket_mb}"))
+def run(rank, world, bucket_mb, tmp, out_dir, find_unused=False):
+    tag = f"b{bucket_mb}" + ("u" if find_unused else "")
+    fs, model, crit, batches = setup(os.path.join(tmp, f"r{rank}_{tag}"))
     net = model.impl.net
     ddp = torch.nn.parallel.DistributedDataParallel(model, bucket_cap_mb=bucket_mb, broadcast_buffers=False,
-                                                    find_unused_parameters=False)
+                                                    find_unused_parameters=find_unused)
     launches = []
 
     def hook(state, bucket):
@@ -109,15 +112,15 @@ def run(rank, world, bucket_mb, tmp, out_dir):
         torch.cuda.synchronize()
         per_iter.append(np.array(launches, dtype=np.int64).reshape(-1, 3))
     g = torch.cat([p.grad.float().flatten() for _, p in model.named_parameters()]).cpu().numpy()
-    np.savez(os.path.join(out_dir, f"rank{rank}_b{bucket_mb}.npz"), grad=g, launches0=per_iter[0],
+    np.savez(os.path.join(out_dir, f"rank{rank}_{tag}.npz"), grad=g, launches0=per_iter[0],
              launches1=per_iter[1])
 
 
 def main(out_dir, tmp):
     rank, world, local = mm.parallel.init_from_env()
     torch.cuda.set_device(local)
-    for mb in BUCKETS_MB:
-        run(rank, world, mb, tmp, out_dir)
+    for mb, unused in RUNS:
+        run(rank, world, mb, tmp, out_dir, unused)
         dist.barrier()
     dist.destroy_process_group()
 

@@ -62,7 +62,9 @@ def ddp_run(tmp_path_factory):
             raise
         logs.append(o.decode(errors="replace")[-3000:])
     assert all(p.returncode == 0 for p in procs), logs
-    return {mb: [dict(np.load(out / f"rank{r}_b{mb}.npz")) for r in range(2)] for mb in BUCKETS_MB}
+    runs = {mb: [dict(np.load(out / f"rank{r}_b{mb}.npz")) for r in range(2)] for mb in BUCKETS_MB}
+    runs["unused"] = [dict(np.load(out / f"rank{r}_b25u.npz")) for r in range(2)]
+    return runs
 
 
 @pytest.mark.parametrize("mb", BUCKETS_MB)
@@ -74,6 +76,16 @@ def test_ddp_ranks_bit_identical(ddp_run, mb):
 
 def test_ddp_bucket_size_invariant(ddp_run):
     assert np.array_equal(ddp_run[BUCKETS_MB[0]][0]["grad"], ddp_run[BUCKETS_MB[1]][0]["grad"])
+
+
+def test_ddp_find_unused_parameters(ddp_run):
+    """fairseq --find-unused-parameters: DDP walks the graph from the loss, so the adapter switches
+    to the loss-linked gradient bridge (fairseq_adapter._LinkedBridge).  Ranks agree bit
+    for bit, and the averaged gradient is the per-group release's bit for bit."""
+    r0, r1 = ddp_run["unused"]
+    assert np.isfinite(r0["grad"]).all()
+    assert np.array_equal(r0["grad"], r1["grad"])
+    assert np.array_equal(r0["grad"], ddp_run[BUCKETS_MB[0]][0]["grad"])
 
 
 def test_ddp_buckets_overlap_backward(ddp_run):

@@ -103,6 +103,32 @@ def test_gemm_epilogues(K):
     assert rel(out, (1 - gr) * t + gr * o) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(10000, 3072, 768), (12000, 768, 768), (5000, 768, 768), (2000, 768, 192),
+                                    (333, 520, 256)])
+def test_gemm_dropout_masks_every_tile(K, M, N, Kd):
+    """The dropout keep flags of the fused GEMM epilogues — computed inside the k-loop on the fast
+    path (gemm_common.h epi_bits_step, round 6) or hashed in the epilogue (odd counter offset) — equal
+    the standalone dropout kernel's mask for the same counters, on every tile height (128 / 96 / 160
+    / 192 rows) and for the ReLU, residual and GELU sites.  A bias of 30 keeps every activation
+    positive, so the zero pattern of the output is the mask."""
+    x = (0.1 * torch.randn(M, Kd, device="cuda")).half()
+    W = (0.05 * torch.randn(N, Kd, device="cuda")).half()
+    big = torch.full((N,), 30.0, device="cuda").half()
+    zero = torch.zeros(M, N, device="cuda").half()
+    z = torch.empty(M, N, device="cuda").half()
+    try:
+        for mode in (0, 2, 3, 5):
+            K.call("mms2ut_gemm_set_tall", mode)
+            for seed, off in ((77, 4096), (78, 4097), (79, 2 ** 33 - 4 * N)):
+                m = K.dropout_mask(M * N, 0.1, seed, off, "cuda").view(M, N) != 0
+                for epi, kw in ((K.EPI_RELU_DROP, {}), (K.EPI_DROP_RESID, dict(aux=zero)),
+                                (K.EPI_GELU_DROP, dict(out2=z))):
+                    y = K.linear(x, W, big, epi=epi, p=0.1, drop=(seed, off), **kw)
+                    assert torch.equal(y != 0, m), (mode, seed, off, epi)
+    finally:
+        K.call("mms2ut_gemm_set_tall", 1)
+
+
 def test_wgrad_splitk(K):
     M, N, K_ = 5000, 96, 200
     dy = torch.randn(M, N, device="cuda").half()

@@ -328,10 +328,18 @@ def test_fairseq_dropin_trains_like_native(monkeypatch, tmp_path):
     names = [n for n, _ in model.named_parameters()]
     model.train()
     runs = {}
-    for kind in ("fairseq", "alias", "native"):
+    for kind in ("fairseq", "alias", "native", "at_end"):
         model.zero_grad(set_to_none=True)
         net.drop.reset(7)
-        if kind == "native":
+        if kind == "at_end":
+            # the loss-linked bridge: torch.autograd.grad over the parameters works
+            model.grad_release = "at_end"
+            loss, ss, log = alias(model, sample)
+            grads = torch.autograd.grad(loss, [p for _, p in model.named_parameters()])
+            model.grad_release = "per_group"
+            torch.cuda.synchronize()
+            g = {n: gr.clone() for (n, _), gr in zip(model.named_parameters(), grads)}
+        elif kind == "native":
             net.params.grad.zero_()                # as the native Trainer does per micro-batch
             loss, ss, log = P.SpeechToUnitCriterion(task.impl, 0.2)(model.impl, sample)
             loss.backward()
@@ -352,6 +360,8 @@ def test_fairseq_dropin_trains_like_native(monkeypatch, tmp_path):
     la, ga = runs["alias"]
     lf, gf = runs["fairseq"]
     assert la == ln and all(torch.equal(ga[n], gn[n]) for n in names)
+    le, ge = runs["at_end"]
+    assert le == ln and all(torch.equal(ge[n], gn[n]) for n in names)
     assert abs(lf - ln) / abs(ln) < 1e-5, (lf, ln)
     assert _rel_all(gf, gn, names) < 5e-3
     fusion = [n for n in names if n.startswith("encoder.multimodal_attns.0.") and n.endswith("weight")]
