@@ -346,6 +346,11 @@ int mms2ut_gate_bwd(const mms2ut_half* dres, const mms2ut_half* merge, const mms
 /* copy rows with strides (cols fp16 elements)                                               */
 int mms2ut_copy2d(const mms2ut_half* src, int64_t lds, mms2ut_half* dst, int64_t ldd, int64_t rows,
                   int cols, hipStream_t stream);
+/* copy2d, and columns [cols, cols + zcols) of every dst row set to zero in the same launch
+ * (src may be NULL with cols = 0: a strided zero fill) — the zero-padded weight / key layouts of
+ * the subsampler and the fusion without a separate memset                                     */
+int mms2ut_copy2d_pad(const mms2ut_half* src, int64_t lds, mms2ut_half* dst, int64_t ldd, int64_t rows,
+                      int cols, int zcols, hipStream_t stream);
 /* out = a + b (fp16) */
 int mms2ut_add_f16(const mms2ut_half* a, const mms2ut_half* b, mms2ut_half* out, int64_t n,
                    hipStream_t stream);
@@ -360,6 +365,11 @@ int mms2ut_add_f16(const mms2ut_half* a, const mms2ut_half* b, mms2ut_half* out,
 int mms2ut_ls_xent_fwd(const mms2ut_half* logits, int64_t ld, const int64_t* target, int64_t rows,
                        int V, float eps, int pad_idx, float* lse, float* part, float* loss_out,
                        hipStream_t stream);
+/* the same, for a trainer's step log: acc[0..1] += {loss, nll} (may be NULL) and call_out[0..1] =
+ * this call's {loss, nll} (written, may be NULL) — no zeroed accumulator and no copies        */
+int mms2ut_ls_xent_fwd_log(const mms2ut_half* logits, int64_t ld, const int64_t* target, int64_t rows,
+                           int V, float eps, int pad_idx, float* lse, float* part, float* acc, float* call_out,
+                           hipStream_t stream);
 /* dlogits = grad * ((1-eps-eps_i)(p - onehot) + eps_i(V p - 1)), 0 on pad rows; in place OK */
 int mms2ut_ls_xent_bwd(const mms2ut_half* logits, int64_t ld, const int64_t* target, int64_t rows,
                        int V, float eps, int pad_idx, const float* lse, const float* grad,
@@ -411,6 +421,10 @@ int mms2ut_grad_norm_check(float* buf, int world, int rank, float* ost, int stag
 /* x *= alpha in place (fp16, n % 8 == 0): the data-parallel gradient pre-division by world size
  * (torch DDP's allreduce hook divides each bucket before its SUM all-reduce)                    */
 int mms2ut_scale_f16(mms2ut_half* x, int64_t n, float alpha, hipStream_t stream);
+/* dst[0..n) = vals[0..n) (fp32, n <= 8; vals is a host array read at the call, passed to the
+ * kernel as arguments): the trainer's per-step log vector (loss / nll / ntokens / nsentences /
+ * sample size) initialised in one launch instead of a fill per slot                          */
+int mms2ut_set_f32(float* dst, int n, const float* vals, hipStream_t stream);
 /* acc (fp32) += x (fp16), n % 8 == 0: gradient accumulation over --update-freq micro-batches    */
 int mms2ut_accum_f16_f32(float* acc, const mms2ut_half* x, int64_t n, hipStream_t stream);
 int mms2ut_adam_fp16_master(mms2ut_half* param, const mms2ut_half* grad, float* master,

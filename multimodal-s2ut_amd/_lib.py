@@ -158,6 +158,7 @@ SIGNATURES = {
     "mms2ut_ctc_loss_bwd": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp, vp, i32, vp, vp, vp, i64, vp]),
     "mms2ut_scale_f16": (i32, [vp, i64, f32, vp]),
     "mms2ut_accum_f16_f32": (i32, [vp, vp, i64, vp]),
+    "mms2ut_set_f32": (i32, [vp, i32, vp, vp]),
     "mms2ut_splitk_reduce": (i32, [vp, i32, i64, i32, i32, vp, i64, i32, f32, vp]),
     "mms2ut_splitk_reduce_bias": (i32, [vp, i32, i64, i32, i32, vp, i64, vp, vp, vp]),
     "mms2ut_transpose_batch": (i32, [vp, vp, vp, i32, i32, vp]),
@@ -192,8 +193,10 @@ SIGNATURES = {
     "mms2ut_im2col_ld": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mms2ut_col2im": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mms2ut_gate_bwd": (i32, [vp, vp, vp, vp, vp, i64, i32, vp]),
+    "mms2ut_copy2d_pad": (i32, [vp, i64, vp, i64, i64, i32, i32, vp]),
     "mms2ut_copy2d": (i32, [vp, i64, vp, i64, i64, i32, vp]),
     "mms2ut_ls_xent_fwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp]),
+    "mms2ut_ls_xent_fwd_log": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp, vp]),
     "mms2ut_ls_xent_bwd": (i32, [vp, i64, vp, i64, i32, f32, i32, vp, vp, vp, vp]),
     "mms2ut_grad_sqnorm": (i32, [vp, i64, vp, i32, vp]),
     "mms2ut_grad_norm_finalize": (i32, [vp, i32, vp, vp, vp]),

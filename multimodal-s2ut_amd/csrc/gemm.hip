@@ -231,9 +231,6 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
 #define MMS_GEMM_DMA_AFTER_READS 0
 #endif
   constexpr bool READ_FIRST = !A_KC || !B_KC || MMS_GEMM_DMA_AFTER_READS;
-  // dropout keep bits of the lane's 8 epilogue passes, a share per k-step (epi_bits_step)
-  const EpiDrop D = epi_drop_setup<EPI>(P, bm + wm * 64 + (lane >> 3), bn + wn * 64 + 8 * (lane & 7), 8, nk);
-  uint64_t kb[1] = {0};
   // All 16 fragments of the stage are read before its MFMAs (the second k-half's reads no longer
   // wait behind the first half's MFMAs): 0-5 % faster isolated on the step's NT shapes, step flat
   // (profiles/round3_v5_gemm_read_all_ab.txt).
@@ -264,7 +261,6 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
       dma_tile<A_KC>(ra, SA(sb), P.lda, bm, k_rel(nxt, A_KC), wid, lane);
       dma_tile<B_KC>(rb, SB(sb), P.ldb, bn, k_rel(nxt, B_KC), wid, lane);
     }
-    if (epi_drops<EPI>() && D.pre) epi_bits_step<8>(P, D, kt, nk, kb);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       h16x8 fa[4], fb[4];
@@ -311,7 +307,7 @@ MMS_DEV void dma_gemm_tile(const GemmP& P, char* smem, int z, int tm, int tn) {
     for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
   (void)Cz; (void)auxz;
 #else
-  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz, D.pre, kb[0]);
+  staged_epilogue<EPI>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
 #endif
 }
 
@@ -380,10 +376,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
     dma_tile<true>(rb, SB(0), P.ldb, bn, 0, wid, lane);
   }
   constexpr bool PR = PRIO && EPI != MMS_EPI_F32;
-  // dropout keep bits of the lane's 2 FRT epilogue passes, a share per k-step (epi_bits_step)
-  constexpr int NP = 2 * FRT;
-  const EpiDrop D = epi_drop_setup<EPI>(P, bm + 16 * FRT * wm + (lane >> 3), bn + wn * 64 + 8 * (lane & 7), NP, nk);
-  uint64_t kb[(NP + 7) / 8] = {};
   for (int kt = 0; kt < nk; ++kt) {
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
@@ -400,7 +392,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb2[kk][j] = read_frag<true>(SB(cur), wn * 64 + j * 16, kk, lane);
     }
-    if (epi_drops<EPI>() && D.pre) epi_bits_step<NP>(P, D, kt, nk, kb);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       if (PR) __builtin_amdgcn_s_setprio(1);
@@ -419,12 +410,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
   // through the wave's 16 KiB staging area (staged_epilogue places wave rows at bm + 64 wm)
   constexpr int WR = 16 * FRT, F1 = FRT < 4 ? FRT : 4;
   staged_epilogue<EPI, F1>(P, smem, reinterpret_cast<const f32x4(&)[F1][4]>(acc[0]), bm + (WR - 64) * wm, bn, wm,
-                           wn, wid, lane, P.C, P.aux, D.pre, kb[0]);
+                           wn, wid, lane, P.C, P.aux);
   if constexpr (FRT > 4) {
     __syncthreads();
     staged_epilogue<EPI, FRT - 4>(P, smem, reinterpret_cast<const f32x4(&)[FRT - 4][4]>(acc[4]),
-                                  bm + (WR - 64) * wm + 64, bn, wm, wn, wid, lane, P.C, P.aux, D.pre,
-                                  kb[(NP + 7) / 8 - 1]);
+                                  bm + (WR - 64) * wm + 64, bn, wm, wn, wid, lane, P.C, P.aux);
   }
   stamp_end(P.stamps, t_start);
 }

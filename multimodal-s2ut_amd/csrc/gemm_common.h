@@ -329,70 +329,10 @@ constexpr bool epi_drops() {
          EPI == MMS_EPI_GELU_DROP_BWD;
 }
 
-// Dropout keep bits of the staged epilogue, computed inside the k-loop (round 6).  A lane's
-// epilogue elements are fixed by the tile: pass p covers row m0 + 8p, columns n .. n+7 (m0 =
-// the wave's first row + lane / 8, n = the wave's column + 8 (lane % 8)).  When every counter pair
-// of the lane's passes shares its high word (the staged epilogue's fast path), pass p's 8 keep flags
-// are 4 mixes of (pbase + 4 p ld_rng + h) ^ hmix — work with no dependence on the accumulators, so
-// the k-loop issues a share of the passes per k-step beside its MFMAs (a 16x16x32 MFMA leaves the
-// SIMD's vector issue free for half its cycles) instead of the epilogue running them after the
-// last MFMA.  Same hash of the same counters: bit-identical.
-struct EpiDrop {
-  bool pre;           // wave-uniform: the bits are precomputed (else the epilogue hashes itself)
-  uint32_t hmix, pbase;
-};
-template <int EPI>
-MMS_DEV EpiDrop epi_drop_setup(const GemmP& P, int m0, int n, int npass, int nk) {
-  EpiDrop D{false, 0u, 0u};
-#ifdef MMS_EPI_NOPRE   // A/B build: keep bits hashed in the epilogue, as before round 6
-  return D;
-#endif
-  if (epi_drops<EPI>() && P.thresh && nk > 0) {
-    const uint64_t cf = P.offset + (uint64_t)m0 * P.ld_rng + n;
-    const uint64_t cl = P.offset + (uint64_t)(m0 + 8 * (npass - 1)) * P.ld_rng + n + 7;
-    const bool ok = mms_same_hi(cf, cl) && ((cf & 1) == 0) && ((P.ld_rng & 1) == 0);
-    D.hmix = mms_hi_mix(P.seed, cf);
-    D.pbase = (uint32_t)(cf >> 1);
-    D.pre = __all(ok);
-  }
-  return D;
-}
-// the 8 keep flags of pass p, bit e = column n + e
-MMS_DEV uint32_t epi_pass_bits(const GemmP& P, const EpiDrop& D, int p) {
-  const uint32_t p0 = D.pbase + (uint32_t)(4 * p) * (uint32_t)P.ld_rng;
-  uint32_t b = 0;
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    const uint32_t hv = mms_mix32((p0 + h) ^ D.hmix);
-    b |= (uint32_t)((hv & 0xffffU) >= P.thresh) << (2 * h);
-    b |= (uint32_t)((hv >> 16) >= P.thresh) << (2 * h + 1);
-  }
-  return b;
-}
-// k-step kt of nk: the passes [kt NP / nk, (kt + 1) NP / nk) of the lane's NP into bits (pass p at
-// bits 8 (p % 8) of kb[p / 8]).  A run-time loop over the step's pass (or passes, when nk < NP):
-// unrolled over all NP with a predicate the compiler computes every pass and selects.
-template <int NP>
-MMS_DEV void epi_bits_step(const GemmP& P, const EpiDrop& D, int kt, int nk, uint64_t (&kb)[(NP + 7) / 8]) {
-  const int lo = kt * NP / nk, hi = (kt + 1) * NP / nk;
-  for (int p = lo; p < hi; ++p) {
-    const uint64_t b = epi_pass_bits(P, D, p);
-    if (NP <= 8) {
-      kb[0] |= b << (8 * p);
-    } else {
-      const uint64_t lo8 = p < 8 ? b << (8 * (p & 7)) : 0ull, hi8 = p >= 8 ? b << (8 * (p & 7)) : 0ull;
-      kb[0] |= lo8;
-      kb[(NP + 7) / 8 - 1] |= hi8;
-    }
-  }
-}
-
-// FR: 16-row fragments of the wave's tile in this pass (4 = 64 rows; 2 = 32 rows).  pre: keep bits
-// from the k-loop (epi_bits_step; wave-uniform), pass p's 8 flags at bits 8p of pre_bits.
+// FR: 16-row fragments of the wave's tile in this pass (4 = 64 rows; 2 = 32 rows)
 template <int EPI, int FR = 4>
 MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4], int bm, int bn,
-                             int wm, int wn, int wid, int lane, void* Cz, const h16* auxz, bool pre = false,
-                             uint64_t pre_bits = 0) {
+                             int wm, int wn, int wid, int lane, void* Cz, const h16* auxz) {
   constexpr int PASSES = FR * 2;   // 8 rows per pass
   float* stage = reinterpret_cast<float*>(smem) + wid * 64 * 64;
 #pragma unroll
@@ -460,7 +400,7 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][
   // boundary): one mixer per pair of elements instead of two (bit-identical to mms_keep4)
   uint32_t hmix = 0, pbase = 0;
   bool same_hi = false, fast = false;
-  if (DROPS && P.thresh && !pre) {
+  if (DROPS && P.thresh) {
     const uint64_t cf = P.offset + (uint64_t)m0 * P.ld_rng + n;
     const uint64_t cl = P.offset + (uint64_t)(m0 + 8 * (PASSES - 1)) * P.ld_rng + n + 7;
     same_hi = mms_same_hi(cf, cl) && ((cf & 1) == 0) && ((P.ld_rng & 1) == 0);
@@ -479,11 +419,7 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] = x[e] * P.alpha + bv[e];
     bool keep[8] = {true, true, true, true, true, true, true, true};
-    if (DROPS && P.thresh && pre) {
-      const uint32_t b8 = (uint32_t)(pre_bits >> (8 * pass));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) keep[e] = (b8 >> e) & 1u;
-    } else if (DROPS && P.thresh && fast) {
+    if (DROPS && P.thresh && fast) {
       const uint32_t p0 = pbase + (uint32_t)(4 * pass) * (uint32_t)P.ld_rng;
 #pragma unroll
       for (int h = 0; h < 4; ++h) {

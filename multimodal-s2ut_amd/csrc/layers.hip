@@ -623,11 +623,7 @@ extern "C" int mms2ut_conv1d_glu_fwd(const mms2ut_conv1d_glu* c, float* main_ws,
     const mms2ut_half* W = c->w[i];
     if (D.kp[i] != D.ck[i]) {   // the weight, zero-padded to the padded K
       mms2ut_half* Wp = at<mms2ut_half>(A, off, i * CA_N + CA_WP);
-      if (hipMemsetAsync(Wp, 0, (size_t)N * D.kp[i] * 2, s) != hipSuccess) {
-        mms::set_error("conv1d_glu_fwd: hipMemsetAsync failed");
-        return 1;
-      }
-      if ((rc = mms2ut_copy2d(W, D.ck[i], Wp, D.kp[i], N, (int)D.ck[i], s))) return rc;
+      if ((rc = mms2ut_copy2d_pad(W, D.ck[i], Wp, D.kp[i], N, (int)D.ck[i], (int)(D.kp[i] - D.ck[i]), s))) return rc;
       W = Wp;
     }
     if ((rc = linear(cx, col, W, c->b[i], y, D.rows[i], N, D.kp[i]))) return rc;
@@ -792,11 +788,7 @@ mms2ut_gemm_args batched(const mms2ut_half* A, const mms2ut_half* B_, void* C, i
 }
 
 int zero_rows(mms2ut_half* p, int64_t pitch_elems, int64_t width_elems, int64_t rows, hipStream_t s) {
-  if (hipMemset2DAsync(p, (size_t)pitch_elems * 2, 0, (size_t)width_elems * 2, (size_t)rows, s) != hipSuccess) {
-    mms::set_error("gated_fusion: hipMemset2DAsync failed");
-    return 1;
-  }
-  return 0;
+  return mms2ut_copy2d_pad(nullptr, 0, p, pitch_elems, rows, 0, (int)width_elems, s);
 }
 
 }  // namespace
@@ -882,11 +874,10 @@ extern "C" int mms2ut_gated_fusion_fwd(const mms2ut_gated_fusion* f, float* main
       imgn = H_(FA_IMGN);
     }
     if (D.extra) {
-      if (hipMemsetAsync(H_(FA_IMGD), 0, (size_t)D.Rk * Di * 2, s) != hipSuccess) {
-        mms::set_error("gated_fusion_fwd: hipMemsetAsync failed");
-        return 1;
-      }
-      if ((rc = mms2ut_copy2d(imgn, D.Ti * Di, H_(FA_IMGD), D.Tk * Di, D.B, (int)(D.Ti * Di), s))) return rc;
+      // the image rows and the zero bias_kv row of every batch entry in one pass
+      if ((rc = mms2ut_copy2d_pad(imgn, D.Ti * Di, H_(FA_IMGD), D.Tk * Di, D.B, (int)(D.Ti * Di),
+                                  (int)((D.Tk - D.Ti) * Di), s)))
+        return rc;
       imgd = H_(FA_IMGD);
     } else {
       imgd = imgn;

@@ -62,14 +62,18 @@ __global__ void __launch_bounds__(256) ls_xent_fwd_kernel(const h16* __restrict_
   }
 }
 
-// loss_out[0..1] += the nb block partials, in a fixed order (one wave)
+// the nb block partials summed in a fixed order (one wave): acc[0..1] += {loss, nll} and / or
+// call_out[0..1] = {loss, nll} (either may be null)
 __global__ void __launch_bounds__(64) ls_xent_sum_kernel(const float* __restrict__ part, int nb,
-                                                         float* __restrict__ loss_out) {
+                                                         float* __restrict__ acc, float* __restrict__ call_out) {
   float l = 0.f, n = 0.f;
   for (int i = threadIdx.x; i < nb; i += 64) { l += part[i]; n += part[nb + i]; }
   l = wave_sum(l);
   n = wave_sum(n);
-  if (threadIdx.x == 0) { loss_out[0] += l; loss_out[1] += n; }
+  if (threadIdx.x == 0) {
+    if (acc) { acc[0] += l; acc[1] += n; }
+    if (call_out) { call_out[0] = l; call_out[1] = n; }
+  }
 }
 
 template <int CPL>
@@ -320,12 +324,18 @@ int pick_cpl_v(int V, F&& f) {
 
 }  // namespace
 
-extern "C" int mms2ut_ls_xent_fwd(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
-                                  float eps, int pad_idx, float* lse, float* part, float* loss_out,
-                                  hipStream_t s) {
+extern "C" int mms2ut_ls_xent_fwd_log(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
+                                      float eps, int pad_idx, float* lse, float* part, float* acc, float* call_out,
+                                      hipStream_t s) {
   MMS_REQUIRE(ld % 4 == 0 && ld >= V, "ls_xent: ld must be a multiple of 4 and >= V");
-  MMS_REQUIRE(part && loss_out, "ls_xent: null partials / loss");
-  if (rows == 0) return 0;
+  MMS_REQUIRE(part && (acc || call_out), "ls_xent: null partials / loss");
+  if (rows == 0) {
+    if (call_out) {
+      const float z[2] = {0.f, 0.f};
+      return mms2ut_set_f32(call_out, 2, z, s);
+    }
+    return 0;
+  }
   const int nb = (int)std::min<long>((rows + 3) / 4, MMS_LS_XENT_PARTS);
   const int rc = pick_cpl_v(V, [&](auto C) {
     hipLaunchKernelGGL((ls_xent_fwd_kernel<decltype(C)::value>), dim3(nb), dim3(256), 0, s,
@@ -333,8 +343,15 @@ extern "C" int mms2ut_ls_xent_fwd(const h16* logits, int64_t ld, const int64_t* 
     return mms::check_launch("ls_xent_fwd");
   });
   if (rc) return rc;
-  hipLaunchKernelGGL(ls_xent_sum_kernel, dim3(1), dim3(64), 0, s, part, nb, loss_out);
+  hipLaunchKernelGGL(ls_xent_sum_kernel, dim3(1), dim3(64), 0, s, part, nb, acc, call_out);
   return mms::check_launch("ls_xent_sum");
+}
+
+extern "C" int mms2ut_ls_xent_fwd(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
+                                  float eps, int pad_idx, float* lse, float* part, float* loss_out,
+                                  hipStream_t s) {
+  MMS_REQUIRE(loss_out, "ls_xent: null loss");
+  return mms2ut_ls_xent_fwd_log(logits, ld, target, rows, V, eps, pad_idx, lse, part, loss_out, nullptr, s);
 }
 
 extern "C" int mms2ut_ls_xent_bwd(const h16* logits, int64_t ld, const int64_t* target, int64_t rows, int V,
@@ -401,6 +418,20 @@ extern "C" int mms2ut_scale_f16(h16* x, int64_t n, float alpha, hipStream_t s) {
   const long nb = std::min<long>((n8 + 255) / 256, 4096);
   hipLaunchKernelGGL(scale_f16_kernel, dim3(nb), dim3(256), 0, s, x, n8, alpha);
   return mms::check_launch("scale_f16");
+}
+
+struct F32x8 { float v[8]; };
+__global__ void set_f32_kernel(float* __restrict__ dst, int n, F32x8 vals) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = vals.v[threadIdx.x];
+}
+
+extern "C" int mms2ut_set_f32(float* dst, int n, const float* vals, hipStream_t s) {
+  MMS_REQUIRE(dst && vals && n >= 0 && n <= 8, "set_f32: 0 <= n <= 8 values (got %d)", n);
+  if (n == 0) return 0;
+  F32x8 v{};
+  for (int i = 0; i < n; ++i) v.v[i] = vals[i];
+  hipLaunchKernelGGL(set_f32_kernel, dim3(1), dim3(64), 0, s, dst, n, v);
+  return mms::check_launch("set_f32");
 }
 
 extern "C" int mms2ut_accum_f16_f32(float* acc, const h16* x, int64_t n, hipStream_t s) {

@@ -907,13 +907,23 @@ __global__ void gate_bwd_kernel(const h16* __restrict__ dres, const h16* __restr
   }
 }
 
+// dst row r = [src row r (cols) | zcols zeros]; VEC: 8 halves per item (every stride, count and
+// base 8-aligned), else one
+template <int VEC>
 __global__ void copy2d_kernel(const h16* __restrict__ src, long lds, h16* __restrict__ dst, long ldd,
-                              long rows, int cols) {
-  const long n = rows * cols;
+                              long rows, int cols, int zcols) {
+  const int w = (cols + zcols) / VEC, cv = cols / VEC;
+  const long n = rows * w;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / cols;
-    const int c = (int)(i % cols);
-    dst[r * ldd + c] = src[r * lds + c];
+    const long r = i / w;
+    const int c = (int)(i % w);
+    if (VEC == 8) {
+      s16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (c < cv) v = *reinterpret_cast<const s16x8*>(src + r * lds + 8 * c);
+      *reinterpret_cast<s16x8*>(dst + r * ldd + 8 * c) = v;
+    } else {
+      dst[r * ldd + c] = c < cv ? src[r * lds + c] : (h16)0.f;
+    }
   }
 }
 
@@ -1257,13 +1267,26 @@ extern "C" int mms2ut_gate_bwd(const h16* dres, const h16* merge, const h16* g, 
   return mms::check_launch("gate_bwd");
 }
 
+extern "C" int mms2ut_copy2d_pad(const h16* src, int64_t lds, h16* dst, int64_t ldd, int64_t rows, int cols,
+                                 int zcols, hipStream_t s) {
+  MMS_REQUIRE(rows >= 0 && cols >= 0 && zcols >= 0 && (cols == 0 || src) && dst, "copy2d_pad: bad arguments");
+  MMS_REQUIRE(rows <= 1 || ldd >= cols + zcols, "copy2d_pad: dst rows overlap");
+  const long n = (long)rows * (cols + zcols);
+  if (n == 0) return 0;
+  const bool v8 = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && (lds | ldd | cols | zcols) % 8 == 0;
+  if (v8) {
+    hipLaunchKernelGGL((copy2d_kernel<8>), dim3(grid_for(n / 8, 256)), dim3(256), 0, s, src, (long)lds, dst,
+                       (long)ldd, (long)rows, cols, zcols);
+  } else {
+    hipLaunchKernelGGL((copy2d_kernel<1>), dim3(grid_for(n, 256)), dim3(256), 0, s, src, (long)lds, dst,
+                       (long)ldd, (long)rows, cols, zcols);
+  }
+  return mms::check_launch("copy2d");
+}
+
 extern "C" int mms2ut_copy2d(const h16* src, int64_t lds, h16* dst, int64_t ldd, int64_t rows, int cols,
                              hipStream_t s) {
-  const long n = (long)rows * cols;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(copy2d_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, src, (long)lds, dst,
-                     (long)ldd, (long)rows, cols);
-  return mms::check_launch("copy2d");
+  return mms2ut_copy2d_pad(src, lds, dst, ldd, rows, cols, 0, s);
 }
 
 namespace mms {

@@ -788,9 +788,10 @@ def wgrad_group(problems, rows, max_blocks=0):
     call("mms2ut_wgrad_group", arr, len(problems), int(rows), int(max_blocks), _s())
 
 
-def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
+def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, out_f32=None, side=True):
     """dW[N,K] (fp16 view into the flat grad buffer) = dy[M,N]^T @ x[M,K].
-    With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead.
+    With accumulate_f32 (an fp32 [N,K] buffer) the result is added there instead; with out_f32 it
+    is written there in fp32.
     With db (fp16 [N]) the bias gradient sum_rows dy comes out of the same GEMM: its first column
     of tiles sums the dy rows it stages anyway.  A product with >= 256 output tiles (one per CU)
     runs unsplit through the grouped kernel (no fp32 slabs); smaller ones split K over the rows
@@ -798,6 +799,9 @@ def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
     M, N = dy.shape
     K = x.shape[1]
     assert dW is None or tuple(dW.shape) == (N, K)
+    if out_f32 is not None:
+        assert accumulate_f32 is None and db is None and tuple(out_f32.shape) == (N, K)
+        accumulate_f32 = out_f32     # the split-K slab path below, its reduction storing (mode 0)
     if accumulate_f32 is None and -(-N // 128) * -(-K // 128) >= 256 and _group_ok(dy, x, dW):
         ctx = side_begin(dy, x) if side else None
         with (ctx or _NULLCTX):
@@ -822,7 +826,7 @@ def linear_wgrad(dy, x, dW, *, db=None, accumulate_f32=None, side=True):
             call("mms2ut_splitk_reduce", rs.data_ptr(), s, N, 1, N, db.data_ptr(), N, 1, 1.0, _s())
         if accumulate_f32 is not None:
             call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, accumulate_f32.data_ptr(),
-                 accumulate_f32.stride(0), 2, 1.0, _s())
+                 accumulate_f32.stride(0), 0 if out_f32 is not None else 2, 1.0, _s())
             return accumulate_f32
         call("mms2ut_splitk_reduce", slabs.data_ptr(), s, N * K, N, K, dW.data_ptr(), dW.stride(0), 1,
              1.0, _s())
@@ -1064,13 +1068,21 @@ def copy2d(src, dst, rows, cols):
 LS_XENT_PARTS = 512   # include/mms2ut.h MMS_LS_XENT_PARTS
 
 
-def ls_xent_fwd(logits, ld, target, rows, V, eps, pad, loss_out):
-    """loss_out[0:2] += {label-smoothed loss, nll} (fixed-order sum); returns lse [rows]."""
+def ls_xent_fwd(logits, ld, target, rows, V, eps, pad, loss_out, call_out=None):
+    """loss_out[0:2] += {label-smoothed loss, nll} (fixed-order sum; loss_out may be None) and, with
+    call_out, call_out[0:2] = this call's {loss, nll}; returns lse [rows]."""
     lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
     part = _workspace("ls_xent_part", 2 * LS_XENT_PARTS, logits.device)
-    call("mms2ut_ls_xent_fwd", logits.data_ptr(), ld, target.data_ptr(), rows, V, float(eps), pad,
-         lse.data_ptr(), part.data_ptr(), loss_out.data_ptr(), _s())
+    call("mms2ut_ls_xent_fwd_log", logits.data_ptr(), ld, target.data_ptr(), rows, V, float(eps), pad,
+         lse.data_ptr(), part.data_ptr(), _p(loss_out), _p(call_out), _s())
     return lse
+
+
+def set_f32(dst, vals):
+    """dst[:len(vals)] = vals (fp32 device vector, <= 8 values) in one launch."""
+    import ctypes
+    arr = (ctypes.c_float * len(vals))(*[float(v) for v in vals])
+    call("mms2ut_set_f32", dst.data_ptr(), len(vals), ctypes.addressof(arr), _s())
 
 
 def ls_xent_bwd(logits, ld, target, rows, V, eps, pad, lse, grad, out):

@@ -1761,11 +1761,11 @@ class MMS2UTModel:
         B, Tt = ctx["B"], ctx["Tt"]
         dinner = dinner or {}
         E = self.P(f"{spec.prefix}.embed_tokens.weight")
-        dE32 = torch.zeros(V, d, dtype=torch.float32, device=E.device)
-        # tied output projection: dE += dlogits^T xl ; dxl = dlogits E.  Both halves of the tied
+        dE32 = torch.empty(V, d, dtype=torch.float32, device=E.device)
+        # tied output projection: dE = dlogits^T xl ; dxl = dlogits E.  Both halves of the tied
         # embedding gradient (this wgrad and the token scatter below) run on the side stream, in
-        # order, accumulating into dE32 (zeroed here on the main stream before the fork).
-        K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, accumulate_f32=dE32)
+        # order: the wgrad writes dE32 (no zero fill), the scatter adds to it.
+        K.linear_wgrad(dlogits[:, :V], ctx["xl"], None, out_f32=dE32)
         dxl = torch.empty(B * Tt, d, dtype=F16, device=E.device)
         # dxl = dlogits E over K = Vp: E zero-padded to Vp rows (refreshed per step), so the GEMM
         # runs on the LDS-DMA path (K % 64 == 0) instead of the predicated one

@@ -156,14 +156,14 @@ class _ModelFn(torch.autograd.Function):
         fctx.model = model
         fctx.saved = (ectx, dctx, enc, batch, actx, Te)
         fctx.bridged = anchor is not model.anchor   # a caller-provided anchor must get a gradient
-        if aux is None:
-            aux = torch.zeros(1, dtype=torch.float32, device=logits.device)
-        if not states:
-            return logits, aux.reshape(())
+        if aux is not None:
+            aux = aux.reshape(())
+        if not states:     # aux: None without multitask heads (no zero tensor per step)
+            return logits, aux
         fctx.set_materialize_grads(False)
         es, ins = model.encoder_states(ectx), model.inner_states(dctx)
         fctx.n_enc = len(es)
-        return (logits, aux.reshape(()), *es, *ins)
+        return (logits, aux, *es, *ins)
 
     @staticmethod
     def backward(fctx, dlogits, daux, *dhidden):
@@ -211,8 +211,8 @@ BWD_CPU_S = [0.0]
 
 
 def model_outputs(model, batch, states=False):
-    """(padded logits [B*Tt, round64(V)] fp16, weighted multitask loss fp32 0-dim) — both
-    autograd-connected through the hand-written backward.  states=True appends the encoder_states
+    """(padded logits [B*Tt, round64(V)] fp16, weighted multitask loss fp32 0-dim, or None when the
+    model has no multitask heads) — autograd-connected through the hand-written backward.  states=True appends the encoder_states
     and decoder inner_states outputs (see _ModelFn)."""
     return _ModelFn.apply(model.anchor, model, batch, states)
 
@@ -224,14 +224,15 @@ def model_logits(model, batch):
 
 class _LSXentFn(torch.autograd.Function):
     @staticmethod
-    def forward(fctx, logits, target, V, eps, pad):
+    def forward(fctx, logits, target, V, eps, pad, acc):
         rows, ld = logits.shape
-        out = torch.zeros(2, dtype=torch.float32, device=logits.device)
-        lse = K.ls_xent_fwd(logits, ld, target, rows, V, eps, pad, out)
+        # the kernel writes this call's {loss, nll} (and adds them to acc, the caller's log, if
+        # given): no zeroed accumulator, no copies
+        out = torch.empty(2, dtype=torch.float32, device=logits.device)
+        lse = K.ls_xent_fwd(logits, ld, target, rows, V, eps, pad, acc, call_out=out)
         fctx.saved = (logits, target, lse, V, eps, pad)
-        fctx.mark_non_differentiable(out)
-        loss = out[0].clone()
-        nll = out[1].clone()
+        fctx.set_materialize_grads(False)   # no zero-filled gradient for the nll output
+        loss, nll = out[0], out[1]
         fctx.mark_non_differentiable(nll)
         return loss, nll
 
@@ -243,9 +244,10 @@ class _LSXentFn(torch.autograd.Function):
         g = gloss.reshape(1).to(torch.float32).contiguous()
         # in place: the logits are dead after this point
         K.ls_xent_bwd(logits, ld, target, rows, V, eps, pad, lse, g, logits)
-        return logits, None, None, None, None
+        return logits, None, None, None, None, None
 
 
-def label_smoothed_ce(logits, target, V, eps, pad):
-    """fairseq label_smoothed_nll_loss(lprobs=log_softmax(logits.float()), reduce=sum)."""
-    return _LSXentFn.apply(logits, target.reshape(-1), V, eps, pad)
+def label_smoothed_ce(logits, target, V, eps, pad, acc=None):
+    """fairseq label_smoothed_nll_loss(lprobs=log_softmax(logits.float()), reduce=sum).
+    acc: an optional fp32 device [2] (e.g. a trainer's step log) that {loss, nll} are added to."""
+    return _LSXentFn.apply(logits, target.reshape(-1), V, eps, pad, acc)

@@ -196,8 +196,11 @@ class Trainer:
             m.drop.reset(self.seed_base)
         if n > 1 and self.acc is None:
             self.acc = torch.zeros(m.params.numel, dtype=torch.float32, device=m.params.flat.device)
-        self.log.zero_()
         ntok = sum(int(b.ntokens) for b in batches)
+        # the step log in one launch: loss / nll accumulate into it (the LS-CE kernel adds each
+        # micro-batch's sums), ntokens / nsentences / sample size per world are known up front
+        K.set_f32(self.log, [0.0, 0.0, float(ntok), float(sum(int(b.nsentences) for b in batches)),
+                             float(ntok) / self.world])
         for i, batch in enumerate(batches):
             last = i == n - 1
             if self.reducer is not None and last:
@@ -214,11 +217,12 @@ class Trainer:
             if m.params.zero_each_step:
                 m.params.grad.zero_()
             loss, nll = runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"],
-                                                  cfg["label_smoothing"], cfg["padding_idx"])
+                                                  cfg["label_smoothing"], cfg["padding_idx"],
+                                                  acc=self.log[LOG_LOSS:LOG_NLL + 1])
             del logits
             # multitask heads: loss + sum_t weight_t * loss_t (fairseq MultitaskCriterion); the
             # logged loss stays the main one (fairseq logs multitask losses separately)
-            (loss + aux if m.cfg.get("multitask") else loss).backward(self.opt.loss_scale())
+            (loss + aux if aux is not None else loss).backward(self.opt.loss_scale())
             m.grad_ready_hook = None
             if n > 1:
                 if i == 0:
@@ -227,16 +231,10 @@ class Trainer:
                     K.accum_f16_f32(self.acc, m.params.grad)
                 elif self.reducer is None:
                     K.add_f32_to_f16(m.params.grad, self.acc, m.params.grad)
-            self.log[LOG_LOSS] += loss.detach()
-            self.log[LOG_NLL] += nll.detach()
         if self.reducer is not None:
             self.reducer.finish()
             self.reducer.acc = None
-        # logging / sample-size sync: fixed scalars summed over ranks (fill_ takes the scalar as a
-        # kernel argument; item assignment would be a blocking H2D copy)
-        self.log[LOG_NTOKENS].fill_(float(ntok))
-        self.log[LOG_NSENT].fill_(float(sum(int(b.nsentences) for b in batches)))
-        self.log[LOG_SS_OVER_WORLD].fill_(float(ntok) / self.world)
+        # logging / sample-size sync: the log (set at the step start) summed over ranks
         all_reduce_scalars(self.log)
         if self.grad_tap is not None:
             # the final (reduced, accumulated) fp16 gradient, in stream order before the optimizer

@@ -53,7 +53,7 @@ def _step_grads(mm, model, batch, cfg, modality, poison):
         model.params.grad.zero_()
     logits, aux = mm.runtime.model_outputs(model, batch)
     loss, _ = mm.runtime.label_smoothed_ce(logits, batch.target, cfg["vocab_size"], cfg["label_smoothing"], 1)
-    (loss + aux if cfg.get("multitask") else loss).backward(torch.tensor(16.0, device="cuda"))
+    (loss + aux if aux is not None else loss).backward(torch.tensor(16.0, device="cuda"))
     torch.cuda.synchronize()
     return model.params.grad.clone()
 

@@ -129,6 +129,22 @@ def test_gemm_dropout_masks_every_tile(K, M, N, Kd):
         K.call("mms2ut_gemm_set_tall", 1)
 
 
+@pytest.mark.parametrize("rows,lds,ldd,cols,zcols", [(577, 768, 1536, 768, 768), (33, 85, 96, 85, 11),
+                                                       (8, 443136, 443904, 443136, 768), (5, 0, 40, 0, 24)])
+def test_copy2d_pad(K, rows, lds, ldd, cols, zcols):
+    """mms2ut_copy2d_pad: rows copied and the pad columns zeroed in one launch (vector and scalar
+    forms; src NULL = strided zero fill), nothing else in dst touched."""
+    src = torch.randn(max(rows * lds, 1), device="cuda").half()
+    dst = torch.full((rows * ldd + 16,), 7.0, device="cuda").half()
+    ref = dst.clone()
+    K.call("mms2ut_copy2d_pad", src.data_ptr() if cols else 0, lds, dst.data_ptr(), ldd, rows, cols, zcols, K._s())
+    for r in range(rows):
+        ref[r * ldd:r * ldd + cols] = src[r * lds:r * lds + cols]
+        ref[r * ldd + cols:r * ldd + cols + zcols] = 0
+    torch.cuda.synchronize()
+    assert torch.equal(dst, ref)
+
+
 def test_wgrad_splitk(K):
     M, N, K_ = 5000, 96, 200
     dy = torch.randn(M, N, device="cuda").half()
