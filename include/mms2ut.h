@@ -585,6 +585,12 @@ int mms2ut_layer_ws(const mms2ut_layer* layer, int64_t* main_floats, int64_t* si
 int mms2ut_layer_fwd(const mms2ut_layer* layer, float* main_ws, int64_t main_ws_floats, hipStream_t stream);
 int mms2ut_layer_bwd(const mms2ut_layer* layer, const mms2ut_layer_grad* grad, hipStream_t main,
                      hipStream_t side);
+/* Launches the grouped weight gradients a layer backward held back (mms2ut_layer_bwd launches a
+ * layer's group from inside the next layer's backward, behind its self-attention backward; env
+ * MMS2UT_WGRAD_DEFER selects the point, 0 = no deferral), on the side stream behind `main`'s work
+ * so far.  No-op when nothing is pending.  Call before joining the side stream or reporting a
+ * gradient ready point (the host package does both).                                         */
+int mms2ut_wgrad_flush(hipStream_t main);
 
 /* ---------------------------------------------------------------- Conv1d subsampler
  * fairseq Conv1dSubsampler — SURVEY §8b mms2ut_conv1d_glu_{fwd,bwd} (A3; S2TTransformerEncoder's

@@ -218,6 +218,41 @@ int wgrad_split_mode() {
   return m;
 }
 
+// A layer's grouped weight gradients are held back and launched from inside the NEXT layer's
+// backward, at flush point MMS2UT_WGRAD_DEFER (default 5: behind that layer's self-attention
+// backward; 0 = at the end of their own layer, as before round 6).  Launched at the end of their
+// own layer, the ~430-tile group took the CUs ahead of the next layer's FFN dgrads (the fc1 dgrad ran
+// 4-5x its serial time beside it); behind the attention backward it shares the CUs with the
+// QKV dgrad and the LayerNorm / attention kernels of the layers below instead.  Same-box A/Bs
+// (profiles/round6_wgrad_defer_ab.txt): 16.20-16.31 -> 15.90-15.98 ms (point 5), 16.03-16.09 (1),
+// 16.34-16.44 (3), 16.40-16.42 (4); points 2 and 6 lose (17.1).  Host thread-local (the backward
+// issues from one thread); flushed by mms2ut_wgrad_flush before the side stream is joined or a
+// gradient ready point is reported (data-parallel hooks), so a bucket never misses a gradient.
+struct PendingGroup {
+  bool on = false;
+  mms2ut_wgrad w[8];
+  int n = 0;
+  int64_t rows = 0;
+  int blocks = 0;
+  hipStream_t side = nullptr;
+};
+thread_local PendingGroup g_pend;
+int wgrad_defer_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("MMS2UT_WGRAD_DEFER");
+    m = e ? atoi(e) : 5;
+  }
+  return m;
+}
+int flush_pending(hipStream_t main) {
+  if (!g_pend.on) return 0;
+  g_pend.on = false;
+  int rc = g_pend.side == main ? 0 : mms2ut_stream_wait(g_pend.side, main);
+  if (rc) return rc;
+  return mms2ut_wgrad_group(g_pend.w, g_pend.n, g_pend.rows, g_pend.blocks, g_pend.side);
+}
+
 // dW[N, K] = dy[M, N]^T @ x[M, K] and db[N] = colsum(dy), on the side stream (kernels.linear_wgrad):
 // fp32 split-K slabs with the bias partials as A-row sums, one reduction launch
 int wgrad(const Ctx& c, const mms2ut_half* dy, int64_t lddy, const mms2ut_half* x, int64_t ldx, mms2ut_half* dW,
@@ -426,8 +461,14 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
   }
   if ((rc = dgrad(c, dyd, d, L->w_fc2, L->wt_fc2, SH(S_DF1), R, d, F, MMS_EPI_RELU_DROP_BWD, H_(MMS_SLOT_F1),
                   L->p_act))) return rc;
+  // the layer above's deferred weight gradients, launched at flush point MMS2UT_WGRAD_DEFER of this
+  // layer (1: after this first dgrad, 2: after fc1's dgrad, 3: after LN3, 4: after the next
+  // out-projection dgrad, 5: after the self-attention backward, 6: after the QKV dgrad)
+  const int fp = wgrad_defer_mode();
+  auto flush_at = [&](int point) { return point == fp ? flush_pending(main) : 0; };
+  if ((rc = flush_at(1))) return rc;
   if ((rc = wgrad(c, dyd, d, H_(MMS_SLOT_F1), F, L->g_w_fc2, L->g_b_fc2, R, d, F))) return rc;
-  if ((rc = dgrad(c, SH(S_DF1), F, L->w_fc1, L->wt_fc1, SH(S_DH3), R, F, d))) return rc;
+  if ((rc = dgrad(c, SH(S_DF1), F, L->w_fc1, L->wt_fc1, SH(S_DH3), R, F, d)) || (rc = flush_at(2))) return rc;
   if ((rc = wgrad(c, SH(S_DF1), F, H_(MMS_SLOT_H3), d, L->g_w_fc1, L->g_b_fc1, R, F, d))) return rc;
   if (c.grouped && wgrad_split_mode()) {
     // A/B (MMS2UT_WGRAD_SPLIT=1): the FFN weight gradients as their own grouped launch right here,
@@ -441,7 +482,7 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
   mms2ut_half* dxf = D.dec ? SH(S_DX3) : SH(S_DX2);
   const uint64_t below_off = D.dec ? L->off_ca_res : L->off_sa_res;
   if ((rc = ln_bwd(c, SH(S_DH3), xf, L->ln3_g, F_(MMS_SLOT_M3), F_(MMS_SLOT_R3), G->dy, dxf, SH(S_DY3B), pd, L->seed,
-                   below_off, SF(S_P3), L->g_ln3, R, Dm))) return rc;
+                   below_off, SF(S_P3), L->g_ln3, R, Dm)) || (rc = flush_at(3))) return rc;
   const mms2ut_half* dbr = pd > 0.f ? SH(S_DY3B) : dxf;   // the block below's residual-branch gradient
   mms2ut_half* dxa = SH(S_DX2);                            // gradient of the self-attention block output
   if (D.dec) {
@@ -459,7 +500,7 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
     dbr = pd > 0.f ? SH(S_DY2B) : dxa;
   }
   // ---- self-attention block
-  if ((rc = dgrad(c, dbr, d, L->w_o, L->wt_o, SH(S_DO), R, d, d))) return rc;
+  if ((rc = dgrad(c, dbr, d, L->w_o, L->wt_o, SH(S_DO), R, d, d)) || (rc = flush_at(4))) return rc;
   if ((rc = wgrad(c, dbr, d, H_(MMS_SLOT_O), d, L->g_w_o, L->g_b_o, R, d, d))) return rc;
   {
     mms2ut_half* qkv = H_(MMS_SLOT_QKV);
@@ -467,19 +508,31 @@ extern "C" int mms2ut_layer_bwd(const mms2ut_layer* L, const mms2ut_layer_grad* 
     mms2ut_attn_args a = attn(qkv, 3 * d, qkv + d, qkv + 2 * d, 3 * d, H_(MMS_SLOT_O), d, L->B, L->H, L->T, L->T, hd,
                               L->self_len, D.dec ? 1 : 0, L->p_attn, L->seed, L->off_sa_attn, F_(MMS_SLOT_LSE_SA));
     if ((rc = mms2ut_mha_varlen_bwd(&a, SH(S_DO), d, 0, SF(S_DD_SA), dqkv, 3 * d, 0, dqkv + d, 3 * d, 0, dqkv + 2 * d,
-                                    3 * d, 0, main))) return rc;
-    if ((rc = dgrad(c, dqkv, 3 * d, L->w_qkv, L->wt_qkv, SH(S_DH1), R, 3 * d, d))) return rc;
+                                    3 * d, 0, main)) || (rc = flush_at(5))) return rc;
+    if ((rc = dgrad(c, dqkv, 3 * d, L->w_qkv, L->wt_qkv, SH(S_DH1), R, 3 * d, d)) || (rc = flush_at(6))) return rc;
     if ((rc = wgrad(c, dqkv, 3 * d, H_(MMS_SLOT_H1), d, L->g_w_qkv, L->g_b_qkv, R, 3 * d, d))) return rc;
   }
   // LN1 backward: the layer input's gradient (+ dropout for the layer below when asked)
   if ((rc = ln_bwd(c, SH(S_DH1), L->x, L->ln1_g, F_(MMS_SLOT_M1), F_(MMS_SLOT_R1), dxa, SH(S_DX), SH(S_DXD), G->emit_p,
                    G->emit_seed, G->emit_offset, SF(S_P1), L->g_ln1, R, Dm))) return rc;
+  if ((rc = flush_pending(main))) return rc;   // a flush point past this layer's last one
   if (!c.grouped || ngroup == 0) return 0;
+  if (wgrad_defer_mode() && side != main) {
+    g_pend.on = true;
+    std::copy(group, group + ngroup, g_pend.w);
+    g_pend.n = ngroup;
+    g_pend.rows = R;
+    g_pend.blocks = G->side_blocks;
+    g_pend.side = side;
+    return 0;
+  }
   // the layer's weight gradients: one grouped launch on the side stream, behind everything the
   // main stream enqueued for this layer (it overlaps the next layer's dgrad chain)
   if ((rc = fork(c))) return rc;
   return mms2ut_wgrad_group(group, ngroup, R, side == main ? 0 : G->side_blocks, side);
 }
+
+extern "C" int mms2ut_wgrad_flush(hipStream_t main) { return flush_pending(main); }
 
 // ---------------------------------------------------------------- Conv1d subsampler (one call)
 // fairseq Conv1dSubsampler (S2TTransformerEncoder's front, reached at mm_s2s_transformer.py:464):

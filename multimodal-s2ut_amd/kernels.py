@@ -726,10 +726,17 @@ def side_begin(*tensors):
     return _SIDE_REGION
 
 
+def wgrad_flush():
+    """Launch a layer backward's deferred weight-gradient group now (mms2ut_wgrad_flush)."""
+    call("mms2ut_wgrad_flush", torch._C._cuda_getCurrentRawStream(_dev()))
+
+
 def side_join():
     """Join: the current stream waits for all side-stream work (before consuming gradients)."""
     if _Side.used and _Side.stream is not None:
-        call("mms2ut_stream_wait", torch._C._cuda_getCurrentRawStream(_dev()), _Side.ptr)
+        cur = torch._C._cuda_getCurrentRawStream(_dev())
+        call("mms2ut_wgrad_flush", cur)   # a layer's deferred weight-gradient group, if any
+        call("mms2ut_stream_wait", cur, _Side.ptr)
         _Side.used = False
         _Side.keep.clear()
 

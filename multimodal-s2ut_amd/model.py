@@ -641,6 +641,7 @@ class MMS2UTModel:
     def _ready(self, last_param=None):
         if self.grad_ready_hook is None:
             return
+        K.wgrad_flush()   # a deferred weight-gradient group belongs to the gradients reported ready
         if last_param is None:
             self.grad_ready_hook(self.params.numel)
         else:

@@ -3,7 +3,7 @@ both ranks sharing cuda:0) — launched by tests/test_gpu_dp_fairseq.py as a fre
 (test infrastructure).
 
     RANK=r WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=p MMS2UT_DIST_BACKEND=gloo \
-        python tests/dp_fairseq_child.py OUT_DIR TMP_DIR
+        python tests/dp_fairseq_child.py OUT_DIR TMP_DIR [base]
 
 fairseq-train's distributed path restated (tests/fairseq_stub.py stands in for fairseq, which is
 not importable): setup_task -> load_dataset -> build_model -> .half() -> torch DDP with fairseq's
@@ -36,6 +36,10 @@ mm = importlib.import_module("multimodal-s2ut_amd")
 NODROP = "--dropout 0 --attention-dropout 0 --relu-dropout 0"
 BUCKETS_MB = (25, 1)
 RUNS = ((25, False), (1, False), (25, True))   # (bucket MB, find_unused_parameters)
+# "base" mode: the base 12 + 6 model (d 768, FFN 3072, 8 heads: 301 MB of fp16 gradients, twelve
+# 25 MB buckets), fairseq's default bucket size only
+BASE = ("--encoder-layers 12 --decoder-layers 6 --encoder-embed-dim 768 --encoder-ffn-embed-dim 3072 "
+        "--encoder-attention-heads 8 --decoder-embed-dim 768 --decoder-ffn-embed-dim 3072 --decoder-attention-heads 8")
 
 
 class _SetItem:
@@ -69,9 +73,9 @@ def fusion_yaml():
     return FUSION_NODROP
 
 
-def setup(tmp):
+def setup(tmp, extra=NODROP):
     os.makedirs(tmp, exist_ok=True)
-    fs, regs, args, c, _ = fairseq_stub.dropin_setup(_SetItem(), Path(tmp), fusion_yaml(), extra=NODROP)
+    fs, regs, args, c, _ = fairseq_stub.dropin_setup(_SetItem(), Path(tmp), fusion_yaml(), extra=extra)
     task = fs.tasks.setup_task(args)
     task.load_dataset("train")
     model = task.build_model(args).half()
@@ -80,9 +84,9 @@ def setup(tmp):
     return fs, model, crit, batches
 
 
-def run(rank, world, bucket_mb, tmp, out_dir, find_unused=False):
+def run(rank, world, bucket_mb, tmp, out_dir, find_unused=False, extra=NODROP):
     tag = f"b{bucket_mb}" + ("u" if find_unused else "")
-    fs, model, crit, batches = setup(os.path.join(tmp, f"r{rank}_{tag}"))
+    fs, model, crit, batches = setup(os.path.join(tmp, f"r{rank}_{tag}"), extra)
     net = model.impl.net
     ddp = torch.nn.parallel.DistributedDataParallel(model, bucket_cap_mb=bucket_mb, broadcast_buffers=False,
                                                     find_unused_parameters=find_unused)
@@ -116,14 +120,15 @@ def run(rank, world, bucket_mb, tmp, out_dir, find_unused=False):
              launches1=per_iter[1])
 
 
-def main(out_dir, tmp):
+def main(out_dir, tmp, mode="tiny"):
     rank, world, local = mm.parallel.init_from_env()
     torch.cuda.set_device(local)
-    for mb, unused in RUNS:
-        run(rank, world, mb, tmp, out_dir, unused)
+    runs, extra = (((25, False),), NODROP + " " + BASE) if mode == "base" else (RUNS, NODROP)
+    for mb, unused in runs:
+        run(rank, world, mb, tmp, out_dir, unused, extra)
         dist.barrier()
     dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])

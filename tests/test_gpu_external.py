@@ -139,9 +139,12 @@ def test_model_parity_qformer_dropout_replay(mm, saf, modality):
     # audio branch dropped: the decoder attends to the gate mix of a zero text stream and the fused
     # image features, so its cross-attention logits are nearly flat and the gradients through the
     # score matrix (q_proj / k_proj and the LayerNorm in front of q) carry fewer significant fp16
-    # bits: 2e-2 there (k_proj measured 0.8-1.1e-2 across reduction orders)
+    # bits.  Measured on every short-M GEMM route (profiles/round6_qformer_tolerance.txt): split-K
+    # fixup (the pre-round-5 route, MMS2UT_GEMM_SKINNY=0) 1.06-1.27e-2, short-M kernel (1 / 2)
+    # 1.10-1.33e-2 on this set, <= 1e-2 everywhere else — the drift is the flat logits', not a route's.
+    # Bound: the measured worst 1.33e-2 + 13 % = 1.5e-2.
     loose = ("encoder_attn.q_proj", "encoder_attn.k_proj", "encoder_attn_layer_norm") if modality == "audio" else ()
-    bad = {k: e for k, e in grad_errors(r).items() if e > (2e-2 if any(s in k for s in loose) else 1e-2)}
+    bad = {k: e for k, e in grad_errors(r).items() if e > (1.5e-2 if any(s in k for s in loose) else 1e-2)}
     assert not bad, report(r)
     if modality == "image":
         assert all(float(r.grads[k].abs().max()) == 0 for k in r.grads if "q_former" in k)
