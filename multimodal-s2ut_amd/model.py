@@ -1690,6 +1690,9 @@ class MMS2UTModel:
                 dx = K.add_f16(dx, dstates[l - 1])
                 dmask = None
             self._ready(f"encoder.transformer_layers.{l}.self_attn_layer_norm.bias")
+        # the last layer's deferred weight-gradient group (layers.hip g_pend) beside the subsampler's
+        # backward rather than after it (profiles/round6_wgrad_defer_ab.txt)
+        K.wgrad_flush()
         scale, pd = ctx["emb"]
         dh = K.scale_dropout_bwd(dx, scale, pd, ctx["drop_emb"])
         self.subsample_bwd(ctx["sub"], dh)
@@ -1799,6 +1802,7 @@ class MMS2UTModel:
                 dx = K.add_f16(dx, dinner[l])
                 dmask = None      # the layer below recomputes its masked gradient from dx
             self._ready(f"{spec.prefix}.layers.{l}.self_attn_layer_norm.bias")
+        K.wgrad_flush()   # the decoder's last deferred group beside the cross-attention K/V products
         # cross-attention K/V projections of all layers: one wgrad (+ bias) and one dgrad (K = L_d*2d)
         Wkv, _ = self.cross_kv(spec=spec)
         gWkv, gbkv = self.cross_kv(grad=True, spec=spec)
