@@ -224,9 +224,59 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
   const uint32_t prow = (uint32_t)(row_ctr >> 1);
   const uint32_t hi_mix = mms_hi_mix(P.seed, zctr);
   Pair64<HD, 64 * NW> pf;
-  // softmax + PV of one 64-key tile whose scores s (S^T, unscaled) are computed: masking, running
-  // max / sum, dropout, O rescale and the two 32-key PV steps
-  auto tile_pv = [&](int kb, const h16* tV, f32x4 (&s)[4]) {
+  if constexpr (SHORT) {
+    constexpr int CH = HD / 8, NLS = (KROWS * CH + 64 * NW - 1) / (64 * NW);
+    const auto rK = rsrc_rows(K, kmax, P.ldk);
+    const auto rV = rsrc_rows(V, kmax, P.ldv);
+    s16x8 rk[NLS], rv[NLS];
+#pragma unroll
+    for (int n = 0; n < NLS; ++n) {
+      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
+      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) {
+        rk[n] = ld16b(rK, (r * (int)P.ldk + c * 8) * 2);  // rows >= kmax read as zero
+        rv[n] = ld16b(rV, (r * (int)P.ldv + c * 8) * 2);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NLS; ++n) {
+      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
+      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) {
+        *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
+        *reinterpret_cast<s16x8*>(sV + r * LD + c * 8) = rv[n];
+      }
+    }
+    __syncthreads();
+  } else {
+    if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
+  }
+  PH_STAMP(1);
+  for (int kb = 0; kb < kmax; kb += KB) {
+    PH_STAMP(2 + 2 * (kb / KB));
+    const h16* tK = SHORT ? sK + kb * LD : sK;
+    const h16* tV = SHORT ? sV + kb * LD : sV;
+    if constexpr (!SHORT) {
+      __syncthreads();
+      pf.store(sK, sV);
+      // every load issued so far has landed (the stores above waited for the tile's): re-define the
+      // Q fragments here, or the compiler -- unable to prove across the loop that their loads are
+      // done -- puts vmcnt(0) in front of the first QK^T MFMA, draining the next tile's prefetch
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
+      __syncthreads();
+      if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
+    }
+    PH_STAMP(3 + 2 * (kb / KB));
+    // a wave past the last query row, or whose rows all precede this key tile (causal), only
+    // helps stage K/V
+    if (w_row0 >= P.Tq || (P.causal && kb > w_row0 + 15)) continue;
+    // S^T for 4 tiles of 16 keys: lane -> S[q_own][kb + 16t + 4g + r]
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) s[t] = mfma(frag_rows<HD>(tK, 16 * t, kk * 32, lane), qf[kk], s[t]);
+    }
     // scores stay unscaled: the max commutes with the positive scale, and exp(scale*(s - m)) is one
     // FMA + v_exp_f32 in base 2.  A key tile that is valid for every row of the wave (inside the
     // key length and, causal, entirely at or before the wave's first row) skips the masking.
@@ -285,85 +335,9 @@ __global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4)
     // O^T[d][q] += V^T[d][keys] P^T[keys][q], two 32-key steps
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const h16x8 pfr = pack8(s[2 * c], s[2 * c + 1]);
+      const h16x8 pf = pack8(s[2 * c], s[2 * c + 1]);
 #pragma unroll
-      for (int i = 0; i < NDT; ++i) o[i] = mfma(frag_tr<HD>(tV, 32 * c, 16 * i, lane), pfr, o[i]);
-    }
-  };
-  // S^T for 4 tiles of 16 keys: lane -> S[q_own][kb + 16t + 4g + r]
-  auto tile_s = [&](const h16* tK, f32x4 (&s)[4]) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) s[t] = mfma(frag_rows<HD>(tK, 16 * t, kk * 32, lane), qf[kk], s[t]);
-    }
-  };
-  if constexpr (SHORT) {
-    // all of K is issued, then all of V: K lands first (in-order returns), is staged, and both key
-    // tiles' scores are computed while V is still in flight; V is staged behind them.  Same
-    // arithmetic in the same order as the tile loop below: bit-identical
-    constexpr int CH = HD / 8, NLS = (KROWS * CH + 64 * NW - 1) / (64 * NW);
-    const auto rK = rsrc_rows(K, kmax, P.ldk);
-    const auto rV = rsrc_rows(V, kmax, P.ldv);
-    s16x8 rk[NLS], rv[NLS];
-#pragma unroll
-    for (int n = 0; n < NLS; ++n) {
-      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
-      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) rk[n] = ld16b(rK, (r * (int)P.ldk + c * 8) * 2);  // rows >= kmax read as zero
-    }
-#pragma unroll
-    for (int n = 0; n < NLS; ++n) {
-      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
-      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) rv[n] = ld16b(rV, (r * (int)P.ldv + c * 8) * 2);
-    }
-#pragma unroll
-    for (int n = 0; n < NLS; ++n) {
-      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
-      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) *reinterpret_cast<s16x8*>(sK + r * LD + c * 8) = rk[n];
-    }
-    __syncthreads();
-    PH_STAMP(1);
-    f32x4 s2[2][4];
-    bool act[2];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int kb = tt * KB;
-      // a wave past the last query row, or whose rows all precede this key tile (causal), only
-      // helps stage K/V
-      act[tt] = kb < kmax && w_row0 < P.Tq && !(P.causal && kb > w_row0 + 15);
-      if (act[tt]) tile_s(sK + kb * LD, s2[tt]);
-    }
-#pragma unroll
-    for (int n = 0; n < NLS; ++n) {
-      const int i = threadIdx.x + n * 64 * NW, r = i / CH, c = i % CH;
-      if ((KROWS * CH) % (64 * NW) == 0 || i < KROWS * CH) *reinterpret_cast<s16x8*>(sV + r * LD + c * 8) = rv[n];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
-      if (act[tt]) tile_pv(tt * KB, sV + tt * KB * LD, s2[tt]);
-  } else {
-    if (kmax > 0) pf.load(K, P.ldk, V, P.ldv, 0, kmax);
-    PH_STAMP(1);
-    for (int kb = 0; kb < kmax; kb += KB) {
-      PH_STAMP(2 + 2 * (kb / KB));
-      __syncthreads();
-      pf.store(sK, sV);
-      // every load issued so far has landed (the stores above waited for the tile's): re-define the
-      // Q fragments here, or the compiler -- unable to prove across the loop that their loads are
-      // done -- puts vmcnt(0) in front of the first QK^T MFMA, draining the next tile's prefetch
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) asm volatile("" : "+v"(qf[kk]));
-      __syncthreads();
-      if (kb + KB < kmax) pf.load(K, P.ldk, V, P.ldv, kb + KB, kmax);
-      PH_STAMP(3 + 2 * (kb / KB));
-      // a wave past the last query row, or whose rows all precede this key tile (causal), only
-      // helps stage K/V
-      if (w_row0 >= P.Tq || (P.causal && kb > w_row0 + 15)) continue;
-      f32x4 s[4];
-      tile_s(sK, s);
-      tile_pv(kb, sV, s);
+      for (int i = 0; i < NDT; ++i) o[i] = mfma(frag_tr<HD>(tV, 32 * c, 16 * i, lane), pf, o[i]);
     }
   }
   PH_STAMP(40);
