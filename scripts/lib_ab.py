@@ -29,7 +29,9 @@ for rep in range(reps):
         if p.returncode or not line:
             print(p.stdout[-2000:], p.stderr[-2000:])
             raise SystemExit(f"{name}: bench failed rc={p.returncode}")
-        ms = json.loads(line[-1])["ms_per_step"]
+        d = json.loads(line[-1])
+        ms, ck = d["ms_per_step"], d.get("optimizer", {}).get("master_checksum")
         res.setdefault(name, {}).setdefault("ms", []).append(ms)
-        print(f"{name:12s} rep {rep}: {ms:.3f} ms/step", flush=True)
+        res[name].setdefault("master_checksum", []).append(ck)
+        print(f"{name:12s} rep {rep}: {ms:.3f} ms/step  master checksum {ck!r}", flush=True)
 json.dump(res, open(out, "w"), indent=1)
