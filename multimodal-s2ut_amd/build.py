@@ -40,24 +40,29 @@ def _headers_mtime():
 
 
 def _compile(src, force=True):
+    """-> (object path, True if hipcc ran)"""
     obj = os.path.join(OBJDIR, src.replace(".hip", ".o"))
     if not force and os.path.exists(obj) and \
             os.path.getmtime(obj) >= max(os.path.getmtime(os.path.join(CSRC, src)), _headers_mtime()):
-        return obj      # object newer than its source and every header: reuse
+        return obj, False      # object newer than its source and every header: reuse
     cmd = [HIPCC, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
-    return obj
+    return obj, True
 
 
 def build(force=False, verbose=True):
     os.makedirs(OBJDIR, exist_ok=True)
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
-        return LIB
     srcs = _sources()
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
+        if verbose:   # one line either way, so a build check can tell a rebuild from an up-to-date tree
+            print(f"build: {LIB} up to date (newer than all {len(srcs)} csrc/*.hip sources, headers and "
+                  f"build.py); --force recompiles", file=sys.stderr)
+        return LIB
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda f: _compile(f, force), srcs))
+        res = list(ex.map(lambda f: _compile(f, force), srcs))
+    objs = [o for o, _ in res]
     tmp = LIB + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -65,7 +70,9 @@ def build(force=False, verbose=True):
         raise RuntimeError(f"link failed:\n{r.stderr}")
     os.replace(tmp, LIB)
     if verbose:
-        print(f"built {LIB}", file=sys.stderr)
+        done = [s for s, (_, ran) in zip(srcs, res) if ran]
+        print(f"build: hipcc --offload-arch={ARCH} compiled {len(done)} of {len(srcs)} sources "
+              f"({', '.join(done) or 'none'}), linked {LIB}", file=sys.stderr)
     return LIB
 
 
