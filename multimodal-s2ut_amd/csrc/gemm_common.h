@@ -329,12 +329,14 @@ constexpr bool epi_drops() {
          EPI == MMS_EPI_GELU_DROP_BWD;
 }
 
-// FR: 16-row fragments of the wave's tile in this pass (4 = 64 rows; 2 = 32 rows)
-template <int EPI, int FR = 4>
+// FR: 16-row fragments of the wave's tile in this pass (4 = 64 rows; 2 = 32 rows); SLOT: floats of
+// LDS between consecutive waves' staging areas (>= FR * 16 * 64)
+template <int EPI, int FR = 4, int SLOT = 64 * 64>
 MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4], int bm, int bn,
                              int wm, int wn, int wid, int lane, void* Cz, const h16* auxz) {
+  static_assert(SLOT >= FR * 16 * 64, "staging slot too small");
   constexpr int PASSES = FR * 2;   // 8 rows per pass
-  float* stage = reinterpret_cast<float*>(smem) + wid * 64 * 64;
+  float* stage = reinterpret_cast<float*>(smem) + wid * SLOT;
 #pragma unroll
   for (int i = 0; i < FR; ++i)
 #pragma unroll

@@ -231,6 +231,7 @@ static int run_variant(const Variant& v, const mms2ut_gemm_args& a, hipStream_t 
   if (v.kind == 4) return launch_tallp(a.epi, v.bm, v.var, P, s);
   if (v.kind == 5) return launch_persist(a.epi, v.bm, v.var, P, s);
   if (v.kind == 6) return mmst::launch_stag(a.epi, v.bm, v.var, P, s);
+  if (v.kind == 7) return mmst::launch_pf(a.epi, v.bm, P, s);
   return mmsw::launch_wide(a.epi, v.bm, v.var, P, s, v.kind == 3);
 }
 
@@ -257,11 +258,10 @@ int main(int argc, char** argv) {
   };
   std::vector<Variant> vars = {
       {"lib", 0, 0, 0},
-      {"st160", 6, 160, 0},
-      {"st160_noepi", 6, 160, 2000},
-      {"st160_raw", 6, 160, 3000},
       {"st192", 6, 192, 0},
-      {"st192_noepi", 6, 192, 2000},
+      {"pf192", 7, 192, 0},
+      {"st128", 6, 128, 0},
+      {"pf128", 7, 128, 0},
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
