@@ -116,6 +116,10 @@ int mms2ut_gemm_set_skinny(int mode);
  * ints, or NULL) receives each block's hardware XCD id (HW_REG_XCC_ID).  Bits are identical either
  * way.                                                                                         */
 int mms2ut_gemm_skinny_debug(int scatter, int* xcc_out);
+/* Test hook of the fused epilogues: staged != 0 routes every fp16 epilogue through the fp32 LDS
+ * staging (the round-5 form) instead of the register epilogue (plain / ReLU-dropout: element math
+ * in the MFMA layout, fp16 through LDS).  Bits are identical either way.                        */
+int mms2ut_gemm_set_epilogue(int staged);
 
 /* Grouped weight gradients of one transformer layer (torch.nn.Linear weight / bias grads of the
  * reference layer's projections): for each of the n <= 8 problems, dW[N, K] = dy[rows, N]^T @

@@ -143,6 +143,7 @@ SIGNATURES = {
     "mms2ut_gemm_set_tall": (i32, [i32]),
     "mms2ut_gemm_set_skinny": (i32, [i32]),
     "mms2ut_gemm_skinny_debug": (i32, [i32, vp]),
+    "mms2ut_gemm_set_epilogue": (i32, [i32]),
     "mms2ut_wgrad_group": (i32, [vp, i32, i64, i32, vp]),
     "mms2ut_wgrad_flush": (i32, [vp]),
     "mms2ut_profile_begin": (i32, [i32]),

@@ -409,6 +409,13 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
   // the wave's rows [bm + 16 FRT wm, + 16 FRT): fragments 0-3 (64 rows), then the rest, each
   // through the wave's 16 KiB staging area (staged_epilogue places wave rows at bm + 64 wm)
   constexpr int WR = 16 * FRT, F1 = FRT < 4 ? FRT : 4;
+  if constexpr (epi_regs<EPI>() && MMS_GEMM_REG_TALL) {   // all FRT fragments in one pass (fp16 slots: 2 KiB per fragment)
+    if (reg_epilogue_ok(P)) {
+      reg_epilogue<EPI, FRT, FRT * 2048>(P, smem, acc, bm + (WR - 64) * wm, bn, wm, wn, wid, lane, P.C, P.aux);
+      stamp_end(P.stamps, t_start);
+      return;
+    }
+  }
   staged_epilogue<EPI, F1>(P, smem, reinterpret_cast<const f32x4(&)[F1][4]>(acc[0]), bm + (WR - 64) * wm, bn, wm,
                            wn, wid, lane, P.C, P.aux);
   if constexpr (FRT > 4) {
@@ -741,6 +748,8 @@ int launch_skinny_t(int epi, const GemmP& P, int nsplit, float* part, int* ticke
 // (tile code, chunks per wave): 44 = 64x64 tiles (NLOC <= 2: 64 accumulator + 2 x 64 operand VGPRs
 // keep two blocks per CU), 24 = 32x64 and 22 = 32x32 (NLOC <= 3)
 struct SkinnyPlan { int code = 0, nloc = 0, nsplit = 1; };
+// test hook (mms2ut_gemm_set_epilogue): 1 = every epilogue through the fp32 staging (GemmP.vec16 = 3)
+int g_epi_staged = 0;
 // test hooks (mms2ut_gemm_skinny_debug): deal a tile's splits over different XCDs; record each
 // block's hardware XCD id
 int g_skinny_scatter = 0;
@@ -918,7 +927,7 @@ static int wgrad_group_dispatch(const mms2ut_wgrad* w, int n, int64_t rows, int 
     P.kchunk = (int)((rows + BK - 1) / BK * BK);
     if (P.kchunk == 0) P.kchunk = BK;
     P.alpha = 1.f;
-    P.vec16 = 1;
+    P.vec16 = g_epi_staged ? 3 : 1;
     P.rowsum16 = q.db;
     P.group_m = kGroupM;
     G.tiles_m[i] = (q.N + BM - 1) / BM;
@@ -1213,6 +1222,10 @@ extern "C" int mms2ut_gemm_skinny_debug(int scatter, int* xcc_out) {
   g_skinny_xcc = xcc_out;
   return 0;
 }
+extern "C" int mms2ut_gemm_set_epilogue(int staged) {
+  g_epi_staged = staged ? 1 : 0;
+  return 0;
+}
 extern "C" int mms2ut_gemm_set_skinny(int mode) {
   MMS_REQUIRE(mode >= 0 && mode <= 2, "gemm_set_skinny: mode must be 0, 1 or 2 (got %d)", mode);
   g_skinny_mode = mode;
@@ -1290,7 +1303,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
     if (a->aux) v = v && al16(a->aux) && a->ldaux % 8 == 0 && (a->epi != MMS_EPI_GATE || a->N % 8 == 0);
     if (a->out2) v = v && al16(a->out2) && a->ldo2 % 8 == 0;
     if (a->bias) v = v && al16(a->bias);
-    F.vec16 = v ? 1 : 0;
+    F.vec16 = v ? (g_epi_staged ? 3 : 1) : 0;
     F.stamps = stamp_take(((long)a->M * ((a->N + 7) / 8) + 255) / 256);
     return launch_fixup(a->epi, F, a->splitk_ws, splitk, stream);
   }
@@ -1316,7 +1329,7 @@ static int gemm_dispatch(const mms2ut_gemm_args* a, hipStream_t stream) {
                     (a->epi != MMS_EPI_GATE || a->N % 8 == 0);
     if (a->out2) v = v && al16(a->out2) && a->ldo2 % 8 == 0;
     if (a->bias) v = v && al16(a->bias);
-    P.vec16 = v ? 1 : 0;
+    P.vec16 = v ? (g_epi_staged ? 3 : 1) : 0;
   }
   if (splitk == 1 && skinny_eligible(a)) {
     const SkinnyPlan pl = skinny_plan(a, a->splitk_ws != nullptr);

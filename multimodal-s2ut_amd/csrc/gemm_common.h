@@ -20,7 +20,8 @@ struct GemmP {
   const h16* aux; long ldaux; long sX1, sX2;
   h16* out2; long ldo2;
   float p; uint32_t thresh; uint64_t seed, offset; long ld_rng;
-  int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity
+  int vec16;  // every fp16 row operand of the epilogue is 16-B aligned at 8-column granularity (3: and
+              // the fp32-staged epilogue forced, mms2ut_gemm_set_epilogue)
   float* rowsum; long ld_rowsum;  // RS kernels: split-K partial A-row sums (bias gradient)
   h16* rowsum16;                  // RS kernels, unsplit: the fp16 A-row sums (grouped wgrad)
   int group_m;  // tile-rows per L2 group (tile_coords)
@@ -329,12 +330,148 @@ constexpr bool epi_drops() {
          EPI == MMS_EPI_GELU_DROP_BWD;
 }
 
+// Register epilogue (round 6): for the epilogues whose element math needs no operand in row-major
+// order (plain / bias, ReLU-dropout) the math runs on the accumulators in the MFMA layout (lane l:
+// row 16 i + (l & 15), columns 16 j + 4 (l >> 4) .. + 3), the fp16 results go through the wave's own
+// LDS slot (FR x 16 rows x 128 B, half the bytes of the fp32 staging, one pass for up to 8 fragments)
+// and come back row-major for 16-B stores of whole 128-B row segments.  Same per-element arithmetic
+// and the same dropout counters as the staged path: bit-identical.  The slot is written and read by
+// one wave only, so no workgroup barrier sits between the two.
+#ifndef MMS_GEMM_REG_EPI
+#define MMS_GEMM_REG_EPI 1
+#endif
+#ifndef MMS_GEMM_REG_STAGED
+#define MMS_GEMM_REG_STAGED 1
+#endif
+#ifndef MMS_GEMM_REG_TALL
+#define MMS_GEMM_REG_TALL 1
+#endif
+template <int EPI>
+constexpr bool epi_regs() {
+  return (MMS_GEMM_REG_EPI && (EPI == MMS_EPI_F16 || EPI == MMS_EPI_RELU_DROP)) ||
+         (MMS_GEMM_REG_EPI >= 2 && (EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_RELU_DROP_BWD || EPI == MMS_EPI_F16_ACC));
+}
+
+// The choice between this and the staged path must be the same for every wave of a block: the two
+// lay their LDS slots out differently (the tall kernel packs the fp16 slots) and the staged path
+// holds workgroup barriers.  N % 64 == 0 makes every wave's 64 columns lie wholly inside N or wholly
+// outside it (such a wave has nothing to do).
+MMS_DEV bool reg_epilogue_ok(const GemmP& P) { return P.vec16 == 1 && P.N % 64 == 0; }   // 3: staged (test hook)
+
+// rows bm + 64 wm + 16 i + (l & 15), columns bn + 64 wn ..+ 64 (caller: reg_epilogue_ok(P));
+// SLOTB: bytes between consecutive waves' slots (>= FR * 2048)
+template <int EPI, int FR, int SLOTB>
+MMS_DEV void reg_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4], int bm, int bn, int wm, int wn,
+                          int wid, int lane, void* Cz, const h16* auxz) {
+  static_assert(SLOTB >= FR * 2048, "staging slot too small");
+  if (bn + wn * 64 >= P.N) return;   // wave-uniform: all 64 columns past N
+  char* stage = smem + wid * SLOTB;
+  const int rl = lane & 15, g = lane >> 4;
+  const int m0 = bm + wm * 64 + rl, nw = bn + wn * 64 + 4 * g;
+  // row operand (residual / pre-activation / existing C) at the accumulators' own positions: 8-B
+  // loads, all issued before the element math; rows past M read as zero
+  constexpr bool AUXL = EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_RELU_DROP_BWD || EPI == MMS_EPI_F16_ACC;
+  h16x4 ax[AUXL ? FR : 1][4];
+  if constexpr (AUXL) {
+    const h16* src = EPI == MMS_EPI_F16_ACC ? reinterpret_cast<const h16*>(Cz) : auxz;
+    const long ld = EPI == MMS_EPI_F16_ACC ? P.ldc : P.ldaux;
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ax[i][j] = h16x4{(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
+        if (m0 + 16 * i < P.M) ax[i][j] = *reinterpret_cast<const h16x4*>(src + (long)(m0 + 16 * i) * ld + nw + 16 * j);
+      }
+  }
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[j][e] = 0.f;
+  if (EPI != MMS_EPI_RELU_DROP_BWD && P.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const h16x4 b4 = *reinterpret_cast<const h16x4*>(P.bias + nw + 16 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[j][e] = (float)b4[e];
+    }
+  }
+  constexpr bool DROPS = EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID;
+  const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
+  uint32_t hmix = 0, pbase = 0;
+  bool fast = false;
+  if (DROPS && P.thresh) {
+    const uint64_t cf = P.offset + (uint64_t)m0 * P.ld_rng + nw;
+    const uint64_t cl = P.offset + (uint64_t)(m0 + 16 * (FR - 1)) * P.ld_rng + nw + 51;
+    const bool sh = mms_same_hi(cf, cl) && ((cf & 1) == 0) && ((P.ld_rng & 1) == 0);
+    hmix = mms_hi_mix(P.seed, cf);
+    pbase = (uint32_t)(cf >> 1);
+    fast = __all(sh);
+  }
+#pragma unroll
+  for (int i = 0; i < FR; ++i) {
+    const int rr = i * 16 + rl;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = acc[i][j][e] * P.alpha + bv[j][e];
+      bool keep[4] = {true, true, true, true};
+      if (DROPS && P.thresh && fast) {
+        // pair index of counter offset + (m0 + 16 i) ld_rng + nw + 16 j (ld_rng even)
+        const uint32_t p0 = pbase + (uint32_t)(8 * i) * (uint32_t)P.ld_rng + 8 * j;
+        const uint32_t h0 = mms_mix32(p0 ^ hmix), h1 = mms_mix32((p0 + 1) ^ hmix);
+        keep[0] = (h0 & 0xffffU) >= P.thresh;
+        keep[1] = (h0 >> 16) >= P.thresh;
+        keep[2] = (h1 & 0xffffU) >= P.thresh;
+        keep[3] = (h1 >> 16) >= P.thresh;
+      } else if (DROPS && P.thresh) {
+        mms_keep4(P.seed, P.offset + (uint64_t)(m0 + 16 * i) * P.ld_rng + nw + 16 * j, P.thresh, keep);
+      }
+      h16x4 o4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float o;
+        if (EPI == MMS_EPI_RELU_DROP) o = keep[e] ? fmaxf(x[e], 0.f) * dscale : 0.f;
+        else if (EPI == MMS_EPI_DROP_RESID) o = (float)ax[AUXL ? i : 0][j][e] + (keep[e] ? x[e] * dscale : 0.f);
+        else if (EPI == MMS_EPI_RELU_DROP_BWD) o = (float)ax[AUXL ? i : 0][j][e] > 0.f ? x[e] * dscale : 0.f;
+        else if (EPI == MMS_EPI_F16_ACC) o = (float)ax[AUXL ? i : 0][j][e] + x[e];
+        else o = x[e];
+        o4[e] = (h16)o;
+      }
+      // 16-B chunk 2 j + (g >> 1) of row rr, half g & 1; chunks XOR-swizzled by (rr >> 1) & 7:
+      // conflict-free for ds_write_b64's 16-lane groups and ds_read_b128's lane groups
+      const int ch = (2 * j + (g >> 1)) ^ ((rr >> 1) & 7);
+      *reinterpret_cast<h16x4*>(stage + rr * 128 + (ch << 4) + (g & 1) * 8) = o4;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int q = lane & 7;
+  h16* C = reinterpret_cast<h16*>(Cz);
+  const int n = bn + wn * 64 + 8 * q;
+#pragma unroll
+  for (int pass = 0; pass < 2 * FR; ++pass) {
+    const int rr = pass * 8 + (lane >> 3);
+    const h16x8 v = *reinterpret_cast<const h16x8*>(stage + rr * 128 + ((q ^ ((rr >> 1) & 7)) << 4));
+    const int m = bm + wm * 64 + rr;
+    if (m < P.M) *reinterpret_cast<h16x8*>(C + (long)m * P.ldc + n) = v;
+  }
+}
+
 // FR: 16-row fragments of the wave's tile in this pass (4 = 64 rows; 2 = 32 rows); SLOT: floats of
 // LDS between consecutive waves' staging areas (>= FR * 16 * 64)
 template <int EPI, int FR = 4, int SLOT = 64 * 64>
 MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4], int bm, int bn,
                              int wm, int wn, int wid, int lane, void* Cz, const h16* auxz) {
   static_assert(SLOT >= FR * 16 * 64, "staging slot too small");
+  if constexpr (epi_regs<EPI>() && MMS_GEMM_REG_STAGED) {
+    if (reg_epilogue_ok(P)) {   // launch-uniform: every wave of the block takes the same path
+      reg_epilogue<EPI, FR, SLOT * 4>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+      return;
+    }
+  }
   constexpr int PASSES = FR * 2;   // 8 rows per pass
   float* stage = reinterpret_cast<float*>(smem) + wid * SLOT;
 #pragma unroll
