@@ -411,7 +411,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_tall_kernel(GemmP P, int tiles_m, 
   constexpr int WR = 16 * FRT, F1 = FRT < 4 ? FRT : 4;
   if constexpr (epi_regs<EPI>() && MMS_GEMM_REG_TALL) {   // all FRT fragments in one pass (fp16 slots: 2 KiB per fragment)
     if (reg_epilogue_ok(P)) {
-      reg_epilogue<EPI, FRT, FRT * 2048>(P, smem, acc, bm + (WR - 64) * wm, bn, wm, wn, wid, lane, P.C, P.aux);
+      reg_epilogue<EPI, FRT, FRT * 2048>(P, smem, acc, bm + (WR - 64) * wm, bn, wm, wn, wid, lane, P.C);
       stamp_end(P.stamps, t_start);
       return;
     }

@@ -348,8 +348,7 @@ constexpr bool epi_drops() {
 #endif
 template <int EPI>
 constexpr bool epi_regs() {
-  return (MMS_GEMM_REG_EPI && (EPI == MMS_EPI_F16 || EPI == MMS_EPI_RELU_DROP)) ||
-         (MMS_GEMM_REG_EPI >= 2 && (EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_RELU_DROP_BWD || EPI == MMS_EPI_F16_ACC));
+  return MMS_GEMM_REG_EPI && (EPI == MMS_EPI_F16 || EPI == MMS_EPI_RELU_DROP);
 }
 
 // The choice between this and the staged path must be the same for every wave of a block: the two
@@ -362,33 +361,18 @@ MMS_DEV bool reg_epilogue_ok(const GemmP& P) { return P.vec16 == 1 && P.N % 64 =
 // SLOTB: bytes between consecutive waves' slots (>= FR * 2048)
 template <int EPI, int FR, int SLOTB>
 MMS_DEV void reg_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4], int bm, int bn, int wm, int wn,
-                          int wid, int lane, void* Cz, const h16* auxz) {
+                          int wid, int lane, void* Cz) {
   static_assert(SLOTB >= FR * 2048, "staging slot too small");
   if (bn + wn * 64 >= P.N) return;   // wave-uniform: all 64 columns past N
   char* stage = smem + wid * SLOTB;
   const int rl = lane & 15, g = lane >> 4;
   const int m0 = bm + wm * 64 + rl, nw = bn + wn * 64 + 4 * g;
-  // row operand (residual / pre-activation / existing C) at the accumulators' own positions: 8-B
-  // loads, all issued before the element math; rows past M read as zero
-  constexpr bool AUXL = EPI == MMS_EPI_DROP_RESID || EPI == MMS_EPI_RELU_DROP_BWD || EPI == MMS_EPI_F16_ACC;
-  h16x4 ax[AUXL ? FR : 1][4];
-  if constexpr (AUXL) {
-    const h16* src = EPI == MMS_EPI_F16_ACC ? reinterpret_cast<const h16*>(Cz) : auxz;
-    const long ld = EPI == MMS_EPI_F16_ACC ? P.ldc : P.ldaux;
-#pragma unroll
-    for (int i = 0; i < FR; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ax[i][j] = h16x4{(h16)0.f, (h16)0.f, (h16)0.f, (h16)0.f};
-        if (m0 + 16 * i < P.M) ax[i][j] = *reinterpret_cast<const h16x4*>(src + (long)(m0 + 16 * i) * ld + nw + 16 * j);
-      }
-  }
   float bv[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[j][e] = 0.f;
-  if (EPI != MMS_EPI_RELU_DROP_BWD && P.bias) {
+  if (P.bias) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const h16x4 b4 = *reinterpret_cast<const h16x4*>(P.bias + nw + 16 * j);
@@ -396,7 +380,7 @@ MMS_DEV void reg_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4],
       for (int e = 0; e < 4; ++e) bv[j][e] = (float)b4[e];
     }
   }
-  constexpr bool DROPS = EPI == MMS_EPI_RELU_DROP || EPI == MMS_EPI_DROP_RESID;
+  constexpr bool DROPS = EPI == MMS_EPI_RELU_DROP;
   const float dscale = P.thresh ? 1.f / (1.f - P.p) : 1.f;
   uint32_t hmix = 0, pbase = 0;
   bool fast = false;
@@ -433,9 +417,6 @@ MMS_DEV void reg_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4],
       for (int e = 0; e < 4; ++e) {
         float o;
         if (EPI == MMS_EPI_RELU_DROP) o = keep[e] ? fmaxf(x[e], 0.f) * dscale : 0.f;
-        else if (EPI == MMS_EPI_DROP_RESID) o = (float)ax[AUXL ? i : 0][j][e] + (keep[e] ? x[e] * dscale : 0.f);
-        else if (EPI == MMS_EPI_RELU_DROP_BWD) o = (float)ax[AUXL ? i : 0][j][e] > 0.f ? x[e] * dscale : 0.f;
-        else if (EPI == MMS_EPI_F16_ACC) o = (float)ax[AUXL ? i : 0][j][e] + x[e];
         else o = x[e];
         o4[e] = (h16)o;
       }
@@ -468,7 +449,7 @@ MMS_DEV void staged_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][
   static_assert(SLOT >= FR * 16 * 64, "staging slot too small");
   if constexpr (epi_regs<EPI>() && MMS_GEMM_REG_STAGED) {
     if (reg_epilogue_ok(P)) {   // launch-uniform: every wave of the block takes the same path
-      reg_epilogue<EPI, FR, SLOT * 4>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz, auxz);
+      reg_epilogue<EPI, FR, SLOT * 4>(P, smem, acc, bm, bn, wm, wn, wid, lane, Cz);
       return;
     }
   }
