@@ -5,7 +5,8 @@ tiles (96 / 160 / 192 rows), the 128x128 LDS-DMA and register-staged kernels, th
 batched attention products (alpha != 1) and the grouped weight gradients.  Also the launch-uniform
 path choice: N = 1004 (the unit vocabulary, padded ldc 1024) takes the staged path in every wave —
 a per-wave choice there mixed the two LDS slot layouts inside one block (round 6), which only a
-repeated run exposes, so every case runs several times.  Dropout streams as the step uses them: large
+repeated run exposes, so every case runs several times; N = 320 / 192 leave a block's second
+64-column half past N (that wave returns early).  Dropout streams as the step uses them: large
 and odd counter offsets, seeds per site."""
 import pytest
 import torch
@@ -40,7 +41,8 @@ def _both(K_, fn, reps=3):
 
 
 @pytest.mark.parametrize("M,N,Kd", [(9607, 3072, 768), (11003, 768, 768), (7589, 2304, 768), (12000, 768, 3072),
-                                    (2000, 768, 768), (3011, 1004, 768), (777, 3072, 768), (131, 768, 768)])
+                                    (2000, 768, 768), (3011, 1004, 768), (777, 3072, 768), (131, 768, 768),
+                                    (1500, 320, 768), (9, 192, 256)])
 def test_linear_epilogues_bit_identical(K_, M, N, Kd):
     g = torch.Generator(device="cuda").manual_seed(M + N + Kd)
     x = (torch.randn(M, Kd, device="cuda", generator=g) * 0.5).half()
