@@ -420,10 +420,11 @@ MMS_DEV void reg_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4],
         else o = x[e];
         o4[e] = (h16)o;
       }
-      // 16-B chunk 2 j + (g >> 1) of row rr, half g & 1; chunks XOR-swizzled by (rr >> 1) & 7:
-      // conflict-free for ds_write_b64's 16-lane groups and ds_read_b128's lane groups
+      // 16-B chunk 2 j + (g >> 1) of row rr, 8-B half g & 1; chunks XOR-swizzled by (rr >> 1) & 7 and
+      // halves by rr & 1: a ds_write_b64 16-lane group (16 rows, one (j, g)) covers the 32 write banks
+      // once, ds_read_b128's lane groups read distinct chunks (PMC: SQ_LDS_BANK_CONFLICT 0)
       const int ch = (2 * j + (g >> 1)) ^ ((rr >> 1) & 7);
-      *reinterpret_cast<h16x4*>(stage + rr * 128 + (ch << 4) + (g & 1) * 8) = o4;
+      *reinterpret_cast<h16x4*>(stage + rr * 128 + (ch << 4) + (((g ^ rr) & 1) << 3)) = o4;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -435,9 +436,11 @@ MMS_DEV void reg_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4],
 #pragma unroll
   for (int pass = 0; pass < 2 * FR; ++pass) {
     const int rr = pass * 8 + (lane >> 3);
-    const h16x8 v = *reinterpret_cast<const h16x8*>(stage + rr * 128 + ((q ^ ((rr >> 1) & 7)) << 4));
+    typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+    u32x4_ v = *reinterpret_cast<const u32x4_*>(stage + rr * 128 + ((q ^ ((rr >> 1) & 7)) << 4));
+    if (rr & 1) v = u32x4_{v[2], v[3], v[0], v[1]};   // odd rows store their two halves swapped
     const int m = bm + wm * 64 + rr;
-    if (m < P.M) *reinterpret_cast<h16x8*>(C + (long)m * P.ldc + n) = v;
+    if (m < P.M) *reinterpret_cast<u32x4_*>(C + (long)m * P.ldc + n) = v;
   }
 }
 
