@@ -427,9 +427,11 @@ MMS_DEV void reg_epilogue(const GemmP& P, char* smem, const f32x4 (&acc)[FR][4],
       *reinterpret_cast<h16x4*>(stage + rr * 128 + (ch << 4) + (((g ^ rr) & 1) << 3)) = o4;
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // the slot is re-read by other lanes of this wave: drain its LDS writes first (DS operations of a
+  // wave complete in order, the wait makes that explicit at the cost of one short stall)
+  // (same-box A/B with / without the wait: step 15.58-15.60 vs 15.57-15.66 ms, profiles/round6_reg_epilogue_drain_ab.txt)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int q = lane & 7;
   h16* C = reinterpret_cast<h16*>(Cz);
   const int n = bn + wn * 64 + 8 * q;
